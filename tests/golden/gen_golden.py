@@ -1,0 +1,235 @@
+"""Generate the golden fixtures in tests/golden/*.npz by running the REFERENCE itself.
+
+CONTAINER-ONLY (needs /root/reference, which never travels to the GPU box).  Re-run with
+    python tests/golden/gen_golden.py
+It imports the reference's own `network.py`, `utilities.py`, `vgg19.py`, `lossfn.py` and
+executes the reference's own `train_candy.train()` / `train_video.train()` loop bodies with:
+  * `tests/golden/_stubs` ahead on sys.path: architecture-only torchvision VGG (no weight
+    download is possible offline) and an empty cv2 (absent in this image);
+  * seeded weights from `oracle/seeding.py` (numpy PCG64) loaded after construction;
+  * a one-batch in-memory loader instead of the disk datasets, a tqdm recorder to capture the
+    loss postfix, an Adam subclass that records gradients at step(), and torch.save disabled.
+Nothing from the reference is copied into the repo: only inputs/outputs (data) are saved.
+"""
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+RC_DIR = os.path.join(REF, "Real-time-Coherent-Video-Style-Transfer-Network-(ReCoNet)")
+AA_DIR = os.path.join(REF, "Revisit-Attention-Mechanism-in-Arbitrary-Neural-Style-Transfer-(AdaAttN)")
+
+sys.path.insert(0, os.path.join(HERE, "_stubs"))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "video-style-transfer_amd"))
+
+from oracle.seeding import seed_module  # noqa: E402
+from vst.synthetic import frame_pair_batch, style_image  # noqa: E402
+
+torch.set_num_threads(8)
+f32 = np.float32
+
+
+def _fresh_project(path, names=("network", "utilities", "datasets", "flowlib", "vgg19", "lossfn")):
+    for n in names:
+        sys.modules.pop(n, None)
+    while path in sys.path:
+        sys.path.remove(path)
+    sys.path.insert(0, path)
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _np(t):
+    return t.detach().cpu().numpy().astype(f32)
+
+
+class _TqdmRecorder:
+    records = []
+
+    def __init__(self, it, **_):
+        self.it = it
+
+    def __iter__(self):
+        return iter(self.it)
+
+    def set_postfix(self, d):
+        _TqdmRecorder.records.append(dict(d))
+
+
+def _make_recording_adam(named):
+    id2name = {id(p): n for n, p in named}
+
+    class RecordingAdam(torch.optim.Adam):
+        grads = {}
+        after = {}
+
+        def step(self, closure=None):
+            for g in self.param_groups:
+                for p in g["params"]:
+                    RecordingAdam.grads[id2name[id(p)]] = p.grad.detach().clone()
+            r = super().step(closure)
+            for g in self.param_groups:
+                for p in g["params"]:
+                    RecordingAdam.after[id2name[id(p)]] = p.detach().clone()
+            return r
+
+    return RecordingAdam
+
+
+def _grad_summary(prefix, grads, after, out, seed):
+    """Per-tensor: L2 norm, first 64 values, 256 seeded random-index samples; post-step slices."""
+    rng = np.random.default_rng(seed)
+    names = sorted(grads)
+    out[prefix + "names"] = np.array(names)
+    for n in names:
+        g = grads[n].reshape(-1).double()
+        out[f"{prefix}gnorm/{n}"] = np.array(float(g.norm()))
+        out[f"{prefix}ghead/{n}"] = _np(g[:64])
+        idx = rng.integers(0, g.numel(), size=min(256, g.numel()))
+        out[f"{prefix}gidx/{n}"] = idx.astype(np.int64)
+        out[f"{prefix}gval/{n}"] = _np(g[idx])
+        out[f"{prefix}phead/{n}"] = _np(after[n].reshape(-1)[:64])
+
+
+# --------------------------------------------------------------------------------------------
+# ReCoNet (RC/)
+# --------------------------------------------------------------------------------------------
+def gen_reconet():
+    _fresh_project(RC_DIR)
+    rc_util = _load("utilities", os.path.join(RC_DIR, "utilities.py"))
+    sys.modules["utilities"] = rc_util
+    rc_net = _load("network", os.path.join(RC_DIR, "network.py"))
+    sys.modules["network"] = rc_net
+
+    units = {}
+    rng = np.random.default_rng(100)
+    # warp (RC/utilities.py:39-57): random content + flows reaching out of bounds
+    for tag, shp, amp in (("img", (2, 3, 8, 12), 4.0), ("feat", (2, 5, 9, 15), 3.0), ("wide", (1, 2, 5, 40), 12.0)):
+        x = torch.from_numpy(rng.standard_normal(shp).astype(f32))
+        flo = torch.from_numpy(rng.uniform(-amp, amp, (shp[0], 2, shp[2], shp[3])).astype(f32))
+        units[f"warp_{tag}_x"], units[f"warp_{tag}_flo"] = _np(x), _np(flo)
+        units[f"warp_{tag}_out"] = _np(rc_util.warp(x, flo.clone()))
+    # known answer: zero flow is NOT the identity (align_corners=False vs /(W-1) normalisation)
+    ramp = torch.arange(24, dtype=torch.float32).view(1, 1, 4, 6)
+    units["warp_ramp_x"] = _np(ramp)
+    units["warp_ramp_out"] = _np(rc_util.warp(ramp, torch.zeros(1, 2, 4, 6)))
+    # flow_warp_mask (RC/utilities.py:60-90)
+    for i in range(3):
+        H, W = (16, 24) if i < 2 else (7, 33)
+        f01 = torch.from_numpy(rng.uniform(-3, 3, (2, H, W)).astype(f32))
+        f10 = -f01 + torch.from_numpy(rng.uniform(-1.5, 1.5, (2, H, W)).astype(f32))
+        units[f"fwm{i}_f01"], units[f"fwm{i}_f10"] = _np(f01), _np(f10)
+        units[f"fwm{i}_mask"] = _np(rc_util.flow_warp_mask(f01.clone(), f10.clone()))
+    # gram_matrix (RC/utilities.py:93-98)
+    y = torch.from_numpy(rng.standard_normal((2, 4, 5, 7)).astype(f32))
+    units["gram_y"], units["gram_out"] = _np(y), _np(rc_util.gram_matrix(y))
+    units["gram_ones_out"] = _np(rc_util.gram_matrix(torch.ones(1, 2, 3, 3)))
+    # vgg_normalize (RC/utilities.py:101-106): returns normalised AND mutates input to x/255
+    x = torch.from_numpy(rng.uniform(0, 255, (2, 3, 4, 5)).astype(f32))
+    units["vggn_x"] = _np(x)
+    out = rc_util.vgg_normalize(x)
+    units["vggn_out"], units["vggn_x_after"] = _np(out), _np(x)
+    np.savez_compressed(os.path.join(HERE, "rc_units.npz"), **units)
+
+    # forward fixtures
+    fwd = {}
+    with torch.no_grad():
+        m = rc_net.ReCoNet()
+        seed_module(m, 1)
+        for tag, seed, shp in (("a", 2, (2, 3, 32, 64)), ("ragged", 3, (1, 3, 36, 60))):
+            x = torch.from_numpy(np.random.default_rng(seed).uniform(0, 255, shp).astype(f32))
+            sd1, feat, out = m(x)
+            fwd[f"reconet_{tag}_x"], fwd[f"reconet_{tag}_sd1"] = _np(x), _np(sd1)
+            fwd[f"reconet_{tag}_features"], fwd[f"reconet_{tag}_out"] = _np(feat), _np(out)
+        v = rc_net.Vgg16()
+        seed_module(v, 4)
+        x = torch.from_numpy(np.random.default_rng(5).standard_normal((2, 3, 32, 64)).astype(f32))
+        feats = v(x)
+        fwd["vgg16_x"] = _np(x)
+        for name in feats._fields:
+            fwd[f"vgg16_{name}"] = _np(getattr(feats, name))
+        # real trained checkpoints shipped with the reference (weights_only load)
+        x = torch.from_numpy(np.random.default_rng(6).uniform(0, 255, (1, 3, 32, 64)).astype(f32))
+        fwd["sd_x"] = _np(x)
+        for cls, fn in ((rc_net.ReCoNetSD1, "SD1_epoch_4_batchSize_2.pth"), (rc_net.ReCoNetSD2, "SD2_epoch_4_batchSize_2.pth")):
+            net = cls()
+            net.load_state_dict(torch.load(os.path.join(RC_DIR, "models_old", fn), weights_only=True, map_location="cpu"))
+            for i, o in enumerate(net(x)):
+                fwd[f"{cls.__name__}_out{i}"] = _np(o)
+    np.savez_compressed(os.path.join(HERE, "rc_fwd.npz"), **fwd)
+
+    # full training step through the reference's own train_candy.train()
+    step = {}
+    for tag, (B, H, W, seeds) in {"b2": (2, 32, 64, (11, 12, 13, 14)), "b1r": (1, 36, 60, (21, 22, 23, 24))}.items():
+        fake_ds = types.ModuleType("datasets")
+        fake_ds.FlyingThings3D_Monkaa = lambda *a, **k: None
+        style = style_image(seeds[3], H, W)
+        fake_ds.toTensor255 = lambda _img, _s=style: _s[0].clone()
+        sys.modules["datasets"] = fake_ds
+        tc = _load(f"rc_train_candy_{tag}", os.path.join(RC_DIR, "train_single", "train_candy.py"))
+
+        img1, img2, flow, mask = frame_pair_batch(seeds[2], B, H, W, mask_fn=rc_util.flow_warp_mask)
+        holder = {}
+
+        def reconet_factory(n=1, _h=holder, _s=seeds[0]):
+            net = rc_net.ReCoNet(n)
+            seed_module(net, _s)
+            _h["model"] = net
+            tc.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(net.named_parameters())))
+            return net
+
+        def vgg_factory(device="cpu", _s=seeds[1]):
+            v = rc_net.Vgg16(device)
+            seed_module(v, _s)
+            return v
+
+        class _Img:
+            BILINEAR = 2
+
+            @staticmethod
+            def open(_p):
+                class _O:
+                    def convert(self, *_):
+                        return self
+
+                    def resize(self, *_):
+                        return self
+
+                return _O()
+
+        tc.device, tc.batch_size, tc.IMG_SIZE, tc.epoch_start, tc.epoch_end = "cpu", B, (W, H), 1, 1
+        tc.DataLoader = lambda *a, **k: [(img1.clone(), img2.clone(), flow.clone(), mask.clone())]
+        tc.ReCoNet, tc.Vgg16, tc.Image, tc.tqdm = reconet_factory, vgg_factory, _Img, _TqdmRecorder
+        _TqdmRecorder.records = []
+        save = torch.save
+        torch.save = lambda *a, **k: None
+        try:
+            tc.train()
+        finally:
+            torch.save = save
+        rec = _TqdmRecorder.records[-1]
+        step[f"{tag}_img1"], step[f"{tag}_img2"] = _np(img1), _np(img2)
+        step[f"{tag}_flow"], step[f"{tag}_mask"], step[f"{tag}_style"] = _np(flow), _np(mask), _np(style)
+        step[f"{tag}_seeds"] = np.array(seeds)
+        for k in ("loss", "CL", "SL", "FTL", "OTL", "RL"):
+            step[f"{tag}_{k}"] = np.array(rec[k], dtype=np.float64)
+        adam = tc.optim.Adam
+        _grad_summary(f"{tag}_", adam.grads, adam.after, step, seed=seeds[0] + 1000)
+    np.savez_compressed(os.path.join(HERE, "rc_step.npz"), **step)
+    print("reconet fixtures written")
+
+
+if __name__ == "__main__":
+    gen_reconet()

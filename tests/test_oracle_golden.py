@@ -1,0 +1,95 @@
+"""Pin the oracle (CPU restatement) against golden vectors produced by the reference itself.
+
+Tolerance: 1e-4 relative to the tensor's max magnitude for forward tensors (both sides are
+fp32 torch-CPU; the restatement reorders a few ops), 1e-3 for losses and gradients.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import reconet_ref as R
+from oracle import shapes
+
+from conftest import rel_err
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def test_known_answers():
+    # gram_matrix(ones(1,2,3,3)) == 0.5 everywhere (RC/utilities.py:93-98)
+    g = R.gram_matrix(torch.ones(1, 2, 3, 3))
+    assert torch.allclose(g, torch.full_like(g, 0.5))
+    # vgg_normalize mutates its argument to x/255 (RC/utilities.py:105)
+    x = torch.full((1, 3, 2, 2), 255.0)
+    out = R.vgg_normalize_(x)
+    assert torch.allclose(x, torch.ones_like(x))
+    assert torch.allclose(out[0, :, 0, 0], (1 - torch.tensor(R.IMAGENET_MEAN)) / torch.tensor(R.IMAGENET_STD))
+
+
+def test_units(golden):
+    u = golden("rc_units")
+    for tag in ("img", "feat", "wide", "ramp"):
+        flo = u.get(f"warp_{tag}_flo")
+        x = T(u[f"warp_{tag}_x"])
+        flo = T(flo) if flo is not None else torch.zeros(x.shape[0], 2, *x.shape[2:])
+        assert rel_err(R.warp(x, flo), u[f"warp_{tag}_out"]) < 1e-5, tag
+    # zero flow is not the identity for this warp
+    assert np.abs(u["warp_ramp_out"] - u["warp_ramp_x"]).max() > 1.0
+    for i in range(3):
+        m = R.flow_warp_mask(T(u[f"fwm{i}_f01"]), T(u[f"fwm{i}_f10"]))
+        assert np.array_equal(m.numpy(), u[f"fwm{i}_mask"]), i
+    assert rel_err(R.gram_matrix(T(u["gram_y"])), u["gram_out"]) < 1e-6
+    x = T(u["vggn_x"]).clone()
+    out = R.vgg_normalize_(x)
+    assert rel_err(out, u["vggn_out"]) < 1e-6 and rel_err(x, u["vggn_x_after"]) < 1e-7
+
+
+def test_forward(golden):
+    f = golden("rc_fwd")
+    P = oracle.seeded_params(shapes.reconet(), 1)
+    with torch.no_grad():
+        for tag in ("a", "ragged"):
+            sd1, feat, out = R.reconet_forward(P, T(f[f"reconet_{tag}_x"]))
+            assert rel_err(sd1, f[f"reconet_{tag}_sd1"]) < 1e-4
+            assert rel_err(feat, f[f"reconet_{tag}_features"]) < 1e-4
+            assert rel_err(out, f[f"reconet_{tag}_out"]) < 1e-4
+        VP = oracle.seeded_params(shapes.vgg16(), 4)
+        outs = R.vgg_forward(VP, T(f["vgg16_x"]), R.VGG16_PLAN)
+        for o, name in zip(outs, ("relu1_2", "relu2_2", "relu3_3", "relu4_3")):
+            assert rel_err(o, f["vgg16_" + name]) < 1e-4, name
+
+
+@pytest.mark.parametrize("tag", ["b2", "b1r"])
+def test_train_step(golden, tag):
+    s = golden("rc_step")
+    seeds = s[f"{tag}_seeds"]
+    P = oracle.seeded_params(shapes.reconet(), int(seeds[0]), requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg16(), int(seeds[1]))
+    grams = R.style_grams(VP, T(s[f"{tag}_style"]))
+    L = R.reconet_losses(P, VP, T(s[f"{tag}_img1"]).clone(), T(s[f"{tag}_img2"]).clone(),
+                         T(s[f"{tag}_flow"]), T(s[f"{tag}_mask"]), grams)
+    for k in ("loss", "CL", "SL", "FTL", "OTL", "RL"):
+        assert rel_err(L[k].item(), s[f"{tag}_{k}"]) < 1e-3, k
+    L["loss"].backward()
+    names = list(s[f"{tag}_names"])
+    assert sorted(names) == sorted(P)
+    gmax = max(float(s[f"{tag}_gnorm/{n}"]) for n in names)
+    state = {}
+    grads = {n: P[n].grad for n in names}
+    params = {n: P[n].detach().clone() for n in names}
+    R.adam_step(params, grads, state)
+    for n in names:
+        g = P[n].grad
+        gn = float(s[f"{tag}_gnorm/{n}"])
+        # each tensor: norm within 1e-3 relative (or 1e-4 of the largest gradient norm)
+        assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"{tag}_gidx/{n}"]
+        assert np.abs(g.reshape(-1)[idx].numpy() - s[f"{tag}_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+        # Adam's first step is ~ -lr*sign(g): compare where the gradient is not round-off noise
+        # (conv biases feeding InstanceNorm have mathematically zero gradient)
+        gh = s[f"{tag}_ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        assert np.abs(params[n].reshape(-1)[:64].numpy() - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
