@@ -1,0 +1,173 @@
+"""Benchmark: ReCoNet training frame-pairs/s at 256x512 on MI355X (BASELINE.json metric).
+
+Workload (one "step"): the reference `train_candy` loop body (RC/train_single/train_candy.py:77-152)
+on one batch of B synthetic frame pairs per GPU, 3x256x512, precomputed flow + occlusion mask,
+full loss (FTL + OTL + content + Gram style + TV) through the Vgg16 loss network, backward and
+Adam — config 3 of BASELINE.json (`--config 2` drops the temporal terms).  Random-init weights
+(no checkpoint download offline), synthetic data already resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL all-reduce)
+
+Prints ONE JSON line (rank 0).  `roofline` = the dominant kernel family (conv_gemm_kernel: conv
+forward + data-gradient implicit GEMM on fp32 MFMA), algorithmic FLOPs / HIP-event-timed launch
+time inside the timed region vs the 157.3 TFLOP/s fp32 MFMA peak.  `cpu_baseline` = the oracle
+(CPU restatement of the same step, oracle/reconet_ref.py) on a bounded sample, rank 0 at N=1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "video-style-transfer_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="frame pairs per GPU")
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (CPU restatement of the reference step) on a bounded sample: B=1 pair at full size."""
+    import oracle
+    from oracle import reconet_ref as R
+    from oracle import shapes
+    from vst.synthetic import frame_pair_batch, style_image
+
+    torch.set_num_threads(args.cpu_threads)
+    H, W = args.height, args.width
+    P = oracle.seeded_params(shapes.reconet(), 1, requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg16(), 2)
+    grams = R.style_grams(VP, style_image(3, H, W))
+    img1, img2, flow, mask = frame_pair_batch(1234, 1, H, W, mask_fn=R.flow_warp_mask)
+    state = {}
+
+    def one():
+        L = R.reconet_losses(P, VP, img1.clone(), img2.clone(), flow, mask, grams, temporal=args.config == 3)
+        for p in P.values():
+            p.grad = None
+        L["loss"].backward()
+        with torch.no_grad():
+            R.adam_step({k: p for k, p in P.items()}, {k: p.grad for k, p in P.items()}, state)
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        one()
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {"value": 1.0 / dt, "unit": "frame-pairs/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of B=1 synthetic 3x{H}x{W} frame pair, "
+                      f"config {args.config}, oracle/reconet_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from vst import kprof, ops
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+    from vst.synthetic import frame_pair_batch, style_image
+
+    torch.manual_seed(0)  # identical random-init replicas on every rank
+    model = N.ReCoNet().to(dev)
+    vgg = N.Vgg16().to(dev)
+    B, H, W = args.batch, args.height, args.width
+    style = style_image(7, H, W).to(dev)
+    trainer = ReCoNetTrainer(model, vgg, style, temporal=args.config == 3)
+
+    def hip_mask(f01, f10):
+        return ops.flow_warp_mask(f01.to(dev), f10.to(dev))
+
+    img1, img2, flow, mask = frame_pair_batch(1234 + rank, B, H, W, mask_fn=hip_mask, device=dev)
+    frames = torch.stack([img1, img2]).contiguous()
+    del img1, img2
+
+    for _ in range(args.warmup):
+        out = trainer.step(frames, flow, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = kprof.KernelTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = trainer.step(frames, flow, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ks = timer.summary()
+    loss = float(out["loss"].item())
+
+    result = None
+    if rank == 0:
+        value = B * world * args.steps / elapsed
+        achieved = ks["tflops"]
+        result = {
+            "metric": "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "frame-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights",
+            "config": {"workload": f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), "
+                                   f"B={B} frame pairs/GPU, 3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}",
+                       "global_batch": B * world, "height": H, "width": W, "parallelism": f"dp{world}"},
+            "frames_per_s": 2 * value,
+            "loss_last_step": loss,
+            "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (conv fwd + dgrad implicit GEMM, all tile variants)",
+                         "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "launches": ks["launches"], "avg_launch_us": ks["avg_us"],
+                         "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
+                         "share_of_step": ks["total_ms"] / (1e3 * elapsed)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+/*
+ * vst_hip.h — C ABI of libvst_hip.so, the MI355X (gfx950 / CDNA4) kernels of the
+ * video-style-transfer training hot path (ReCoNet step: stylizer conv stack, frozen VGG feature
+ * pass, Gram / temporal / TV losses, Adam).
+ *
+ * The reference (Maboroshi0327/Video-Style-Transfer) has no native layer: every entry below
+ * replaces an implicit PyTorch/ATen kernel behind one of the reference's Python call sites,
+ * cited per entry as RC/<file>:<line> (RC/ = "Real-time-Coherent-Video-Style-Transfer-Network-
+ * (ReCoNet)/").  The Python module API that mirrors the reference (`network.py`,
+ * `utilities.py`) calls these through ctypes (video-style-transfer_amd/vst/_lib.py).
+ *
+ * Conventions
+ *   - Tensors: contiguous NCHW fp32 device pointers owned by the caller (PyTorch's caching
+ *     allocator). The library never allocates or frees device memory; scratch comes in through
+ *     `workspace`/`ws`/`partial` arguments sized by the documented formulas.
+ *   - `stream`: a hipStream_t passed as void*; every call is asynchronous on it, no host sync,
+ *     so whole steps can be captured into a hipGraph.
+ *   - Return: 0 on success, negative VST_E* on invalid arguments, positive hipError_t on a
+ *     launch failure.  No exceptions cross the ABI.
+ */
+#ifndef VST_HIP_H
+#define VST_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library ------------------------------------------------------------------------------ */
+int vst_version(void);
+const char* vst_strerror(int code);
+
+/* ---- convolution (implicit GEMM on v_mfma_f32_32x32x2_f32) --------------------------------
+ * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv
+ * (RC/network.py:114-120), torchvision VGG Conv2d(3x3, pad 1) + ReLU (RC/network.py:12-24),
+ * and their autograd backward (dgrad / wgrad), the conv1 bias add and ConvTanh's
+ * tanh(y/255)*150+127.5 (RC/network.py:83-85) as epilogues.
+ *
+ * Weights are re-packed tap-major into A[k][m] (k = (kh*KS+kw)*C + c, leading dim Mpad, rows
+ * padded to Kpad with zeros):  forward: m = cout, c = cin;  transposed (dgrad): m = cin, c = cout.
+ */
+int vst_conv_pack_dims(int M, int K, int* Mpad, int* Kpad);
+int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KS, int transposed, int Mpad, int Kpad,
+                    void* stream);
+/* out[n][m][Ho][Wo] = epi(sum_k A[k][m] * gather(src[n], k, pixel)).
+ * gmode 0: reflect pad, 1: zero pad (forward gather y = oy*stride + kh - pad on the x`up` grid);
+ * gmode 2: transposed gather (dgrad) ty = oy + pad - kh, valid iff ty % stride == 0.
+ * epi bits: 1 bias, 2 relu, 4 reconet-tanh (aux: tanh value, may be NULL), 8 mask (out *= mask>0),
+ * 16 accumulate into out.  a_batch_stride > 0: per-image A (Gram backward).
+ * gmask (may be NULL, same shape as src): gathered values are zeroed where gmask <= 0 — the
+ * ReLU backward of the layer that produced src, fused into the dgrad gather. */
+int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
+                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KS, int gmode, int stride, int pad,
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream);
+/* adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hs*up+2p][Ws*up+2p] -> dx [NC][Hs][Ws] */
+int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
+                     void* stream);
+/* weight gradient, split-K over output pixels with deterministic slab reduction;
+ * workspace floats = vst_wgrad_workspace(N, Cout, KS*KS*Cin, Ho*Wo) */
+long vst_wgrad_workspace(int N, int M, int J, int HWo);
+int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
+                   int Cout, int Ho, int Wo, int KS, int gmode, int stride, int pad, int up, int accumulate,
+                   void* stream);
+
+/* ---- Gram matrix (RC/utilities.py:93-98): G[n] = F[n] F[n]^T * scale ----------------------
+ * workspace floats = vst_wgrad_workspace(N, C, C, HW) */
+int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, void* stream);
+/* Gram backward, part 1: S[n] = scale * (gG[n] + gG[n]^T) written as a packed A [Kpad][Mpad]
+ * (zero padded); part 2: dF = S F via vst_conv_gemm(KS=1, a_batch_stride=Kpad*Mpad)
+ * (bmm backward of RC/utilities.py:97) */
+int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, void* stream);
+
+/* ---- InstanceNorm2d(affine) [+ReLU] [+residual] (RC/network.py:91-97, 140-150) ------------
+ * stats: [N*C][2] (mean, rstd) saved for backward. */
+int vst_instnorm_fwd(const float* x, const float* w, const float* b, const float* res, float* y, float* stats, int N,
+                     int C, int HW, float eps, int relu, void* stream);
+/* partial: N*C*3 floats; gw, gb, gbias_prev (sum of gx = grad of the feeding conv's bias) may be NULL */
+int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* stats, const float* w, float* gx,
+                     float* gw, float* gb, float* gbias_prev, float* partial, int N, int C, int HW, int relu,
+                     int accumulate, void* stream);
+/* out[c] (+)= sum_{n,i} x[n][c][i]; partial: N*C floats (conv bias gradient) */
+int vst_channel_sum(const float* x, float* out, float* partial, int N, int C, int HW, int accumulate, void* stream);
+
+/* ---- VGG MaxPool2d(2, 2) (RC/network.py:12-24 via torchvision features) -------------------- */
+int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream);
+int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, void* stream);
+
+/* ---- flow warp (RC/utilities.py:39-57) / occlusion mask (RC/utilities.py:60-90) ------------
+ * warp_bwd scatters with float atomics into gx (zero it first or accumulate). */
+int vst_warp_fwd(const float* x, const float* flo, float* out, int B, int C, int H, int W, void* stream);
+int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, int H, int W, void* stream);
+int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int B, int H, int W, float threshold,
+                       void* stream);
+/* F.interpolate(mode="bilinear", align_corners=False) (RC/train_single/train_candy.py:91,97);
+ * optional per-channel scale (chscale[C], device) and binarize (> 0) epilogues */
+int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
+                        const float* chscale, int binarize, void* stream);
+
+/* ---- losses (RC/train_single/train_candy.py:90-145) ----------------------------------------
+ * ws: >= 2048 floats; out: 3 floats {loss, weight/denom, denom count}.  Backward reads gout[0]
+ * and out[1] from device memory. */
+/* mode 0 FTL: sum m*(a-b)^2 / nnz, m = mask>0 broadcast over C;  mode 1 OTL: a=styled2, b=warped
+ * styled1, c=img2, d=warped img1, sum m*((a-b) - lum(c-d))^2 / nnz */
+int vst_masked_sqdiff_fwd(int mode, const float* a, const float* b, const float* c, const float* d,
+                          const float* mask, int N, int C, long HW, float weight, float* ws, float* out, void* stream);
+int vst_masked_sqdiff_bwd(int mode, const float* a, const float* b, const float* c, const float* d,
+                          const float* mask, int N, int C, long HW, const float* gout, const float* out, float* ga,
+                          float* gb, void* stream);
+/* weight * mean((a - b[i % nb])^2) (nn.MSELoss, train_candy.py:45,127-137) */
+int vst_mse_fwd(const float* a, const float* b, long n, long nb, float weight, float* ws, float* out, void* stream);
+int vst_mse_bwd(const float* a, const float* b, long n, long nb, const float* gout, const float* out, float* ga,
+                float* gb, void* stream);
+/* weight * sum of squared right/down differences (train_candy.py:141-145) */
+int vst_tv_fwd(const float* s, long NC, int H, int W, float weight, float* ws, float* out, void* stream);
+int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs, void* stream);
+
+/* ---- elementwise ---------------------------------------------------------------------------
+ * vgg_normalize (RC/utilities.py:101-106): out = (x/255 - mean)/std, inplace_scale: x <- x/255 */
+int vst_vgg_normalize(float* x, float* out, int N, int HW, int inplace_scale, void* stream);
+int vst_vgg_normalize_bwd(const float* gout, const float* gscaled, float* gx, int N, int HW, void* stream);
+/* ReLU backward: gx = gy * (y > 0) */
+int vst_relu_bwd(const float* gy, const float* y, float* gx, long n, void* stream);
+/* ConvTanh backward from the saved tanh value (prenorm: fold vgg_normalize's backward in) */
+int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, long HW, int prenorm, void* stream);
+
+/* ---- optimizer: torch.optim.Adam defaults over one flat parameter buffer
+ * (RC/train_single/train_candy.py:44,152); gscale multiplies the gradient (1/world_size) */
+int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
+             long step, float gscale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VST_HIP_H */

@@ -163,12 +163,18 @@ def gen_reconet():
         # real trained checkpoints shipped with the reference (weights_only load)
         x = torch.from_numpy(np.random.default_rng(6).uniform(0, 255, (1, 3, 32, 64)).astype(f32))
         fwd["sd_x"] = _np(x)
+        ckpt = {}
         for cls, fn in ((rc_net.ReCoNetSD1, "SD1_epoch_4_batchSize_2.pth"), (rc_net.ReCoNetSD2, "SD2_epoch_4_batchSize_2.pth")):
             net = cls()
-            net.load_state_dict(torch.load(os.path.join(RC_DIR, "models_old", fn), weights_only=True, map_location="cpu"))
+            sd = torch.load(os.path.join(RC_DIR, "models_old", fn), weights_only=True, map_location="cpu")
+            net.load_state_dict(sd)
+            for k, v in sd.items():
+                ckpt[f"{cls.__name__}/{k}"] = _np(v)
             for i, o in enumerate(net(x)):
                 fwd[f"{cls.__name__}_out{i}"] = _np(o)
     np.savez_compressed(os.path.join(HERE, "rc_fwd.npz"), **fwd)
+    # the reference's own trained distillation checkpoints (data), so the GPU box can run them
+    np.savez_compressed(os.path.join(HERE, "rc_sd_ckpt.npz"), **ckpt)
 
     # full training step through the reference's own train_candy.train()
     step = {}

@@ -1,0 +1,296 @@
+"""HIP path vs the oracle and the reference's golden vectors, on a real MI355X.
+
+Tolerances (north_star: "within 1e-3 relative fp32"):
+  * single ops vs the oracle (fp32 torch-CPU autograd): max|diff| <= 1e-4 * max|ref| (1e-3 for
+    gradients through long reductions);
+  * model forward vs golden: 1e-3 relative to the tensor's max magnitude;
+  * loss terms: 1e-3 relative; gradients: per-tensor norm within 1e-3 (+1e-4 of the largest norm).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import oracle
+from oracle import reconet_ref as R
+from oracle import shapes
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def G(a):
+    return T(a).to(DEV) if isinstance(a, np.ndarray) else a.to(DEV)
+
+
+def C(t):
+    return t.detach().cpu()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+# ----------------------------------------------------------------------------- units vs golden
+def test_warp_mask_gram_norm_golden(golden):
+    from vst.reconet import utilities as U
+
+    u = golden("rc_units")
+    for tag in ("img", "feat", "wide"):
+        out = U.warp(G(u[f"warp_{tag}_x"]), G(u[f"warp_{tag}_flo"]))
+        assert rel_err(C(out), u[f"warp_{tag}_out"]) < 1e-5, tag
+    x = G(u["warp_ramp_x"])
+    assert rel_err(C(U.warp(x, torch.zeros(1, 2, 4, 6, device=DEV))), u["warp_ramp_out"]) < 1e-6
+    for i in range(3):
+        m = U.flow_warp_mask(G(u[f"fwm{i}_f01"]), G(u[f"fwm{i}_f10"]))
+        assert np.array_equal(C(m).numpy(), u[f"fwm{i}_mask"]), i
+    assert rel_err(C(U.gram_matrix(G(u["gram_y"]))), u["gram_out"]) < 1e-5
+    assert torch.allclose(C(U.gram_matrix(torch.ones(1, 2, 3, 3, device=DEV))), torch.full((1, 2, 2), 0.5))
+    x = G(u["vggn_x"]).clone()
+    out = U.vgg_normalize(x)
+    assert rel_err(C(out), u["vggn_out"]) < 1e-6 and rel_err(C(x), u["vggn_x_after"]) < 1e-7
+
+
+# ----------------------------------------------------------------------------- conv family vs oracle
+CONV_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad_mode, up, act)
+    (2, 3, 20, 28, 48, 9, 1, "reflect", 1, None),     # ReCoNet conv1 (Cin=3 slow gather path)
+    (2, 48, 16, 24, 96, 3, 2, "reflect", 1, None),    # conv2 (stride 2)
+    (2, 96, 10, 12, 192, 3, 2, "reflect", 1, None),   # conv3
+    (2, 192, 9, 15, 192, 3, 1, "reflect", 1, None),   # residual conv, ragged
+    (2, 192, 5, 8, 96, 3, 1, "reflect", 2, None),     # deconv1 (nearest x2 upsample)
+    (1, 96, 9, 6, 48, 3, 1, "reflect", 2, None),      # deconv2
+    (2, 48, 16, 20, 3, 9, 1, "reflect", 1, "tanh"),   # deconv3 ConvTanh (Cout=3)
+    (2, 3, 12, 20, 64, 3, 1, "zero", 1, "relu"),      # VGG conv1_1
+    (2, 64, 8, 12, 128, 3, 1, "zero", 1, "relu"),     # VGG conv
+    (1, 256, 4, 6, 512, 3, 1, "zero", 1, "relu"),     # VGG conv4_x
+]
+
+
+def _oracle_conv(x, w, b, stride, pad_mode, up, act):
+    k = w.shape[-1]
+    if up == 2:
+        x = R.upsample_nearest2x(x)
+    if pad_mode == "reflect":
+        y = F.conv2d(R.reflect_pad(x, k // 2), w, b, stride=stride)
+    else:
+        y = F.conv2d(x, w, b, stride=stride, padding=k // 2)
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "tanh":
+        y = torch.tanh(y / 255) * 150 + 255 / 2
+    return y
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"{c[1]}-{c[4]}-k{c[5]}s{c[6]}{c[7][0]}u{c[8]}{c[9] or ''}" for c in CONV_CASES])
+def test_conv_fwd_bwd(case):
+    from vst import ops
+
+    N, Cin, H, W, Cout, k, stride, pad_mode, up, act = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    x = torch.randn(N, Cin, H, W, generator=g) * (40.0 if act == "tanh" else 1.0)
+    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = _oracle_conv(xr, wr, br, stride, pad_mode, up, act)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+
+    xg, wg, bg = (G(t).requires_grad_(True) for t in (x, w, b))
+    pad = k // 2
+    y = ops.conv2d(xg, wg, bg, stride=stride, pad=pad, pad_mode=pad_mode, up=up, act=act)
+    assert y.shape == yr.shape
+    assert rel_err(C(y), yr.detach()) < 1e-4
+    y.backward(G(gy))
+    assert rel_err(C(xg.grad), xr.grad) < 1e-4
+    assert rel_err(C(wg.grad), wr.grad) < 1e-4
+    assert rel_err(C(bg.grad), br.grad) < 1e-4
+
+
+def test_conv_relu_frozen_weights_dgrad_mask():
+    """VGG path: frozen weights, ReLU mask fused into the dgrad gather (no relu_bwd pass)."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 64, 10, 14, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.06
+    b = torch.randn(64, generator=g) * 0.1
+    xr = x.clone().requires_grad_(True)
+    y1 = torch.relu(F.conv2d(xr, w, b, padding=1))
+    y2 = torch.relu(F.conv2d(y1, w, b, padding=1))
+    gy = torch.randn(y2.shape, generator=g)
+    y2.backward(gy)
+    xg = G(x).requires_grad_(True)
+    wg, bg = G(w), G(b)
+    z1 = ops.conv2d(xg, wg, bg, pad=1, act="relu")
+    z2 = ops.conv2d(z1, wg, bg, pad=1, act="relu")
+    z2.backward(G(gy))
+    assert rel_err(C(z2), y2.detach()) < 1e-4
+    assert rel_err(C(xg.grad), xr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("relu,res,shape", [(True, False, (2, 48, 16, 20)), (False, True, (2, 192, 9, 15)),
+                                            (True, False, (1, 96, 64, 128))])
+def test_instance_norm(relu, res, shape):
+    from vst import ops
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(shape, generator=g) * 3 + 1.5
+    w = 1 + 0.1 * torch.randn(shape[1], generator=g)
+    b = 0.1 * torch.randn(shape[1], generator=g)
+    r = torch.randn(shape, generator=g)
+    xr, wr, br, rr = (t.clone().requires_grad_(True) for t in (x, w, b, r))
+    yr = R.instance_norm(xr, wr, br)
+    if relu:
+        yr = torch.relu(yr)
+    if res:
+        yr = yr + rr
+    gy = torch.randn(shape, generator=g)
+    yr.backward(gy)
+    xg, wg, bg, rg = (G(t).requires_grad_(True) for t in (x, w, b, r))
+    y = ops.instance_norm(xg, wg, bg, relu=relu, res=rg if res else None)
+    y.backward(G(gy))
+    assert rel_err(C(y), yr.detach()) < 1e-5
+    assert rel_err(C(xg.grad), xr.grad) < 1e-4
+    assert rel_err(C(wg.grad), wr.grad) < 1e-4
+    assert rel_err(C(bg.grad), br.grad) < 1e-4
+    if res:
+        assert rel_err(C(rg.grad), rr.grad) < 1e-6
+
+
+def test_pool_warp_gram_losses_bwd():
+    from vst import ops
+
+    g = torch.Generator().manual_seed(11)
+    # maxpool (odd size drops the trailing row/col)
+    x = torch.randn(2, 8, 9, 15, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = R.maxpool2x2(xr)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xg = G(x).requires_grad_(True)
+    y = ops.maxpool2x2(xg)
+    y.backward(G(gy))
+    assert torch.equal(C(y), yr.detach()) and rel_err(C(xg.grad), xr.grad) < 1e-6
+    # warp backward (atomic scatter)
+    x = torch.randn(2, 5, 12, 20, generator=g)
+    flo = torch.rand(2, 2, 12, 20, generator=g) * 8 - 4
+    xr = x.clone().requires_grad_(True)
+    yr = R.warp(xr, flo)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xg = G(x).requires_grad_(True)
+    y = ops.warp(xg, G(flo))
+    y.backward(G(gy))
+    assert rel_err(C(y), yr.detach()) < 1e-5 and rel_err(C(xg.grad), xr.grad) < 1e-5
+    # gram + broadcast style MSE backward
+    f = torch.randn(3, 64, 7, 9, generator=g)
+    gs = torch.randn(1, 64, 64, generator=g) * 0.1
+    fr = f.clone().requires_grad_(True)
+    lr_ = F.mse_loss(R.gram_matrix(fr), gs.expand(3, -1, -1)) * 7.0
+    lr_.backward()
+    fg = G(f).requires_grad_(True)
+    lg = ops.mse(ops.gram_matrix(fg), G(gs), 7.0)
+    lg.backward()
+    assert rel_err(C(lg), lr_.detach()) < 1e-5 and rel_err(C(fg.grad), fr.grad) < 1e-4
+    # TV
+    s = torch.randn(2, 3, 10, 13, generator=g)
+    sr = s.clone().requires_grad_(True)
+    tr = 0.5 * torch.sum((sr[:, :, :-1, 1:] - sr[:, :, :-1, :-1]) ** 2 + (sr[:, :, 1:, :-1] - sr[:, :, :-1, :-1]) ** 2)
+    tr.backward()
+    sg = G(s).requires_grad_(True)
+    tg = ops.tv_loss(sg, 0.5)
+    tg.backward()
+    assert rel_err(C(tg), tr.detach()) < 1e-5 and rel_err(C(sg.grad), sr.grad) < 1e-5
+
+
+# ----------------------------------------------------------------------------- models vs golden
+def _seeded(module, spec, seed):
+    params = oracle.seeded_params(spec, seed)
+    sd = module.state_dict()
+    assert sorted(sd) == sorted(params), "state_dict keys differ from the reference"
+    module.load_state_dict({k: v for k, v in params.items()})
+    return module
+
+
+def test_state_dict_keys_match_reference():
+    from vst.reconet import network as N
+
+    for cls, spec in ((N.ReCoNet, shapes.reconet()), (N.ReCoNetSD1, shapes.reconet_sd1()),
+                      (N.ReCoNetSD2, shapes.reconet_sd2()), (N.Vgg16, shapes.vgg16())):
+        sd = cls().state_dict()
+        assert [(k, tuple(v.shape)) for k, v in sd.items()] == [(k, tuple(s)) for k, s in spec], cls.__name__
+
+
+def test_reconet_vgg16_forward_golden(golden):
+    from vst.reconet import network as N
+
+    f = golden("rc_fwd")
+    m = _seeded(N.ReCoNet(), shapes.reconet(), 1).to(DEV)
+    with torch.no_grad():
+        for tag in ("a", "ragged"):
+            sd1, feat, out = m(G(f[f"reconet_{tag}_x"]))
+            assert rel_err(C(sd1), f[f"reconet_{tag}_sd1"]) < 1e-3
+            assert rel_err(C(feat), f[f"reconet_{tag}_features"]) < 1e-3
+            assert rel_err(C(out), f[f"reconet_{tag}_out"]) < 1e-3
+        v = _seeded(N.Vgg16(), shapes.vgg16(), 4).to(DEV)
+        outs = v(G(f["vgg16_x"]))
+        for name in outs._fields:
+            assert rel_err(C(getattr(outs, name)), f["vgg16_" + name]) < 1e-3, name
+
+
+def test_sd_checkpoints_forward_golden(golden):
+    from vst.reconet import network as N
+
+    f = golden("rc_fwd")
+    ck = golden("rc_sd_ckpt")
+    for cls in (N.ReCoNetSD1, N.ReCoNetSD2):
+        net = cls()
+        net.load_state_dict({k.split("/", 1)[1]: T(v) for k, v in ck.items() if k.startswith(cls.__name__ + "/")})
+        net = net.to(DEV)
+        with torch.no_grad():
+            outs = net(G(f["sd_x"]))
+        for i, o in enumerate(outs):
+            assert rel_err(C(o), f[f"{cls.__name__}_out{i}"]) < 1e-3, (cls.__name__, i)
+
+
+@pytest.mark.parametrize("tag", ["b2", "b1r"])
+def test_train_step_golden(golden, tag):
+    """One full train_candy step (losses, gradients, Adam update) vs the reference's own train()."""
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+
+    s = golden("rc_step")
+    seeds = s[f"{tag}_seeds"]
+    model = _seeded(N.ReCoNet(), shapes.reconet(), int(seeds[0])).to(DEV)
+    vgg = _seeded(N.Vgg16(), shapes.vgg16(), int(seeds[1])).to(DEV)
+    tr = ReCoNetTrainer(model, vgg, G(s[f"{tag}_style"]))
+    frames = torch.stack([G(s[f"{tag}_img1"]), G(s[f"{tag}_img2"])])
+    out = tr.losses(frames, G(s[f"{tag}_flow"]), G(s[f"{tag}_mask"]))
+    for k in ("loss", "CL", "SL", "FTL", "OTL", "RL"):
+        assert rel_err(out[k].item(), s[f"{tag}_{k}"]) < 1e-3, k
+    tr.flat.zero_grad()
+    out["loss"].backward()
+    names = list(s[f"{tag}_names"])
+    named = dict(model.named_parameters())
+    gmax = max(float(s[f"{tag}_gnorm/{n}"]) for n in names)
+    for n in names:
+        gr = C(named[n].grad).reshape(-1)
+        gn = float(s[f"{tag}_gnorm/{n}"])
+        assert abs(float(gr.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"{tag}_gidx/{n}"]
+        assert np.abs(gr[idx].numpy() - s[f"{tag}_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+    tr.step_count = 0
+    tr.flat.adam(1, tr.lr, tr.betas, tr.eps)
+    for n in names:
+        gh = s[f"{tag}_ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        got = C(named[n]).reshape(-1)[:64].numpy()
+        assert np.abs(got - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n

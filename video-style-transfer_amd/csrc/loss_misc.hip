@@ -1,0 +1,386 @@
+// Loss reductions, elementwise ops and the optimizer of the ReCoNet training step (gfx950).
+//
+// Every loss is a two-stage deterministic reduction: a grid-stride kernel writes per-block
+// partials {sum, count}; a one-block finisher sums them in fixed order and writes
+//   out[0] = weight * sum / denom,  out[1] = weight / denom
+// (denom = the on-device non-zero count for the temporal losses, so the reference's
+// `torch.nonzero(mask).shape[0]` host sync disappears; numel for MSE; 1 for TV).  Backward
+// kernels read the upstream gradient and out[1] from device memory: no host round trip.
+//
+// Reference semantics: RC/train_single/train_candy.py:90-145 (FTL, OTL, content, style, TV),
+// RC/utilities.py:101-106 (vgg_normalize), RC/network.py:83-85 (ConvTanh),
+// torch.optim.Adam defaults (train_candy.py:44,152).
+#include "vst_common.h"
+#include "vst_hip.h"
+
+namespace {
+
+constexpr int RT = 256;
+constexpr int MAXB = 1024;
+
+__device__ __forceinline__ void block_partial(float s, float c, float* partial) {
+  __shared__ float sh[2][RT / 64];
+  s = wave_sum(s);
+  c = wave_sum(c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[0][w] = s;
+    sh[1][w] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < RT / 64; ++i) {
+      a += sh[0][i];
+      b += sh[1][i];
+    }
+    partial[2 * blockIdx.x] = a;
+    partial[2 * blockIdx.x + 1] = b;
+  }
+}
+
+__global__ void finish_kernel(const float* __restrict__ partial, int nb, float* __restrict__ out, float weight,
+                              double fixed_denom, int use_count) {
+  __shared__ double sh[2][RT / 64];
+  double s = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < nb; i += RT) {
+    s += partial[2 * i];
+    c += partial[2 * i + 1];
+  }
+  s = wave_sum_d(s);
+  c = wave_sum_d(c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[0][w] = s;
+    sh[1][w] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < RT / 64; ++i) {
+      a += sh[0][i];
+      b += sh[1][i];
+    }
+    double d = use_count ? b : fixed_denom;
+    float inv = (float)(1.0 / (d > 0.0 ? d : 1.0));
+    // reference: loss = sum * (1 / nnz) * LAMBDA   (train_candy.py:105-106) in fp32
+    float sum = (float)a;
+    out[0] = sum * inv * weight;
+    out[1] = inv * weight;
+    out[2] = (float)b;
+  }
+}
+
+// FTL (mode 0): sum_{n,c,p} m(n,p) * (a - b)^2, m = (mask > 0), count = C * nnz(m)
+// OTL (mode 1): ot = a - b, it = lum(c - d); sum_{n,c,p} m * (ot - it)^2, count = C * nnz(m != 0)
+template <int MODE>
+__global__ void masked_sqdiff_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                     const float* __restrict__ c, const float* __restrict__ d,
+                                     const float* __restrict__ mask, int N, int C, long HW, float* partial) {
+  float s = 0.f, cnt = 0.f;
+  const long total = (long)N * HW;
+  for (long idx = (long)blockIdx.x * RT + threadIdx.x; idx < total; idx += (long)gridDim.x * RT) {
+    const long n = idx / HW, p = idx - n * HW;
+    float m = mask[idx];
+    if (MODE == 0) m = m > 0.f ? 1.f : 0.f;
+    if (m == 0.f) continue;
+    cnt += (float)C;
+    const long base = n * C * HW + p;
+    if (MODE == 0) {
+      for (int ch = 0; ch < C; ++ch) {
+        float df = a[base + ch * HW] - b[base + ch * HW];
+        s += m * (df * df);
+      }
+    } else {
+      float i0 = c[base] - d[base], i1 = c[base + HW] - d[base + HW], i2 = c[base + 2 * HW] - d[base + 2 * HW];
+      float it = 0.2126f * i0 + 0.7152f * i1 + 0.0722f * i2;
+      for (int ch = 0; ch < 3; ++ch) {
+        float df = (a[base + ch * HW] - b[base + ch * HW]) - it;
+        s += m * (df * df);
+      }
+    }
+  }
+  block_partial(s, cnt, partial);
+}
+
+template <int MODE>
+__global__ void masked_sqdiff_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                         const float* __restrict__ c, const float* __restrict__ d,
+                                         const float* __restrict__ mask, int N, int C, long HW,
+                                         const float* __restrict__ gout, const float* __restrict__ scale,
+                                         float* __restrict__ ga, float* __restrict__ gb) {
+  const long total = (long)N * HW;
+  const float k = 2.f * gout[0] * scale[1];
+  for (long idx = (long)blockIdx.x * RT + threadIdx.x; idx < total; idx += (long)gridDim.x * RT) {
+    const long n = idx / HW, p = idx - n * HW;
+    float m = mask[idx];
+    if (MODE == 0) m = m > 0.f ? 1.f : 0.f;
+    const long base = n * C * HW + p;
+    float it = 0.f;
+    if (MODE == 1) {
+      float i0 = c[base] - d[base], i1 = c[base + HW] - d[base + HW], i2 = c[base + 2 * HW] - d[base + 2 * HW];
+      it = 0.2126f * i0 + 0.7152f * i1 + 0.0722f * i2;
+    }
+    for (int ch = 0; ch < C; ++ch) {
+      const long o = base + ch * HW;
+      float g = k * m * ((a[o] - b[o]) - it);
+      if (ga) ga[o] = g;
+      if (gb) gb[o] = -g;
+    }
+  }
+}
+
+// sum (a - b[i % nb])^2
+__global__ void sqdiff_kernel(const float* __restrict__ a, const float* __restrict__ b, long n, long nb,
+                              float* partial) {
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < n; i += (long)gridDim.x * RT) {
+    float df = a[i] - b[i % nb];
+    s += df * df;
+  }
+  block_partial(s, 0.f, partial);
+}
+
+__global__ void sqdiff_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b, long n, long nb,
+                                  const float* __restrict__ gout, const float* __restrict__ scale,
+                                  float* __restrict__ ga, float* __restrict__ gb) {
+  const float k = 2.f * gout[0] * scale[1];
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < n; i += (long)gridDim.x * RT) {
+    float g = k * (a[i] - b[i % nb]);
+    if (ga) ga[i] = g;
+    if (gb) gb[i] = -g;
+  }
+}
+
+// TV: sum over y<H-1, x<W-1 of (s[y][x+1]-s[y][x])^2 + (s[y+1][x]-s[y][x])^2  (train_candy.py:141-145)
+__global__ void tv_kernel(const float* __restrict__ s, long NC, int H, int W, float* partial) {
+  float acc = 0.f;
+  const long total = NC * (H - 1) * (W - 1);
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < total; i += (long)gridDim.x * RT) {
+    int x = (int)(i % (W - 1));
+    long t = i / (W - 1);
+    int y = (int)(t % (H - 1));
+    long nc = t / (H - 1);
+    const float* p = s + nc * H * W + (long)y * W + x;
+    float d1 = p[1] - p[0], d2 = p[W] - p[0];
+    acc += d1 * d1 + d2 * d2;
+  }
+  block_partial(acc, 0.f, partial);
+}
+
+__global__ void tv_bwd_kernel(const float* __restrict__ s, long NC, int H, int W, const float* __restrict__ gout,
+                              const float* __restrict__ scale, float* __restrict__ gs) {
+  const float k = 2.f * gout[0] * scale[1];
+  const long total = NC * H * W;
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < total; i += (long)gridDim.x * RT) {
+    int x = (int)(i % W);
+    long t = i / W;
+    int y = (int)(t % H);
+    const float* p = s + i;
+    float g = 0.f;
+    if (y < H - 1 && x < W - 1) g -= (p[1] - p[0]) + (p[W] - p[0]);
+    if (x >= 1 && y < H - 1) g += p[0] - p[-1];
+    if (y >= 1 && x < W - 1) g += p[0] - p[-W];
+    gs[i] = k * g;
+  }
+}
+
+// S[n][k][m] = scale * (g[n][k][m] + g[n][m][k]) for k, m < C; zero in the [Kpad][Mpad] padding
+// (bmm backward of F F^T: dF = (gG + gG^T) F / (C H W); S is symmetric so [k][m] is the packed A)
+__global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict__ S, int N, int C, int Kpad, int Mpad,
+                                  float scale) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * Kpad * Mpad) return;
+  int m = (int)(idx % Mpad);
+  long t = idx / Mpad;
+  int k = (int)(t % Kpad);
+  long n = t / Kpad;
+  float v = 0.f;
+  if (k < C && m < C) {
+    const float* gn = g + n * C * C;
+    v = (gn[k * C + m] + gn[m * C + k]) * scale;
+  }
+  S[idx] = v;
+}
+
+// ReLU backward: gx = gy * (y > 0)
+__global__ void relu_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y, float* __restrict__ gx,
+                                long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gx[i] = y[i] > 0.f ? gy[i] : 0.f;
+}
+
+__constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
+
+// out = (x/255 - mean[c]) / std[c]; inplace_scale: x <- x/255 (RC/utilities.py:105 `batch.div_(255.0)`)
+__global__ void vgg_norm_kernel(float* __restrict__ x, float* __restrict__ out, long total, long HW,
+                                int inplace_scale) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int c = (int)((i / HW) % 3);
+  float v = x[i] / 255.0f;
+  if (inplace_scale) x[i] = v;
+  out[i] = (v - kMean[c]) / kStd[c];
+}
+
+// gx = (gout / std[c]) / 255 (+ g_scaled / 255 when the mutated input also carries a gradient)
+__global__ void vgg_norm_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ gscaled,
+                                    float* __restrict__ gx, long total, long HW) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int c = (int)((i / HW) % 3);
+  float g = gout[i] / kStd[c];
+  if (gscaled) g += gscaled[i];
+  gx[i] = g / 255.0f;
+}
+
+// ConvTanh backward from the saved tanh value t: gv = ((gy * 150) * (1 - t^2)) / 255
+// prenorm: gy = (gy / std[c]) / 255 first (fused vgg_normalize backward)
+__global__ void tanh_out_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ t, float* __restrict__ gv,
+                                    long total, long HW, int prenorm) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  float g = gy[i];
+  if (prenorm) {
+    int c = (int)((i / HW) % 3);
+    g = (g / kStd[c]) / 255.0f;
+  }
+  float tt = t[i];
+  gv[i] = ((g * 150.0f) * (1.0f - tt * tt)) / 255.0f;
+}
+
+// torch.optim.Adam (no weight decay / amsgrad / maximize): exp_avg.lerp_(g, 1-b1);
+// exp_avg_sq = exp_avg_sq*b2 + (1-b2) g^2; p -= step_size * exp_avg / (sqrt(exp_avg_sq)/bc2_sqrt + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long n, float b1, float b2, float eps, float step_size,
+                            float bc2_sqrt, float gscale) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = g[i] * gscale;
+  float mi = m[i];
+  mi = mi + (1.0f - b1) * (gi - mi);
+  float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] + (-step_size) * (mi / denom);
+}
+
+static int nblocks(long work) {
+  long b = (work + RT - 1) / RT;
+  return (int)(b < 1 ? 1 : (b > MAXB ? MAXB : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+// workspace: >= 2*1024 floats; out: 3 floats (loss, weight/denom, count)
+int vst_masked_sqdiff_fwd(int mode, const float* a, const float* b, const float* c, const float* d,
+                          const float* mask, int N, int C, long HW, float weight, float* ws, float* out,
+                          void* stream) {
+  VST_CHECK_ARG(a && b && mask && ws && out && N > 0 && C > 0 && HW > 0 && (mode == 0 || mode == 1));
+  VST_CHECK_ARG(mode == 0 || (c && d && C == 3));
+  hipStream_t st = (hipStream_t)stream;
+  int nb = nblocks((long)N * HW);
+  if (mode == 0)
+    masked_sqdiff_kernel<0><<<nb, RT, 0, st>>>(a, b, c, d, mask, N, C, HW, ws);
+  else
+    masked_sqdiff_kernel<1><<<nb, RT, 0, st>>>(a, b, c, d, mask, N, C, HW, ws);
+  finish_kernel<<<1, RT, 0, st>>>(ws, nb, out, weight, 1.0, 1);
+  return vst_launch_status();
+}
+
+int vst_masked_sqdiff_bwd(int mode, const float* a, const float* b, const float* c, const float* d,
+                          const float* mask, int N, int C, long HW, const float* gout, const float* out, float* ga,
+                          float* gb, void* stream) {
+  VST_CHECK_ARG(a && b && mask && gout && out && N > 0 && C > 0 && HW > 0 && (mode == 0 || mode == 1));
+  hipStream_t st = (hipStream_t)stream;
+  int nb = nblocks((long)N * HW);
+  if (mode == 0)
+    masked_sqdiff_bwd_kernel<0><<<nb, RT, 0, st>>>(a, b, c, d, mask, N, C, HW, gout, out, ga, gb);
+  else
+    masked_sqdiff_bwd_kernel<1><<<nb, RT, 0, st>>>(a, b, c, d, mask, N, C, HW, gout, out, ga, gb);
+  return vst_launch_status();
+}
+
+// loss = weight * mean((a - b[i % nb])^2) over n elements
+int vst_mse_fwd(const float* a, const float* b, long n, long nb, float weight, float* ws, float* out, void* stream) {
+  VST_CHECK_ARG(a && b && ws && out && n > 0 && nb > 0);
+  hipStream_t st = (hipStream_t)stream;
+  int g = nblocks(n);
+  sqdiff_kernel<<<g, RT, 0, st>>>(a, b, n, nb, ws);
+  finish_kernel<<<1, RT, 0, st>>>(ws, g, out, weight, (double)n, 0);
+  return vst_launch_status();
+}
+
+int vst_mse_bwd(const float* a, const float* b, long n, long nb, const float* gout, const float* out, float* ga,
+                float* gb, void* stream) {
+  VST_CHECK_ARG(a && b && gout && out && n > 0 && nb > 0 && (!gb || nb == n));
+  sqdiff_bwd_kernel<<<nblocks(n), RT, 0, (hipStream_t)stream>>>(a, b, n, nb, gout, out, ga, gb);
+  return vst_launch_status();
+}
+
+int vst_tv_fwd(const float* s, long NC, int H, int W, float weight, float* ws, float* out, void* stream) {
+  VST_CHECK_ARG(s && ws && out && NC > 0 && H > 1 && W > 1);
+  hipStream_t st = (hipStream_t)stream;
+  int g = nblocks(NC * (H - 1) * (W - 1));
+  tv_kernel<<<g, RT, 0, st>>>(s, NC, H, W, ws);
+  finish_kernel<<<1, RT, 0, st>>>(ws, g, out, weight, 1.0, 0);
+  return vst_launch_status();
+}
+
+int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs, void* stream) {
+  VST_CHECK_ARG(s && gout && out && gs && NC > 0 && H > 1 && W > 1);
+  tv_bwd_kernel<<<nblocks(NC * H * W), RT, 0, (hipStream_t)stream>>>(s, NC, H, W, gout, out, gs);
+  return vst_launch_status();
+}
+
+int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, void* stream) {
+  VST_CHECK_ARG(g && S && N > 0 && C > 0 && Kpad >= C && Mpad >= C);
+  long total = (long)N * Kpad * Mpad;
+  symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale);
+  return vst_launch_status();
+}
+
+int vst_relu_bwd(const float* gy, const float* y, float* gx, long n, void* stream) {
+  VST_CHECK_ARG(gy && y && gx && n > 0);
+  relu_bwd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(gy, y, gx, n);
+  return vst_launch_status();
+}
+
+int vst_vgg_normalize(float* x, float* out, int N, int HW, int inplace_scale, void* stream) {
+  VST_CHECK_ARG(x && out && N > 0 && HW > 0);
+  long total = (long)N * 3 * HW;
+  vgg_norm_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, total, HW, inplace_scale);
+  return vst_launch_status();
+}
+
+int vst_vgg_normalize_bwd(const float* gout, const float* gscaled, float* gx, int N, int HW, void* stream) {
+  VST_CHECK_ARG(gout && gx && N > 0 && HW > 0);
+  long total = (long)N * 3 * HW;
+  vgg_norm_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, gscaled, gx, total, HW);
+  return vst_launch_status();
+}
+
+int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, long HW, int prenorm, void* stream) {
+  VST_CHECK_ARG(gy && t && gv && total > 0 && HW > 0);
+  tanh_out_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gy, t, gv, total, HW, prenorm);
+  return vst_launch_status();
+}
+
+int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
+             long step, float gscale, void* stream) {
+  VST_CHECK_ARG(p && g && m && v && n > 0 && step > 0);
+  double bc1 = 1.0 - pow((double)b1, (double)step);
+  double bc2 = 1.0 - pow((double)b2, (double)step);
+  float step_size = (float)(lr / bc1);
+  float bc2_sqrt = (float)sqrt(bc2);
+  adam_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(p, g, m, v, n, b1, b2, eps, step_size, bc2_sqrt,
+                                                                 gscale);
+  return vst_launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,240 @@
+// Gather/scatter kernels of the ReCoNet step for gfx950:
+//   * MaxPool2d(2, 2) forward / backward (VGG features "M" layers, RC/network.py:17-24),
+//   * flow warp forward / backward (RC/utilities.py:39-57: bilinear grid_sample, zeros padding,
+//     align_corners=False, grid normalised by (W-1)/(H-1) -> source x = ((2(x+u)/(W-1)-1)+1)W/2-0.5),
+//   * forward-backward flow consistency mask (RC/utilities.py:60-90),
+//   * bilinear resize with align_corners=False (F.interpolate, train_candy.py:91,97).
+#include "vst_common.h"
+#include "vst_hip.h"
+
+namespace {
+
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, long NC, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * Ho * Wo) return;
+  int ox = (int)(idx % Wo);
+  long t = idx / Wo;
+  int oy = (int)(t % Ho);
+  long nc = t / Ho;
+  const float* p = x + nc * H * W + (long)(2 * oy) * W + 2 * ox;
+  float2 a = make_float2(p[0], p[1]);
+  float2 b = make_float2(p[W], p[W + 1]);
+  // first maximum in scan order wins (matches max_pool2d's `val > maxval` scan; NaN propagates)
+  float m = a.x;
+  if (a.y > m || isnan(a.y)) m = a.y;
+  if (b.x > m || isnan(b.x)) m = b.x;
+  if (b.y > m || isnan(b.y)) m = b.y;
+  y[idx] = m;
+}
+
+// gx over the full input (zeros where no window routes a gradient)
+__global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ gx,
+                                   long NC, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * H * W) return;
+  int ix = (int)(idx % W);
+  long t = idx / W;
+  int iy = (int)(t % H);
+  long nc = t / H;
+  int oy = iy >> 1, ox = ix >> 1;
+  float g = 0.f;
+  if (oy < Ho && ox < Wo) {
+    const float* p = x + nc * H * W + (long)(2 * oy) * W + 2 * ox;
+    float v[4] = {p[0], p[1], p[W], p[W + 1]};
+    int arg = 0;
+    float m = v[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (v[k] > m || isnan(v[k])) {
+        m = v[k];
+        arg = k;
+      }
+    if (arg == (iy & 1) * 2 + (ix & 1)) g = gy[nc * Ho * Wo + (long)oy * Wo + ox];
+  }
+  gx[idx] = g;
+}
+
+struct Bilin {
+  int x0, y0;
+  float w[4];  // nw, ne, sw, se
+};
+
+// grid_sample(align_corners=False) bilinear coordinates + weights, same fp32 op order as ATen
+__device__ __forceinline__ Bilin warp_coords(int x, int y, float u, float v, int H, int W) {
+  float gx = 2.0f * ((float)x + u) / (float)max(W - 1, 1) - 1.0f;
+  float gy = 2.0f * ((float)y + v) / (float)max(H - 1, 1) - 1.0f;
+  float ix = ((gx + 1.f) * W - 1.f) / 2.f;
+  float iy = ((gy + 1.f) * H - 1.f) / 2.f;
+  float fx = floorf(ix), fy = floorf(iy);
+  Bilin b;
+  b.x0 = (int)fx;
+  b.y0 = (int)fy;
+  float ix_se = fx + 1.f, iy_se = fy + 1.f;
+  b.w[0] = (ix_se - ix) * (iy_se - iy);
+  b.w[1] = (ix - fx) * (iy_se - iy);
+  b.w[2] = (ix_se - ix) * (iy - fy);
+  b.w[3] = (ix - fx) * (iy - fy);
+  return b;
+}
+
+__global__ void warp_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flo, float* __restrict__ out,
+                                int B, int C, int H, int W) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const int y = (int)(p / W), xx = (int)(p % W);
+  const float* f = flo + (long)b * 2 * HW;
+  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
+  long off[4];
+  float wt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
+    bool ok = cx >= 0 && cx < W && cy >= 0 && cy < H;
+    off[k] = ok ? (long)cy * W + cx : 0;
+    wt[k] = ok ? bl.w[k] : 0.f;
+  }
+  const float* xb = x + (long)b * C * HW;
+  float* ob = out + (long)b * C * HW;
+  for (int c = 0; c < C; ++c) {
+    const float* xc = xb + c * HW;
+    // ATen sums nw, ne, sw, se in this order; out-of-bounds corners contribute 0 (weight zeroed)
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += xc[off[k]] * wt[k];
+    ob[c * HW + p] = s;
+  }
+}
+
+__global__ void warp_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ flo, float* __restrict__ gx,
+                                int B, int C, int H, int W) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const int y = (int)(p / W), xx = (int)(p % W);
+  const float* f = flo + (long)b * 2 * HW;
+  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
+  const float* gb = gout + (long)b * C * HW;
+  float* xb = gx + (long)b * C * HW;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
+    if (cx < 0 || cx >= W || cy < 0 || cy >= H) continue;
+    long o = (long)cy * W + cx;
+    for (int c = 0; c < C; ++c) atomicAdd(xb + c * HW + o, gb[c * HW + p] * bl.w[k]);
+  }
+}
+
+// mask[y][x] = (|warp(grid+flo01, flo10) - grid|_1 < thr)
+__global__ void flow_mask_kernel(const float* __restrict__ flo01, const float* __restrict__ flo10,
+                                 float* __restrict__ mask, int B, int H, int W, float thr) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const int y = (int)(p / W), xx = (int)(p % W);
+  const float* f10 = flo10 + (long)b * 2 * HW;
+  const float* f01 = flo01 + (long)b * 2 * HW;
+  Bilin bl = warp_coords(xx, y, f10[p], f10[HW + p], H, W);
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
+    if (cx < 0 || cx >= W || cy < 0 || cy >= H) continue;
+    long o = (long)cy * W + cx;
+    s0 += ((float)cx + f01[o]) * bl.w[k];
+    s1 += ((float)cy + f01[HW + o]) * bl.w[k];
+  }
+  float err = fabsf(s0 - (float)xx) + fabsf(s1 - (float)y);
+  mask[idx] = err < thr ? 1.f : 0.f;
+}
+
+__device__ __forceinline__ void resize_axis(int d, int n_in, int n_out, int& i0, int& i1, float& l1) {
+  float scale = (float)n_in / (float)n_out;
+  float src = ((float)d + 0.5f) * scale - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  i0 = (int)src;
+  i0 = i0 > n_in - 1 ? n_in - 1 : i0;
+  i1 = i0 < n_in - 1 ? i0 + 1 : i0;
+  l1 = src - (float)i0;
+}
+
+// out[nc] = resize(x[nc]) * chscale[c % C] ; binarize: out = out > 0
+__global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ out, long NC, int C, int H, int W, int Ho,
+                              int Wo, const float* chscale, int binarize) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * Ho * Wo) return;
+  int ox = (int)(idx % Wo);
+  long t = idx / Wo;
+  int oy = (int)(t % Ho);
+  long nc = t / Ho;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  resize_axis(oy, H, Ho, y0, y1, ly);
+  resize_axis(ox, W, Wo, x0, x1, lx);
+  const float* p = x + nc * H * W;
+  float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
+            ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
+  if (chscale) v *= chscale[nc % C];
+  if (binarize) v = v > 0.f ? 1.f : 0.f;
+  out[idx] = v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream) {
+  VST_CHECK_ARG(x && y && NC > 0 && H >= 2 && W >= 2);
+  long total = NC * (H / 2) * (W / 2);
+  maxpool_fwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, y, NC, H, W);
+  return vst_launch_status();
+}
+
+int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, void* stream) {
+  VST_CHECK_ARG(x && gy && gx && NC > 0 && H >= 2 && W >= 2);
+  long total = NC * H * W;
+  maxpool_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, gx, NC, H, W);
+  return vst_launch_status();
+}
+
+int vst_warp_fwd(const float* x, const float* flo, float* out, int B, int C, int H, int W, void* stream) {
+  VST_CHECK_ARG(x && flo && out && B > 0 && C > 0 && H > 0 && W > 0);
+  long total = (long)B * H * W;
+  warp_fwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, flo, out, B, C, H, W);
+  return vst_launch_status();
+}
+
+// gx must be zeroed (or hold a gradient to accumulate into): float atomics scatter into it
+int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, int H, int W, void* stream) {
+  VST_CHECK_ARG(gout && flo && gx && B > 0 && C > 0 && H > 0 && W > 0);
+  long total = (long)B * H * W;
+  warp_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, flo, gx, B, C, H, W);
+  return vst_launch_status();
+}
+
+int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int B, int H, int W, float threshold,
+                       void* stream) {
+  VST_CHECK_ARG(flo01 && flo10 && mask && B > 0 && H > 0 && W > 0);
+  long total = (long)B * H * W;
+  flow_mask_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(flo01, flo10, mask, B, H, W, threshold);
+  return vst_launch_status();
+}
+
+int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
+                        const float* chscale, int binarize, void* stream) {
+  VST_CHECK_ARG(x && out && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0);
+  long total = NC * Ho * Wo;
+  resize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, NC, C, H, W, Ho, Wo, chscale,
+                                                                       binarize);
+  return vst_launch_status();
+}
+
+}  // extern "C"

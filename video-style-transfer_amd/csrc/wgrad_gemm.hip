@@ -1,0 +1,322 @@
+// Split-K "activation-gradient x im2col(input)^T" GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+//   slab[z][m][j] = sum_{r in chunk z}  A[n][m][r] * gather(src[n], j, r)
+//
+// Serves the conv weight gradient (dW[co][(kh,kw,ci)], RC/network.py:70 Conv2d backward) and the
+// Gram matrix F F^T (RC/utilities.py:93-98, KS = 1, A == src).  The reduction runs over output
+// pixels r of ONE image per block (grid.z = N * S splits); partial slabs are summed by
+// `wgrad_reduce` (into PyTorch's [co][ci][kh][kw] order) or `gram_reduce` (per image, scaled),
+// which keeps the result deterministic (no float atomics).
+#include "vst_common.h"
+#include "vst_hip.h"
+
+namespace {
+
+constexpr int BK = 16;  // pixels per k-tile
+constexpr int NT = 256;
+
+struct WgParams {
+  const float* a;    // [N][M][Ho][Wo]
+  const float* src;  // [N][Cs][Hs][Ws]
+  float* slab;       // [N*S][Mpad][Jpad]
+  int M, Mpad, J, Jpad;
+  int Cs, Hs, Ws, Ho, Wo;
+  int KS, gmode, stride, pad, up;
+  int S, chunk;
+  FastDiv fd_Wo, fd_Cs, fd_KS;
+};
+
+template <int WM, int TM, int WN, int TN>
+__global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int A_PER = BM * BK / NT;
+  constexpr int B_PER = BN * BK / NT;
+  constexpr int SA = BM + 1, SB = BN + 1;  // padded rows: transposed writes stay conflict-free
+
+  __shared__ float As[2][BK][SA];
+  __shared__ float Bs[2][BK][SB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int lo = lane & 31, hi = lane >> 5;
+  const int wm = wave / WN, wn = wave % WN;
+  const int j0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+  const int n = blockIdx.z / P.S;
+  const int sidx = blockIdx.z - n * P.S;
+  const int HWo = P.Ho * P.Wo;
+  const int r_begin = sidx * P.chunk;
+  const int r_end = min(HWo, r_begin + P.chunk);
+  const long plane = (long)P.Hs * P.Ws;
+  const float* a_n = P.a + (long)n * P.M * HWo;
+  const float* src_n = P.src + (long)n * P.Cs * plane;
+
+  const int rr = tid % BK;   // this thread's pixel row within a k-tile
+  const int cc = tid / BK;   // 0..7: base column (B) / base row (A)
+
+  // decode this thread's B columns once: (ci, kh, kw) packed, -1 if j >= J
+  int jdesc[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    int j = j0 + cc + i * (NT / BK);
+    int d = -1;
+    if (j < P.J) {
+      int tap = (int)fdiv((uint32_t)j, P.fd_Cs);
+      int ci = j - tap * P.Cs;
+      int kh = (int)fdiv((uint32_t)tap, P.fd_KS);
+      int kw = tap - kh * P.KS;
+      d = ci | (kh << 16) | (kw << 24);
+    }
+    jdesc[i] = d;
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float ra[A_PER], rb[B_PER];
+  const int ntiles = r_end > r_begin ? (r_end - r_begin + BK - 1) / BK : 0;
+  const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
+
+  auto load_tile = [&](int t) {
+    const int r = r_begin + t * BK + rr;
+    const bool rv = r < r_end;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int m = m0 + cc + i * (NT / BK);
+      ra[i] = (rv && m < P.M) ? a_n[(long)m * HWo + r] : 0.f;
+    }
+    int oy = 0, ox = 0;
+    if (rv) {
+      oy = (int)fdiv((uint32_t)r, P.fd_Wo);
+      ox = r - oy * P.Wo;
+    }
+    const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int d = jdesc[i];
+      float v = 0.f;
+      if (rv && d >= 0) {
+        int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
+        int y = by + kh, x = bx + kw;
+        bool ok = true;
+        if (P.gmode == 0) {
+          y = y < 0 ? -y : y;
+          y = y >= Hv ? 2 * Hv - 2 - y : y;
+          x = x < 0 ? -x : x;
+          x = x >= Wv ? 2 * Wv - 2 - x : x;
+        } else {
+          ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
+        }
+        if (ok) {
+          if (P.up == 2) {
+            y >>= 1;
+            x >>= 1;
+          }
+          v = src_n[(long)ci * plane + y * P.Ws + x];
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) As[buf][rr][cc + i * (NT / BK)] = ra[i];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) Bs[buf][rr][cc + i * (NT / BK)] = rb[i];
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1);
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[buf][2 * s + hi][(wm * TM + i) * 32 + lo];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[buf][2 * s + hi][(wn * TN + j) * 32 + lo];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  float* slab = P.slab + (long)blockIdx.z * P.Mpad * P.Jpad;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int jj = j0 + (wn * TN + j) * 32 + lo;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        slab[(long)m * P.Jpad + jj] = acc[i][j][r];
+      }
+  }
+}
+
+enum { W32 = 0, W64, W96, W128, W192 };
+static int wsel(int M) {
+  if (M <= 32) return W32;
+  if (M <= 64) return W64;
+  if (M <= 96) return W96;
+  if (M % 192 == 0 && M % 128 != 0) return W192;
+  return W128;
+}
+static int wbm(int c) {
+  const int bm[] = {32, 64, 96, 128, 192};
+  return bm[c];
+}
+constexpr int WBN = 128;
+
+// out[co][ci][kh][kw] (+)= scale * sum_z slab[z][co][(kh*KS+kw)*Cs+ci]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int M, int Mpad,
+                                    int Jpad, int Cs, int KS, float scale, int accumulate) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)M * Cs * KS * KS;
+  if (idx >= total) return;
+  int kw = (int)(idx % KS);
+  long t = idx / KS;
+  int kh = (int)(t % KS);
+  t /= KS;
+  int ci = (int)(t % Cs);
+  int co = (int)(t / Cs);
+  long off = (long)co * Jpad + (kh * KS + kw) * Cs + ci;
+  long zs = (long)Mpad * Jpad;
+  float s = 0.f;
+  for (int z = 0; z < nslab; ++z) s += slab[off + z * zs];
+  s *= scale;
+  if (accumulate) s += out[idx];
+  out[idx] = s;
+}
+
+// out[n][i][j] = scale * sum_{s<S} slab[n*S+s][i][j]
+__global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int N, int S, int C,
+                                   int Mpad, int Jpad, float scale) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * C * C;
+  if (idx >= total) return;
+  int j = (int)(idx % C);
+  long t = idx / C;
+  int i = (int)(t % C);
+  int n = (int)(t / C);
+  long zs = (long)Mpad * Jpad;
+  const float* p = slab + (long)n * S * zs + (long)i * Jpad + j;
+  float s = 0.f;
+  for (int z = 0; z < S; ++z) s += p[z * zs];
+  out[idx] = s * scale;
+}
+
+static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
+  switch (c) {
+    case W32: wgrad_kernel<1, 1, 4, 1><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad_kernel<1, 2, 4, 1><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad_kernel<1, 3, 4, 1><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad_kernel<2, 2, 2, 2><<<g, NT, 0, st>>>(P); break;
+    default: wgrad_kernel<2, 3, 2, 2><<<g, NT, 0, st>>>(P); break;
+  }
+}
+
+static int plan_splits(long tiles, int N, int HWo) {
+  // aim for ~1024 workgroups; at least 2 k-tiles per split
+  long want = 1024 / (tiles * N);
+  if (want < 1) want = 1;
+  long maxs = (HWo + 2 * BK - 1) / (2 * BK);
+  if (want > maxs) want = maxs;
+  return (int)(want < 1 ? 1 : want);
+}
+
+static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
+                  int KS, int gmode, int stride, int pad, int up, int S, hipStream_t st) {
+  WgParams P;
+  P.a = a;
+  P.src = src;
+  P.slab = slab;
+  P.M = M;
+  int c = wsel(M);
+  P.Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
+  P.J = KS * KS * Cs;
+  P.Jpad = (P.J + WBN - 1) / WBN * WBN;
+  P.Cs = Cs;
+  P.Hs = Hs;
+  P.Ws = Ws;
+  P.Ho = Ho;
+  P.Wo = Wo;
+  P.KS = KS;
+  P.gmode = gmode;
+  P.stride = stride;
+  P.pad = pad;
+  P.up = up;
+  P.S = S;
+  int HWo = Ho * Wo;
+  P.chunk = ((HWo + S - 1) / S + BK - 1) / BK * BK;
+  P.fd_Wo = make_fastdiv(Wo);
+  P.fd_Cs = make_fastdiv(Cs);
+  P.fd_KS = make_fastdiv(KS);
+  dim3 g(P.Jpad / WBN, P.Mpad / wbm(c), N * S);
+  launch_wg(c, g, st, P);
+  return vst_launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+// workspace (floats) needed by vst_conv_wgrad / vst_gram for a given problem
+long vst_wgrad_workspace(int N, int M, int J, int HWo) {
+  int c = wsel(M);
+  long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
+  long Jpad = (J + WBN - 1) / WBN * WBN;
+  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo);
+  return (long)N * S * Mpad * Jpad;
+}
+
+int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
+                   int Cout, int Ho, int Wo, int KS, int gmode, int stride, int pad, int up, int accumulate,
+                   void* stream) {
+  VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0);
+  VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
+  int c = wsel(Cout);
+  long Mpad = (Cout + wbm(c) - 1) / wbm(c) * wbm(c);
+  long J = (long)KS * KS * Cin;
+  long Jpad = (J + WBN - 1) / WBN * WBN;
+  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, Ho * Wo);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = run_wg(dy, x, workspace, N, Cout, Cin, Hs, Ws, Ho, Wo, KS, gmode, stride, pad, up, S, st);
+  if (rc) return rc;
+  long total = (long)Cout * J;
+  wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * S, Cout, (int)Mpad, (int)Jpad, Cin, KS,
+                                                           1.0f, accumulate);
+  return vst_launch_status();
+}
+
+// G[n] = F[n] F[n]^T * scale,  F = [N][C][H*W]
+int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, void* stream) {
+  VST_CHECK_ARG(f && g && workspace && N > 0 && C > 0 && HW > 0);
+  int c = wsel(C);
+  long Mpad = (C + wbm(c) - 1) / wbm(c) * wbm(c);
+  long Jpad = (C + WBN - 1) / WBN * WBN;
+  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HW);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = run_wg(f, f, workspace, N, C, C, 1, HW, 1, HW, 1, 1, 1, 0, 1, S, st);
+  if (rc) return rc;
+  long total = (long)N * C * C;
+  gram_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, g, N, S, C, (int)Mpad, (int)Jpad, scale);
+  return vst_launch_status();
+}
+
+}  // extern "C"

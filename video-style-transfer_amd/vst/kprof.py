@@ -1,0 +1,48 @@
+"""Live per-kernel-family timing with HIP events (used by bench.py for the roofline line).
+
+`conv_gemm` launches (forward + data-gradient implicit GEMM, `conv_gemm_kernel<...>`) record a
+start/stop event pair on the stream they are launched on, plus their algorithmic FLOPs
+(2 * N * Cout * Ho * Wo * Cin * k^2 of the reference convolution they implement, no padding or
+stride-2 zero-tap redundancy counted).
+"""
+import torch
+
+_active = None
+
+
+class KernelTimer:
+    def __init__(self):
+        self.records = []  # (start, stop, flops)
+
+    def __enter__(self):
+        global _active
+        _active = self
+        return self
+
+    def __exit__(self, *exc):
+        global _active
+        _active = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
+        flops = sum(f for _, _, f in self.records)
+        n = len(self.records)
+        return {"launches": n, "total_ms": ms, "avg_us": 1e3 * ms / max(n, 1), "flops": flops,
+                "tflops": flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0}
+
+
+def begin(flops):
+    if _active is None:
+        return None
+    s = torch.cuda.Event(enable_timing=True)
+    s.record()
+    return (s, flops)
+
+
+def end(tok):
+    if tok is None:
+        return
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    _active.records.append((tok[0], e, tok[1]))

@@ -1,0 +1,442 @@
+"""Autograd operators over libvst_hip.so.  Every forward AND backward runs a HIP kernel of the
+library on the current stream; there is no PyTorch-compute or CPU fallback (torch only allocates
+device memory).  Reference call sites each operator replaces are cited per class.
+"""
+import ctypes
+
+import torch
+from torch.autograd import Function
+
+from . import kprof
+from ._lib import VstError, lib, ptr, stream
+
+GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
+EPI_BIAS, EPI_RELU, EPI_TANH, EPI_MASK, EPI_ACCUM = 1, 2, 4, 8, 16
+LOSS_WS = 2048
+
+
+def _empty(shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+def _zeros(shape, like):
+    return torch.zeros(shape, device=like.device, dtype=torch.float32)
+
+
+def _check(t, name, ndim=None):
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise VstError(f"{name}: expected a float32 HIP tensor, got {t.dtype} on {t.device}")
+    if ndim is not None and t.dim() != ndim:
+        raise VstError(f"{name}: expected {ndim}-D, got shape {tuple(t.shape)}")
+    return t.contiguous()
+
+
+def pack_dims(M, K):
+    mp, kp = ctypes.c_int(), ctypes.c_int()
+    lib.vst_conv_pack_dims(M, K, ctypes.byref(mp), ctypes.byref(kp))
+    return mp.value, kp.value
+
+
+_PACK_CACHE = {}
+
+
+def packed_weight(w, transposed):
+    """Tap-major A[k][m] pack of a conv weight (cached on (storage, version) for frozen weights)."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), bool(transposed))
+    hit = _PACK_CACHE.get(key)
+    if hit is not None:
+        return hit
+    Cout, Cin, KS, _ = w.shape
+    M, Ck = (Cin, Cout) if transposed else (Cout, Cin)
+    Mpad, Kpad = pack_dims(M, KS * KS * Ck)
+    out = _empty((Kpad * Mpad,), w)
+    lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KS, int(transposed), Mpad, Kpad, stream())
+    if not w.requires_grad:
+        for k in [k for k in _PACK_CACHE if k[0] == key[0] and k[3] == key[3]]:
+            del _PACK_CACHE[k]
+        _PACK_CACHE[key] = out
+    return out
+
+
+def conv_out_hw(H, W, ks, stride, pad, up):
+    return (H * up + 2 * pad - ks) // stride + 1, (W * up + 2 * pad - ks) // stride + 1
+
+
+def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=None, out=None, aux=None, gmask=None,
+              a_batch_stride=0, mask=None, algo_flops=None):
+    N, Cs, Hs, Ws = src.shape
+    if out is None:
+        out = _empty((N, M, Ho, Wo), src)
+    tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * ks)
+    lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, ks * ks * Cs, Ho, Wo,
+                      ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
+    kprof.end(tok)
+    return out
+
+
+def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None):
+    """Input gradient of (upsample x`up` -> pad -> conv(stride)) given the conv-output grad gz."""
+    N, Cin, H, W = x_shape
+    Cout = w.shape[0]
+    Ho, Wo = gz.shape[2:]
+    flops = 2.0 * N * Cout * Ho * Wo * Cin * ks * ks
+    wp = packed_weight(w, transposed=True)
+    if pad_mode == "zero" and up == 1:
+        return conv_gemm(gz, wp, Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1, gmask=gmask, algo_flops=flops)
+    if pad_mode != "reflect":
+        raise VstError("dgrad: zero padding with upsampling is not on the reference path")
+    Hp, Wp = H * up + 2 * pad, W * up + 2 * pad
+    dpad = conv_gemm(gz, wp, Cin, ks, Hp, Wp, GM_TRANSPOSED, stride, 0, 1, gmask=gmask, algo_flops=flops)
+    dx = _empty(x_shape, gz)
+    lib.vst_fold_reflect(ptr(dpad), ptr(dx), N * Cin, H, W, pad, up, 0, stream())
+    return dx
+
+
+def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up):
+    N, Cin, H, W = x.shape
+    Cout = w_shape[0]
+    Ho, Wo = gz.shape[2:]
+    ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
+    dw = _empty(w_shape, x)
+    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks,
+                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, 0, stream())
+    return dw
+
+
+def channel_sum(x):
+    N, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    out = _empty((C,), x)
+    part = _empty((N * C,), x)
+    lib.vst_channel_sum(ptr(x), ptr(out), ptr(part), N, C, HW, 0, stream())
+    return out
+
+
+class Conv2dFn(Function):
+    """[nearest x`up` upsample] -> (reflect|zero) pad -> Conv2d(ks, stride) [+bias] [-> ReLU | ReCoNet tanh].
+    Replaces RC/network.py:72-75 (ConvLayer), 114-120 (UpsampleConvLayer), 83-85 (ConvTanh) and the
+    torchvision VGG Conv2d+ReLU pairs (RC/network.py:17-24, AA/vgg19.py:19-37)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act):
+        x = _check(x, "conv input", 4)
+        w = w.contiguous()
+        N, Cin, H, W = x.shape
+        Cout, _, ks, _ = w.shape
+        Ho, Wo = conv_out_hw(H, W, ks, stride, pad, up)
+        epi = (EPI_BIAS if b is not None else 0) | (EPI_RELU if act == "relu" else 0) | (EPI_TANH if act == "tanh" else 0)
+        aux = _empty((N, Cout, Ho, Wo), x) if act == "tanh" else None
+        out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
+                        stride, pad, up, epi=epi, bias=b.contiguous() if b is not None else None, aux=aux)
+        ctx.geom = (ks, stride, pad, pad_mode, up, act)
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y, t = ctx.saved_tensors
+        ks, stride, pad, pad_mode, up, act = ctx.geom
+        gy = gy.contiguous()
+        gz, gmask = gy, None
+        if act == "tanh":
+            gz = _empty(gy.shape, gy)
+            lib.vst_tanh_out_bwd(ptr(gy), ptr(t), ptr(gz), gy.numel(), gy[0, 0].numel(), 0, stream())
+        elif act == "relu":
+            gmask = y
+            if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+                gz = _empty(gy.shape, gy)
+                lib.vst_relu_bwd(ptr(gy), ptr(y), ptr(gz), gy.numel(), stream())
+                gmask = None
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask)
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = channel_sum(gz)
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, pad=0, pad_mode="zero", up=1, act=None):
+    return Conv2dFn.apply(x, w, b, stride, pad, pad_mode, up, act)
+
+
+class InstanceNormFn(Function):
+    """InstanceNorm2d(C, affine=True) [-> ReLU] [+ residual] (RC/network.py:91-97, 126-132, 140-150)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res, relu, eps):
+        x = _check(x, "instance_norm input", 4)
+        N, C, H, W = x.shape
+        y = _empty(x.shape, x)
+        stats = _empty((N * C * 2,), x)
+        res_c = res.contiguous() if res is not None else None
+        lib.vst_instnorm_fwd(ptr(x), ptr(w.contiguous()), ptr(b.contiguous()), ptr(res_c), ptr(y), ptr(stats), N, C,
+                             H * W, float(eps), int(relu), stream())
+        ctx.relu = relu
+        ctx.has_res = res is not None
+        ctx.save_for_backward(x, y if relu else None, stats, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, stats, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        N, C, H, W = x.shape
+        gx = _empty(x.shape, x)
+        gw = _empty((C,), x)
+        gb = _empty((C,), x)
+        part = _empty((N * C * 3,), x)
+        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(stats), ptr(w.contiguous()), ptr(gx), ptr(gw), ptr(gb), None,
+                             ptr(part), N, C, H * W, int(ctx.relu), 0, stream())
+        gres = gy if ctx.has_res else None
+        return gx, gw, gb, gres, None, None
+
+
+def instance_norm(x, w, b, relu=False, res=None, eps=1e-5):
+    return InstanceNormFn.apply(x, w, b, res, relu, eps)
+
+
+class MaxPool2x2Fn(Function):
+    """nn.MaxPool2d(2, 2) of the VGG feature stacks."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _check(x, "maxpool input", 4)
+        N, C, H, W = x.shape
+        y = _empty((N, C, H // 2, W // 2), x)
+        lib.vst_maxpool2x2_fwd(ptr(x), ptr(y), N * C, H, W, stream())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gx = _empty(x.shape, x)
+        lib.vst_maxpool2x2_bwd(ptr(x), ptr(gy.contiguous()), ptr(gx), N * C, H, W, stream())
+        return gx
+
+
+def maxpool2x2(x):
+    return MaxPool2x2Fn.apply(x)
+
+
+class WarpFn(Function):
+    """utilities.warp (RC/utilities.py:39-57); gradient w.r.t. x only (flow is data)."""
+
+    @staticmethod
+    def forward(ctx, x, flo):
+        x = _check(x, "warp input", 4)
+        flo = _check(flo, "flow", 4)
+        B, C, H, W = x.shape
+        if flo.shape != (B, 2, H, W):
+            raise VstError(f"warp: flow shape {tuple(flo.shape)} does not match {(B, 2, H, W)}")
+        out = _empty(x.shape, x)
+        lib.vst_warp_fwd(ptr(x), ptr(flo), ptr(out), B, C, H, W, stream())
+        ctx.save_for_backward(flo)
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (flo,) = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        gx = _zeros(ctx.shape, flo)
+        lib.vst_warp_bwd(ptr(gout.contiguous()), ptr(flo), ptr(gx), B, C, H, W, stream())
+        return gx, None
+
+
+def warp(x, flo):
+    return WarpFn.apply(x, flo)
+
+
+class GramFn(Function):
+    """gram_matrix (RC/utilities.py:93-98): F F^T / (C H W) per sample, MFMA split-K."""
+
+    @staticmethod
+    def forward(ctx, y):
+        y = _check(y, "gram input", 4)
+        N, C, H, W = y.shape
+        g = _empty((N, C, C), y)
+        ws = _empty((lib.vst_wgrad_workspace(N, C, C, H * W),), y)
+        lib.vst_gram(ptr(y), ptr(g), ptr(ws), N, C, H * W, 1.0 / (C * H * W), stream())
+        ctx.save_for_backward(y)
+        return g
+
+    @staticmethod
+    def backward(ctx, gg):
+        (y,) = ctx.saved_tensors
+        N, C, H, W = y.shape
+        Mpad, Kpad = pack_dims(C, C)
+        S = _empty((N * Kpad * Mpad,), y)
+        lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, 1.0 / (C * H * W), stream())
+        dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=Kpad * Mpad)
+        return dy.view(N, C, H, W)
+
+
+def gram_matrix(y):
+    return GramFn.apply(y)
+
+
+class VggNormalizeFn(Function):
+    """vgg_normalize's arithmetic (x/255 - mean)/std, out of place (AA/utilities.py:79-85 form)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _check(x, "vgg_normalize input", 4)
+        N, C, H, W = x.shape
+        if C != 3:
+            raise VstError("vgg_normalize expects 3 channels")
+        out = _empty(x.shape, x)
+        lib.vst_vgg_normalize(ptr(x), ptr(out), N, H * W, 0, stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = g.shape
+        gx = _empty(g.shape, g)
+        lib.vst_vgg_normalize_bwd(ptr(g.contiguous()), None, ptr(gx), N, H * W, stream())
+        return gx
+
+
+class VggNormalizeInplaceFn(Function):
+    """RC/utilities.py:101-106: `batch.div_(255)` mutates the argument, then returns (batch-mean)/std.
+    Returns (mutated x, normalized); the caller keeps the second."""
+
+    @staticmethod
+    def forward(ctx, x):
+        if not x.is_contiguous():
+            raise VstError("vgg_normalize (in place) needs a contiguous tensor")
+        _check(x, "vgg_normalize input", 4)
+        N, C, H, W = x.shape
+        out = _empty(x.shape, x)
+        lib.vst_vgg_normalize(ptr(x), ptr(out), N, H * W, 1, stream())
+        ctx.mark_dirty(x)
+        return x, out
+
+    @staticmethod
+    def backward(ctx, gscaled, gout):
+        N, C, H, W = gout.shape
+        gx = _empty(gout.shape, gout)
+        gs = gscaled.contiguous() if gscaled is not None else None
+        lib.vst_vgg_normalize_bwd(ptr(gout.contiguous()), ptr(gs), ptr(gx), N, H * W, stream())
+        return gx
+
+
+# ------------------------------------------------------------------ losses (0-d outputs)
+class MSEFn(Function):
+    """weight * mean((a - b)^2); b may be one sample broadcast over a's batch (gram_s.expand)."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight):
+        a = _check(a, "mse a")
+        b = _check(b, "mse b")
+        n, nb = a.numel(), b.numel()
+        if n % nb:
+            raise VstError("mse: b must broadcast over a's leading dim")
+        ws = _empty((LOSS_WS,), a)
+        st = _empty((3,), a)
+        lib.vst_mse_fwd(ptr(a), ptr(b), n, nb, float(weight), ptr(ws), ptr(st), stream())
+        ctx.save_for_backward(a, b, st)
+        return st[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, st = ctx.saved_tensors
+        ga = _empty(a.shape, a) if ctx.needs_input_grad[0] else None
+        gb = _empty(b.shape, b) if ctx.needs_input_grad[1] and a.numel() == b.numel() else None
+        if ctx.needs_input_grad[1] and gb is None:
+            raise VstError("mse: gradient for a broadcast target is not supported")
+        lib.vst_mse_bwd(ptr(a), ptr(b), a.numel(), b.numel(), ptr(g.contiguous()), ptr(st), ptr(ga), ptr(gb), stream())
+        return ga, gb, None
+
+
+def mse(a, b, weight=1.0):
+    return MSEFn.apply(a, b, weight)
+
+
+class MaskedTemporalFn(Function):
+    """mode 0: FTL (train_candy.py:97-106); mode 1: OTL (train_candy.py:109-123).  The reference's
+    nnz = torch.nonzero(mask).shape[0] is counted on device (no host sync)."""
+
+    @staticmethod
+    def forward(ctx, mode, a, b, c, d, mask, weight):
+        a, b = _check(a, "a", 4), _check(b, "b", 4)
+        mask = _check(mask, "mask")
+        N, C, H, W = a.shape
+        c = c.contiguous() if c is not None else None
+        d = d.contiguous() if d is not None else None
+        ws = _empty((LOSS_WS,), a)
+        st = _empty((3,), a)
+        lib.vst_masked_sqdiff_fwd(mode, ptr(a), ptr(b), ptr(c), ptr(d), ptr(mask), N, C, H * W, float(weight), ptr(ws),
+                                  ptr(st), stream())
+        ctx.mode = mode
+        ctx.save_for_backward(a, b, c, d, mask, st)
+        return st[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, c, d, mask, st = ctx.saved_tensors
+        N, C, H, W = a.shape
+        ga = _empty(a.shape, a) if ctx.needs_input_grad[1] else None
+        gb = _empty(b.shape, b) if ctx.needs_input_grad[2] else None
+        if ga is not None or gb is not None:
+            lib.vst_masked_sqdiff_bwd(ctx.mode, ptr(a), ptr(b), ptr(c), ptr(d), ptr(mask), N, C, H * W,
+                                      ptr(g.contiguous()), ptr(st), ptr(ga), ptr(gb), stream())
+        return None, ga, gb, None, None, None, None
+
+
+def feature_temporal_loss(f2, warped_f1, feature_mask, weight):
+    return MaskedTemporalFn.apply(0, f2, warped_f1, None, None, feature_mask, weight)
+
+
+def output_temporal_loss(s2, warped_s1, i2, warped_i1, mask, weight):
+    return MaskedTemporalFn.apply(1, s2, warped_s1, i2, warped_i1, mask, weight)
+
+
+class TVFn(Function):
+    """weight * sum(dx^2 + dy^2) over [:, :, :-1, :-1] (train_candy.py:141-145)."""
+
+    @staticmethod
+    def forward(ctx, s, weight):
+        s = _check(s, "tv input", 4)
+        N, C, H, W = s.shape
+        ws = _empty((LOSS_WS,), s)
+        st = _empty((3,), s)
+        lib.vst_tv_fwd(ptr(s), N * C, H, W, float(weight), ptr(ws), ptr(st), stream())
+        ctx.save_for_backward(s, st)
+        return st[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        s, st = ctx.saved_tensors
+        N, C, H, W = s.shape
+        gs = _empty(s.shape, s)
+        lib.vst_tv_bwd(ptr(s), N * C, H, W, ptr(g.contiguous()), ptr(st), ptr(gs), stream())
+        return gs, None
+
+
+def tv_loss(s, weight):
+    return TVFn.apply(s, weight)
+
+
+# ------------------------------------------------------------------ no-grad helpers
+def resize_bilinear(x, size, chscale=None, binarize=False):
+    x = _check(x, "resize input", 4)
+    N, C, H, W = x.shape
+    out = _empty((N, C) + tuple(size), x)
+    lib.vst_resize_bilinear(ptr(x), ptr(out), N * C, C, H, W, size[0], size[1], ptr(chscale), int(binarize), stream())
+    return out
+
+
+def flow_warp_mask(flo01, flo10, threshold=2.0):
+    """(B,2,H,W) x2 -> (B,H,W) 0/1, or (2,H,W) -> (H,W) like RC/utilities.py:60-90."""
+    single = flo01.dim() == 3
+    f01 = _check(flo01.unsqueeze(0) if single else flo01, "flo01", 4)
+    f10 = _check(flo10.unsqueeze(0) if single else flo10, "flo10", 4)
+    B, _, H, W = f01.shape
+    mask = _empty((B, H, W), f01)
+    lib.vst_flow_warp_mask(ptr(f01), ptr(f10), ptr(mask), B, H, W, float(threshold), stream())
+    return mask[0] if single else mask

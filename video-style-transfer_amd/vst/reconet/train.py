@@ -1,0 +1,100 @@
+"""ReCoNet training step (RC/train_single/train_candy.py:63-152) on MI355X, single- or multi-GPU.
+
+Semantics per step are the reference loop body's:
+  styled = ReCoNet(img1), ReCoNet(img2); vgg_normalize everything; Vgg16 of the 4 images;
+  FTL (feature-level masked temporal, train_candy.py:91-106), OTL (output-level, :109-123),
+  content (relu3_3 MSE, :126-129), style (Gram MSE over 4 layers, :132-138), TV (:141-145),
+  backward, Adam(lr=1e-3) step.
+Batching choices that do not change the arithmetic:
+  * both frames of a pair go through the stylizer / VGG as ONE batch of 2B (InstanceNorm is
+    per sample, so this is the reference's two passes fused);
+  * mean(a1) + mean(a2) over equal-size halves is evaluated as 2 * mean(a1 ++ a2).
+No host synchronisation inside a step: the nnz counts of the temporal masks stay on device and
+the loss terms are returned as device scalars.
+
+Multi-GPU: one process per GPU (torchrun), frame pairs sharded across ranks, one RCCL
+all-reduce (sum) of the flat gradient buffer per step, Adam applies the 1/world average.  The
+FTL/OTL denominators are rank-local nnz and TV is a sum, exactly as the reference computes them
+on its (per-rank) batch.
+"""
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ._flat import FlatParams
+
+LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
+
+
+class ReCoNetTrainer:
+    def __init__(self, model, vgg, style, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weights=None, temporal=True,
+                 process_group=None):
+        self.model = model
+        self.vgg = vgg
+        self.w = dict(LOSS_WEIGHTS if weights is None else weights)
+        self.temporal = temporal
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.flat = FlatParams(model)
+        self.step_count = 0
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        dev = self.flat.p.device
+        self.chscale_cache = {}
+        with torch.no_grad():
+            feats = vgg(ops.VggNormalizeFn.apply(style.to(dev)))
+            self.style_grams = [ops.gram_matrix(f) for f in feats]
+
+    def _chscale(self, Hf, Wf, H, W, dev):
+        key = (Hf, Wf, H, W)
+        if key not in self.chscale_cache:
+            self.chscale_cache[key] = torch.tensor([float(Wf) / W, float(Hf) / H], dtype=torch.float32, device=dev)
+        return self.chscale_cache[key]
+
+    def losses(self, frames, flow, mask):
+        """frames: [2, B, C, H, W] (img1 = frames[0], img2 = frames[1]); returns dict of 0-d tensors."""
+        w = self.w
+        _, B, C, H, W = frames.shape
+        x = frames.reshape(2 * B, C, H, W)
+        _, fmap, styled = self.model(x)
+        s_n = ops.VggNormalizeFn.apply(styled)
+        with torch.no_grad():
+            i_n = ops.VggNormalizeFn.apply(x if C == 3 else x[:, C - 3:].contiguous())
+        sf = self.vgg(s_n)
+        with torch.no_grad():
+            cf = self.vgg(i_n)
+        out = {}
+        if self.temporal:
+            Hf, Wf = fmap.shape[2:]
+            fflow = ops.resize_bilinear(flow, (Hf, Wf), chscale=self._chscale(Hf, Wf, H, W, flow.device))
+            warped_f = ops.warp(fmap[:B], fflow)
+            fmask = ops.resize_bilinear(mask.unsqueeze(1), (Hf, Wf), binarize=True)
+            out["FTL"] = ops.feature_temporal_loss(fmap[B:], warped_f, fmask, w["LAMBDA_F"])
+            warped_s = ops.warp(s_n[:B], flow)
+            with torch.no_grad():
+                warped_i = ops.warp(i_n[:B], flow)
+            out["OTL"] = ops.output_temporal_loss(s_n[B:], warped_s, i_n[B:], warped_i, mask, w["LAMBDA_O"])
+        out["CL"] = ops.mse(sf[2], cf[2], 2.0 * w["ALPHA"])
+        sl = None
+        for f, gs in zip(sf, self.style_grams):
+            term = ops.mse(ops.gram_matrix(f), gs, 2.0 * w["BETA"])
+            sl = term if sl is None else sl + term
+        out["SL"] = sl
+        out["RL"] = ops.tv_loss(s_n, w["GAMMA"])
+        total = None
+        for k in ("FTL", "OTL", "CL", "SL", "RL"):
+            if k in out:
+                total = out[k] if total is None else total + out[k]
+        out["loss"] = total
+        return out
+
+    def step(self, frames, flow, mask):
+        self.flat.zero_grad()
+        out = self.losses(frames, flow, mask)
+        out["loss"].backward()
+        gscale = 1.0
+        if self.world > 1:
+            dist.all_reduce(self.flat.g, op=dist.ReduceOp.SUM, group=self.pg)
+            gscale = 1.0 / self.world
+        self.step_count += 1
+        self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
+        return {k: v.detach() for k, v in out.items()}
