@@ -3,6 +3,7 @@ library on the current stream; there is no PyTorch-compute or CPU fallback (torc
 device memory).  Reference call sites each operator replaces are cited per class.
 """
 import ctypes
+import weakref
 
 import torch
 from torch.autograd import Function
@@ -37,24 +38,36 @@ def pack_dims(M, K):
     return mp.value, kp.value
 
 
-_PACK_CACHE = {}
+# frozen (requires_grad=False) weights: packs cached per weight OBJECT (weak keys, so a freed
+# tensor's entry dies with it and a new tensor at a recycled address never hits a stale pack),
+# validated against the tensor's version counter (in-place updates / load_state_dict re-pack).
+_PACK_CACHE = {}  # id(w) -> (weakref(w), {key: pack})
+
+
+def _cache_entry(w):
+    hit = _PACK_CACHE.get(id(w))
+    if hit is not None and hit[0]() is w:
+        return hit[1]
+    return {}
 
 
 def packed_weight(w, transposed):
-    """Tap-major A[k][m] pack of a conv weight (cached on (storage, version) for frozen weights)."""
-    key = (w.data_ptr(), w._version, tuple(w.shape), bool(transposed))
-    hit = _PACK_CACHE.get(key)
-    if hit is not None:
-        return hit
+    """Tap-major A[k][m] pack of a conv weight."""
+    key = (w._version, w.data_ptr(), bool(transposed))
+    if not w.requires_grad:
+        hit = _cache_entry(w).get(key)
+        if hit is not None:
+            return hit
     Cout, Cin, KS, _ = w.shape
     M, Ck = (Cin, Cout) if transposed else (Cout, Cin)
     Mpad, Kpad = pack_dims(M, KS * KS * Ck)
     out = _empty((Kpad * Mpad,), w)
     lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KS, int(transposed), Mpad, Kpad, stream())
     if not w.requires_grad:
-        for k in [k for k in _PACK_CACHE if k[0] == key[0] and k[3] == key[3]]:
-            del _PACK_CACHE[k]
-        _PACK_CACHE[key] = out
+        entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
+        entry[key] = out
+        wid = id(w)
+        _PACK_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _PACK_CACHE.pop(wid, None)), entry)
     return out
 
 
