@@ -35,12 +35,13 @@ const char* vst_strerror(int code);
  * and their autograd backward (dgrad / wgrad), the conv1 bias add and ConvTanh's
  * tanh(y/255)*150+127.5 (RC/network.py:83-85) as epilogues.
  *
- * Weights are re-packed tap-major into A[k][m] (k = (kh*KS+kw)*C + c, leading dim Mpad, rows
- * padded to Kpad with zeros):  forward: m = cout, c = cin;  transposed (dgrad): m = cin, c = cout.
+ * Weights are re-packed tap-major into A[k][m] (k = (kh*KW+kw)*C + c, leading dim Mpad, rows
+ * padded to Kpad with zeros):  forward: m = cout, c = cin;  transposed (dgrad): m = cin, c = cout;
+ * split_kh (row-split forward for tiny Cout): m = cout*KH + kh, k = kw*Cin + ci.
  */
 int vst_conv_pack_dims(int M, int K, int* Mpad, int* Kpad);
-int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KS, int transposed, int Mpad, int Kpad,
-                    void* stream);
+int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, int KW, int transposed, int split_kh,
+                    int Mpad, int Kpad, void* stream);
 /* out[n][m][Ho][Wo] = epi(sum_k A[k][m] * gather(src[n], k, pixel)).
  * gmode 0: reflect pad, 1: zero pad (forward gather y = oy*stride + kh - pad on the x`up` grid);
  * gmode 2: transposed gather (dgrad) ty = oy + pad - kh, valid iff ty % stride == 0.
@@ -49,8 +50,13 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KS, in
  * gmask (may be NULL, same shape as src): gathered values are zeroed where gmask <= 0 — the
  * ReLU backward of the layer that produced src, fused into the dgrad gather. */
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
-                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KS, int gmode, int stride, int pad,
+                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
                   int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream);
+/* row-split forward epilogue: out[n][co][y][x] = epi(bias + sum_kh P[n][co*KH+kh][y+kh][x]) where P
+ * [N][Cout*KH][H+KH-1][W] came from vst_conv_gemm(KH=1, KW=K, split_kh pack) over the padded rows
+ * (RC/network.py:169 deconv3 = ConvTanh(48, 3, 9): 27 GEMM rows instead of 3 padded to 32) */
+int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* aux, int N, int Cout, int KH, int H,
+                        int W, int epi, void* stream);
 /* adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hs*up+2p][Ws*up+2p] -> dx [NC][Hs][Ws] */
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
                      void* stream);
@@ -58,8 +64,12 @@ int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int 
  * workspace floats = vst_wgrad_workspace(N, Cout, KS*KS*Cin, Ho*Wo) */
 long vst_wgrad_workspace(int N, int M, int J, int HWo);
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
-                   int Cout, int Ho, int Wo, int KS, int gmode, int stride, int pad, int up, int accumulate,
+                   int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
                    void* stream);
+/* same for a stride-1 reflect-padded KxK conv with tiny Cout (row-split, GEMM rows (co,kh));
+ * workspace floats = vst_wgrad_workspace(N, Cout*K, K*Cin, (H+K-1)*W) */
+int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
+                            int W, int Cout, int K, int accumulate, void* stream);
 
 /* ---- Gram matrix (RC/utilities.py:93-98): G[n] = F[n] F[n]^T * scale ----------------------
  * workspace floats = vst_wgrad_workspace(N, C, C, HW) */

@@ -13,7 +13,7 @@ def test_header_parses_and_lists_entry_points():
                  "vst_instnorm_fwd", "vst_instnorm_bwd", "vst_masked_sqdiff_fwd", "vst_adam", "vst_strerror"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"
-    assert len(protos["vst_conv_gemm"][1]) == 23
+    assert len(protos["vst_conv_gemm"][1]) == 24
 
 
 @pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libvst_hip.so not built (run __graft_entry__.build())")
@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_side_argument_validation_without_gpu():
     """Entry points validate arguments before touching the device: bad calls fail with VST_EINVAL."""
     lib = _lib.lib.load()
-    assert lib.vst_conv_gemm(None, None, None, None, None, 1, 3, 8, 8, 4, 27, 8, 8, 3, 0, 1, 1, 1, 0, 0, None, None,
+    assert lib.vst_conv_gemm(None, None, None, None, None, 1, 3, 8, 8, 4, 27, 8, 8, 3, 3, 0, 1, 1, 1, 0, 0, None, None,
                              None) == -1
     mp, kp = ctypes.c_int(), ctypes.c_int()
     assert lib.vst_conv_pack_dims(48, 243, ctypes.byref(mp), ctypes.byref(kp)) == 0

@@ -1,0 +1,102 @@
+"""Microbenchmark of the implicit-GEMM conv kernel on the step's layer shapes, across library
+builds (tuning variants compiled with different -D flags).  Interleaved rounds in one process.
+
+    python tools/gemm_bench.py video-style-transfer_amd/vst/libvst_hip.so video-style-transfer_amd/vst/variants/*.so
+"""
+import ctypes
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, "video-style-transfer_amd")
+from vst._lib import _CTYPES, parse_header  # noqa: E402
+
+# name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gmode, stride, pad, up, algo_flops
+SHAPES = []
+
+
+def conv(name, N, Cin, H, W, Cout, k, stride=1, pad_mode="reflect", up=1):
+    pad = k // 2
+    Ho = (H * up + 2 * pad - k) // stride + 1
+    Wo = (W * up + 2 * pad - k) // stride + 1
+    fl = 2.0 * N * Cout * Ho * Wo * Cin * k * k
+    SHAPES.append((name + ".fwd", N, Cin, H, W, Cout, k, k, Ho, Wo, 0 if pad_mode == "reflect" else 1, stride, pad, up, fl))
+    if pad_mode == "zero":
+        SHAPES.append((name + ".dgrad", N, Cout, Ho, Wo, Cin, k, k, H, W, 2, stride, pad, 1, fl))
+    else:
+        SHAPES.append((name + ".dgrad", N, Cout, Ho, Wo, Cin, k, k, H * up + 2 * pad, W * up + 2 * pad, 2, stride, 0, 1, fl))
+
+
+conv("vgg1_2", 16, 64, 256, 512, 64, 3, pad_mode="zero")
+conv("vgg2_2", 16, 128, 128, 256, 128, 3, pad_mode="zero")
+conv("vgg3_2", 16, 256, 64, 128, 256, 3, pad_mode="zero")
+conv("vgg4_2", 16, 512, 32, 64, 512, 3, pad_mode="zero")
+conv("res", 16, 192, 64, 128, 192, 3)
+conv("deconv1", 16, 192, 64, 128, 96, 3, up=2)
+conv("deconv2", 16, 96, 128, 256, 48, 3, up=2)
+conv("conv2", 16, 48, 256, 512, 96, 3, stride=2)
+conv("conv3", 16, 96, 128, 256, 192, 3, stride=2)
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    for name, (rt, argts) in parse_header().items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = _CTYPES[rt] if rt != "char*" else ctypes.c_char_p
+        fn.argtypes = [_CTYPES[a] for a in argts]
+    return lib
+
+
+def main():
+    paths = sys.argv[1:]
+    libs = [load(p) for p in paths]
+    dev = "cuda"
+    st = torch.cuda.current_stream().cuda_stream
+    only = None
+    results = {(p, s[0]): [] for p in paths for s in SHAPES}
+    bufs = {}
+    for s in SHAPES:
+        name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
+        src = torch.randn(N, Cs, Hs, Ws, device=dev)
+        out = torch.empty(N, M, Ho, Wo, device=dev)
+        bufs[name] = (src, out)
+    for rnd in range(3):
+        for p, lib in zip(paths, libs):
+            for s in SHAPES:
+                name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
+                if only and only not in name:
+                    continue
+                src, out = bufs[name]
+                mp, kp = ctypes.c_int(), ctypes.c_int()
+                lib.vst_conv_pack_dims(M, KH * KW * Cs, ctypes.byref(mp), ctypes.byref(kp))
+                wp = torch.randn(kp.value * mp.value, device=dev) * 0.05
+                args = (src.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cs, Hs, Ws, M, KH * KW * Cs, Ho, Wo,
+                        KH, KW, gm, stride, pad, up, 0, 0, None, None, st)
+                for _ in range(2):
+                    assert lib.vst_conv_gemm(*args) == 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                reps = 5
+                for _ in range(reps):
+                    lib.vst_conv_gemm(*args)
+                e1.record()
+                torch.cuda.synchronize()
+                results[(p, name)].append(e0.elapsed_time(e1) / reps)
+    hdr = "shape".ljust(16) + "".join(p.split("/")[-1].replace("libvst_hip", "").replace(".so", "")[:14].rjust(16) for p in paths)
+    print(hdr)
+    tot = {p: 0.0 for p in paths}
+    for s in SHAPES:
+        line = s[0].ljust(16)
+        for p in paths:
+            ms = statistics.median(results[(p, s[0])])
+            tot[p] += ms
+            line += f"{ms*1e3:8.0f}us{s[-1]/ms/1e9:5.0f}TF".rjust(16)
+        print(line)
+    print("total".ljust(16) + "".join(f"{tot[p]:14.2f}ms" for p in paths))
+
+
+if __name__ == "__main__":
+    main()

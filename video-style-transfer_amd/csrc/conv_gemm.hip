@@ -8,7 +8,7 @@
 //   * data-gradient (transposed gather, stride-divisibility test) into the padded/virtual input
 //     grid, followed by `fold_reflect` (reflection-pad + upsample adjoint),
 //   * 1x1 products with a per-image A (Gram backward dF = S F, RC/utilities.py:93-98).
-// K is ordered tap-major / channel-minor, k = (kh*KS + kw)*Cs + c, so when Cs % 16 == 0 a whole
+// K is ordered tap-major / channel-minor, k = (kh*KW + kw)*Cs + c, so when Cs % 16 == 0 a whole
 // 16-deep k-tile shares one tap and the reflect/zero/upsample index math is done once per tile.
 //
 // Tile: 4 waves (256 threads); each wave owns TM x TN 32x32 accumulators (WM x WN waves).
@@ -19,7 +19,15 @@
 
 namespace {
 
-constexpr int BK = 16;
+__device__ __forceinline__ f32x4 mk4(float a, float b, float c, float d) {
+  f32x4 v = {a, b, c, d};
+  return v;
+}
+
+#ifndef VST_CONV_BK
+#define VST_CONV_BK 16
+#endif
+constexpr int BK = VST_CONV_BK;  // k-tile depth (multiple of 16)
 constexpr int NT = 256;
 
 struct ConvParams {
@@ -34,56 +42,58 @@ struct ConvParams {
   int Cs, Hs, Ws;
   int M, Mpad, K, Kpad;
   int Ho, Wo;
-  int KS, gmode, stride, pad, up;
+  int KH, KW, gmode, stride, pad, up;
   int epi;
-  FastDiv fd_Wo, fd_Cs, fd_KS;
+  FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
 enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16 };
 
 // source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
+// (select-only arithmetic: no divergent branches inside the k loop)
 __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox, int kh, int kw) {
   if (P.gmode == GM_TRANSPOSED) {
     int ty = oy + P.pad - kh, tx = ox + P.pad - kw;
-    if (ty < 0 || tx < 0) return -1;
+    bool ok = ty >= 0 && tx >= 0;
     if (P.stride == 2) {
-      if ((ty | tx) & 1) return -1;
+      ok = ok && !((ty | tx) & 1);
       ty >>= 1;
       tx >>= 1;
     }
-    if (ty >= P.Hs || tx >= P.Ws) return -1;
-    return ty * P.Ws + tx;
+    ok = ok && ty < P.Hs && tx < P.Ws;
+    return ok ? ty * P.Ws + tx : -1;
   }
-  int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
+  const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
   int y = oy * P.stride + kh - P.pad, x = ox * P.stride + kw - P.pad;
+  bool ok = true;
   if (P.gmode == GM_REFLECT) {
-    y = y < 0 ? -y : y;
+    y = abs(y);
     y = y >= Hv ? 2 * Hv - 2 - y : y;
-    x = x < 0 ? -x : x;
+    x = abs(x);
     x = x >= Wv ? 2 * Wv - 2 - x : x;
-  } else if (y < 0 || y >= Hv || x < 0 || x >= Wv) {
-    return -1;
+  } else {
+    ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
   }
-  if (P.up == 2) {
-    y >>= 1;
-    x >>= 1;
-  }
-  return y * P.Ws + x;
+  const int sh = P.up - 1;
+  return ok ? (y >> sh) * P.Ws + (x >> sh) : -1;
 }
 
-template <int WM, int TM, int WN, int TN, bool CFAST>
-__global__ __launch_bounds__(NT) void conv_gemm_kernel(ConvParams P) {
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW>
+__global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int A_F4 = BK * BM / 4;          // float4 per A tile
   constexpr int A_PER = (A_F4 + NT - 1) / NT;
   constexpr int ROWSTEP = NT / BN;           // B rows covered per pass
   constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
+  constexpr int KSTEPS = BK / 2;
   static_assert(NT % BN == 0 && BK % ROWSTEP == 0, "tile");
 
-  __shared__ float As[2][BK][BM];
-  __shared__ float Bs[2][BK][BN];
+  static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
+  constexpr int LS = 20;  // LDS row: [hi][s] 16 floats + 4 pad (conflict-free ds_read_b128 / ds_write_b128)
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -95,7 +105,7 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(ConvParams P) {
   const int HWo = P.Ho * P.Wo;
   const long plane = (long)P.Hs * P.Ws;
   const float* src_n = P.src + (long)n * P.Cs * plane;
-  const float* gm_n = P.gmask ? P.gmask + (long)n * P.Cs * plane : nullptr;
+  const float* gm_n = GM ? P.gmask + (long)n * P.Cs * plane : nullptr;
   const float* A = P.wpack + (long)n * P.a_batch_stride;
 
   // this thread's B column (fixed for the whole k loop)
@@ -117,53 +127,64 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(ConvParams P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float4 ra[A_PER];
+  f32x4 ra[A_PER];
   float rb[B_PER];
+  float rg[GM ? B_PER : 1];
+  // buffer descriptors over this image's source planes (wave-uniform inputs only)
+  const int plane_i = P.Hs * P.Ws;
+  const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane_i * 4u;
+  constexpr int OOR = 0x7ffffff0;  // any offset >= num_records reads 0
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc((void*)src_n, (short)0, (int)src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t gsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(GM ? gm_n : src_n), (short)0, (int)src_bytes, 0x00020000);
   const int ntiles = P.Kpad / BK;
 
+  // Issue every global load of tile t without branches (out-of-range taps read a clamped, valid
+  // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
   auto load_tile = [&](int t) {
     const int k0 = t * BK;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
-      if (idx < A_F4) {
-        int kk = idx / (BM / 4), mm = (idx % (BM / 4)) * 4;
-        ra[i] = *reinterpret_cast<const float4*>(A + (long)(k0 + kk) * P.Mpad + m0 + mm);
+      if (A_F4 % NT == 0 || idx < A_F4) {
+        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * 16 + 4 * idx);
       }
     }
     if (CFAST) {
-      // whole tile shares one tap (Cs % BK == 0): scalar tap decode, one offset per thread
-      const int tap = k0 / P.Cs;
-      const int c0 = k0 - tap * P.Cs;
-      const int kh = tap / P.KS, kw = tap - (tap / P.KS) * P.KS;
-      int off = pvalid ? gather_offset(P, oy, ox, kh, kw) : -1;
-      const long base = (long)(c0 + brow0) * plane + off;
+      // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
+      // offset per thread per group; out-of-range taps use an offset past the buffer end, which
+      // the buffer-load range check turns into 0 (no branch, no select)
+      constexpr int NG = BK / 16, PER_G = B_PER / NG;
 #pragma unroll
-      for (int i = 0; i < B_PER; ++i) {
-        float v = 0.f;
-        if (off >= 0) {
-          v = src_n[base + (long)i * ROWSTEP * plane];
-          if (gm_n && !(gm_n[base + (long)i * ROWSTEP * plane] > 0.f)) v = 0.f;
+      for (int g = 0; g < NG; ++g) {
+        const int kg = k0 + 16 * g;
+        const int tap = kg / P.Cs;
+        const int c0 = kg - tap * P.Cs;
+        const int kh = tap / P.KW, kw = tap - (tap / P.KW) * P.KW;
+        const int off0 = gather_offset(P, oy, ox, kh, kw);
+        const bool ok = pvalid && kg < P.K && off0 >= 0;
+        const int vo = ok ? ((c0 + brow0) * plane_i + off0) * 4 : OOR;
+        const int vstep = ok ? ROWSTEP * plane_i * 4 : 0;
+#pragma unroll
+        for (int i = 0; i < PER_G; ++i) {
+          rb[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
+          if (GM) rg[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo + i * vstep, 0, 0));
         }
-        rb[i] = v;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        int k = k0 + brow0 + i * ROWSTEP;
-        float v = 0.f;
-        if (pvalid && k < P.K) {
-          int tap = (int)fdiv((uint32_t)k, P.fd_Cs);
-          int c = k - tap * P.Cs;
-          int kh = (int)fdiv((uint32_t)tap, P.fd_KS);
-          int kw = tap - kh * P.KS;
-          int off = gather_offset(P, oy, ox, kh, kw);
-          if (off >= 0) {
-            v = src_n[(long)c * plane + off];
-            if (gm_n && !(gm_n[(long)c * plane + off] > 0.f)) v = 0.f;
-          }
-        }
-        rb[i] = v;
+        const int k = k0 + brow0 + i * ROWSTEP;
+        const int kc = k < P.K ? k : 0;
+        const int tap = (int)fdiv((uint32_t)kc, P.fd_Cs);
+        const int c = kc - tap * P.Cs;
+        const int kh = (int)fdiv((uint32_t)tap, P.fd_KW);
+        const int kw = tap - kh * P.KW;
+        const int off0 = gather_offset(P, oy, ox, kh, kw);
+        const bool ok = pvalid && k < P.K && off0 >= 0;
+        const int vo = ok ? (c * plane_i + off0) * 4 : OOR;
+        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, 0, 0));
+        if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, 0, 0));
       }
     }
   };
@@ -171,13 +192,24 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(ConvParams P) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
-      if (idx < A_F4) {
-        int kk = idx / (BM / 4), mm = (idx % (BM / 4)) * 4;
-        *reinterpret_cast<float4*>(&As[buf][kk][mm]) = ra[i];
+      if (A_F4 % NT == 0 || idx < A_F4) {
+        *reinterpret_cast<f32x4*>(&As[buf][idx >> 2][(idx & 3) * 4]) = ra[i];
       }
     }
+    float bv[B_PER];
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) Bs[buf][brow0 + i * ROWSTEP][bcol] = rb[i];
+    for (int i = 0; i < B_PER; ++i) bv[i] = GM ? (rg[i] > 0.f ? rb[i] : 0.f) : rb[i];
+    if (ROWSTEP == 2) {  // rows k = brow0 + 2i: hi = brow0, s = i -> 8 contiguous floats
+      float* d = &Bs[buf][bcol][brow0 * 8];
+      *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[1], bv[2], bv[3]);
+      *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[4], bv[5], bv[6], bv[7]);
+    } else {             // ROWSTEP == 1: rows k = i
+      float* d = &Bs[buf][bcol][0];
+      *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[2], bv[4], bv[6]);
+      *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[8], bv[10], bv[12], bv[14]);
+      *reinterpret_cast<f32x4*>(d + 8) = mk4(bv[1], bv[3], bv[5], bv[7]);
+      *reinterpret_cast<f32x4*>(d + 12) = mk4(bv[9], bv[11], bv[13], bv[15]);
+    }
   };
 
   load_tile(0);
@@ -187,18 +219,27 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(ConvParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
+    // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
+    f32x4 a[TM][2], b[TN][2];
 #pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      float a[TM], b[TN];
+    for (int i = 0; i < TM; ++i) {
+      const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+      a[i][0] = *reinterpret_cast<const f32x4*>(r);
+      a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+    }
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[buf][2 * s + hi][(wm * TM + i) * 32 + lo];
+    for (int j = 0; j < TN; ++j) {
+      const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+      b[j][0] = *reinterpret_cast<const f32x4*>(r);
+      b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+    }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[buf][2 * s + hi][(wn * TN + j) * 32 + lo];
+    for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     if (t + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
   }
@@ -249,35 +290,55 @@ static int cfg_bm(int c) {
 }
 static int cfg_bn(int c) { return c == T32 ? 256 : 128; }
 
-template <bool CF>
+#ifndef VST_MINW_T128
+#define VST_MINW_T128 4
+#endif
+#ifndef VST_MINW_T192
+#define VST_MINW_T192 2
+#endif
+#ifndef VST_MINW_SMALL
+#define VST_MINW_SMALL 4
+#endif
+
+template <bool CF, bool GMK>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
   switch (cfg) {
-    case T32: conv_gemm_kernel<1, 1, 4, 2, CF><<<grid, NT, 0, st>>>(P); break;
-    case T64: conv_gemm_kernel<1, 2, 4, 1, CF><<<grid, NT, 0, st>>>(P); break;
-    case T96: conv_gemm_kernel<1, 3, 4, 1, CF><<<grid, NT, 0, st>>>(P); break;
-    case T128: conv_gemm_kernel<2, 2, 2, 2, CF><<<grid, NT, 0, st>>>(P); break;
-    default: conv_gemm_kernel<2, 3, 2, 2, CF><<<grid, NT, 0, st>>>(P); break;
+    case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3><<<grid, NT, 0, st>>>(P); break;
+    case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
+    case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
+    case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, VST_MINW_T128><<<grid, NT, 0, st>>>(P); break;
+    default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192><<<grid, NT, 0, st>>>(P); break;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
-                                   int transposed, int Mpad, int Kpad) {
+// fwd:        A[k = (kh*KW+kw)*Cin + ci][m = co]
+// transposed: A[k = (kh*KW+kw)*Cout + co][m = ci]        (data gradient)
+// split_kh:   A[k = kw*Cin + ci][m = co*KH + kh]          (row-split GEMM for tiny Cout, see vst_hip.h)
+__global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KH,
+                                   int KW, int transposed, int split_kh, int Mpad, int Kpad) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)Mpad * Kpad;
   if (idx >= total) return;
   int m = (int)(idx % Mpad);
   int k = (int)(idx / Mpad);
-  int Ck = transposed ? Cout : Cin;   // channel count inside the k index
-  int Mm = transposed ? Cin : Cout;
   float v = 0.f;
-  if (m < Mm && k < KS * KS * Ck) {
-    int tap = k / Ck, c = k % Ck;
-    int kh = tap / KS, kw = tap % KS;
-    int co = transposed ? c : m, ci = transposed ? m : c;
-    v = w[(((long)co * Cin + ci) * KS + kh) * KS + kw];
+  if (split_kh) {
+    if (m < Cout * KH && k < KW * Cin) {
+      int co = m / KH, kh = m % KH, kw = k / Cin, ci = k % Cin;
+      v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
+    }
+  } else {
+    int Ck = transposed ? Cout : Cin;  // channel count inside the k index
+    int Mm = transposed ? Cin : Cout;
+    if (m < Mm && k < KH * KW * Ck) {
+      int tap = k / Ck, c = k % Ck;
+      int kh = tap / KW, kw = tap % KW;
+      int co = transposed ? c : m, ci = transposed ? m : c;
+      v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
+    }
   }
-  out[idx] = v;
+  out[apack_index(k, m, Mpad)] = v;
 }
 
 // adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hv+2p][Wv+2p] -> dx [NC][Hs][Ws]
@@ -337,20 +398,20 @@ int vst_conv_pack_dims(int M, int K, int* Mpad, int* Kpad) {
   return VST_OK;
 }
 
-int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KS, int transposed, int Mpad, int Kpad,
-                    void* stream) {
-  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0);
+int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, int KW, int transposed, int split_kh,
+                    int Mpad, int Kpad, void* stream) {
+  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && !(transposed && split_kh));
   long total = (long)Mpad * Kpad;
-  pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, transposed, Mpad,
+  pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad,
                                                                             Kpad);
   return vst_launch_status();
 }
 
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
-                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KS, int gmode, int stride, int pad,
+                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
                   int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream) {
   VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
-  VST_CHECK_ARG(K == KS * KS * Cs);
+  VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
   VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
   VST_CHECK_ARG(!((epi & EPI_BIAS) && !bias) && !((epi & EPI_MASK) && !mask));
   if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad < Ws * up);
@@ -374,7 +435,8 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   P.Kpad = (K + BK - 1) / BK * BK;
   P.Ho = Ho;
   P.Wo = Wo;
-  P.KS = KS;
+  P.KH = KH;
+  P.KW = KW;
   P.gmode = gmode;
   P.stride = stride;
   P.pad = pad;
@@ -382,13 +444,14 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   P.epi = epi;
   P.fd_Wo = make_fastdiv(Wo);
   P.fd_Cs = make_fastdiv(Cs);
-  P.fd_KS = make_fastdiv(KS);
+  P.fd_KW = make_fastdiv(KW);
   dim3 grid(ceil_div((long)Ho * Wo, bn), P.Mpad / bm, N);
-  bool cfast = (Cs % BK) == 0;
+  bool cfast = (Cs % 16) == 0;
+  hipStream_t st = (hipStream_t)stream;
   if (cfast)
-    launch_cfg<true>(cfg, grid, (hipStream_t)stream, P);
+    gmask ? launch_cfg<true, true>(cfg, grid, st, P) : launch_cfg<true, false>(cfg, grid, st, P);
   else
-    launch_cfg<false>(cfg, grid, (hipStream_t)stream, P);
+    gmask ? launch_cfg<false, true>(cfg, grid, st, P) : launch_cfg<false, false>(cfg, grid, st, P);
   return vst_launch_status();
 }
 
@@ -402,3 +465,46 @@ int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Row-split forward for convs with few output channels (ConvTanh 48->3, k9, RC/network.py:169):
+// the GEMM computes P[(co,kh)][q_y][x] = sum_{ci,kw} W[co][ci][kh][kw] Xpad[ci][q_y][x+kw] over the
+// (H+KH-1) padded rows (27 useful rows of 32 instead of 3), this kernel finishes
+//   out[co][y][x] = epi(bias[co] + sum_kh P[(co,kh)][y+kh][x])
+namespace {
+__global__ void rowsplit_reduce_kernel(const float* __restrict__ P, const float* __restrict__ bias,
+                                       float* __restrict__ out, float* __restrict__ aux, int N, int Cout, int KH, int H,
+                                       int W, int epi) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * Cout * H * W;
+  if (idx >= total) return;
+  int x = (int)(idx % W);
+  long t = idx / W;
+  int y = (int)(t % H);
+  t /= H;
+  int co = (int)(t % Cout);
+  long n = t / Cout;
+  const int Hq = H + KH - 1;
+  const float* p = P + ((n * Cout + co) * KH * (long)Hq + y) * W + x;
+  float s = 0.f;
+  for (int kh = 0; kh < KH; ++kh) s += p[((long)kh * Hq + kh) * W];
+  float v = s;
+  if (epi & EPI_BIAS) v += bias[co];
+  if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+  if (epi & EPI_TANH) {
+    const float th = tanhf(v / 255.0f);
+    if (aux) aux[idx] = th;
+    v = th * 150.0f + 127.5f;
+  }
+  out[idx] = v;
+}
+}  // namespace
+
+extern "C" int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* aux, int N, int Cout, int KH,
+                                   int H, int W, int epi, void* stream) {
+  VST_CHECK_ARG(P && out && N > 0 && Cout > 0 && KH > 0 && H > 0 && W > 0 && !((epi & EPI_BIAS) && !bias));
+  long total = (long)N * Cout * H * W;
+  rowsplit_reduce_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(P, bias, out, aux, N, Cout, KH, H, W,
+                                                                                epi);
+  return vst_launch_status();
+}

@@ -185,7 +185,7 @@ __global__ void tv_bwd_kernel(const float* __restrict__ s, long NC, int H, int W
   }
 }
 
-// S[n][k][m] = scale * (g[n][k][m] + g[n][m][k]) for k, m < C; zero in the [Kpad][Mpad] padding
+// S[n](k, m) = scale * (g[n][k][m] + g[n][m][k]) for k, m < C, zero padded, in the packed A layout
 // (bmm backward of F F^T: dF = (gG + gG^T) F / (C H W); S is symmetric so [k][m] is the packed A)
 __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict__ S, int N, int C, int Kpad, int Mpad,
                                   float scale) {
@@ -200,7 +200,7 @@ __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict
     const float* gn = g + n * C * C;
     v = (gn[k * C + m] + gn[m * C + k]) * scale;
   }
-  S[idx] = v;
+  S[n * (long)Kpad * Mpad + apack_index(k, m, Mpad)] = v;
 }
 
 // ReLU backward: gx = gy * (y > 0)

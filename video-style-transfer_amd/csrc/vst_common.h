@@ -55,3 +55,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Packed GEMM A operand ("weights"), k-tiles of 16: element (k, m) lives at
+//   ((k/16) * Mpad + m) * 16 + (k%2) * 8 + (k%16)/2
+// so one MFMA lane's 8 values of a k-tile (k = 2s + hi, s = 0..7, for v_mfma_f32_32x32x2_f32)
+// are contiguous: two ds_read_b128 per 32-row fragment, and a k-tile of BM rows is one
+// contiguous BM*16-float block in global memory.
+__host__ __device__ inline long apack_index(int k, int m, int Mpad) {
+  return ((long)(k >> 4) * Mpad + m) * 16 + (k & 1) * 8 + ((k & 15) >> 1);
+}

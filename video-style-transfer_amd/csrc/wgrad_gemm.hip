@@ -3,7 +3,7 @@
 //   slab[z][m][j] = sum_{r in chunk z}  A[n][m][r] * gather(src[n], j, r)
 //
 // Serves the conv weight gradient (dW[co][(kh,kw,ci)], RC/network.py:70 Conv2d backward) and the
-// Gram matrix F F^T (RC/utilities.py:93-98, KS = 1, A == src).  The reduction runs over output
+// Gram matrix F F^T (RC/utilities.py:93-98, 1x1, A == src).  The reduction runs over output
 // pixels r of ONE image per block (grid.z = N * S splits); partial slabs are summed by
 // `wgrad_reduce` (into PyTorch's [co][ci][kh][kw] order) or `gram_reduce` (per image, scaled),
 // which keeps the result deterministic (no float atomics).
@@ -21,9 +21,10 @@ struct WgParams {
   float* slab;       // [N*S][Mpad][Jpad]
   int M, Mpad, J, Jpad;
   int Cs, Hs, Ws, Ho, Wo;
-  int KS, gmode, stride, pad, up;
+  int KH, KW, gmode, stride, pad, up;
   int S, chunk;
-  FastDiv fd_Wo, fd_Cs, fd_KS;
+  int asplit, Ha;  // row-split A gather: m = co*asplit + kh reads a[co][oy-kh][ox] (a has Ha rows)
+  FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
 template <int WM, int TM, int WN, int TN>
@@ -49,7 +50,8 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
   const int r_begin = sidx * P.chunk;
   const int r_end = min(HWo, r_begin + P.chunk);
   const long plane = (long)P.Hs * P.Ws;
-  const float* a_n = P.a + (long)n * P.M * HWo;
+  const long a_img = P.asplit ? (long)(P.M / P.asplit) * P.Ha * P.Wo : (long)P.M * HWo;
+  const float* a_n = P.a + (long)n * a_img;
   const float* src_n = P.src + (long)n * P.Cs * plane;
 
   const int rr = tid % BK;   // this thread's pixel row within a k-tile
@@ -64,8 +66,8 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
     if (j < P.J) {
       int tap = (int)fdiv((uint32_t)j, P.fd_Cs);
       int ci = j - tap * P.Cs;
-      int kh = (int)fdiv((uint32_t)tap, P.fd_KS);
-      int kw = tap - kh * P.KS;
+      int kh = (int)fdiv((uint32_t)tap, P.fd_KW);
+      int kw = tap - kh * P.KW;
       d = ci | (kh << 16) | (kw << 24);
     }
     jdesc[i] = d;
@@ -86,15 +88,25 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
   auto load_tile = [&](int t) {
     const int r = r_begin + t * BK + rr;
     const bool rv = r < r_end;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int m = m0 + cc + i * (NT / BK);
-      ra[i] = (rv && m < P.M) ? a_n[(long)m * HWo + r] : 0.f;
-    }
     int oy = 0, ox = 0;
     if (rv) {
       oy = (int)fdiv((uint32_t)r, P.fd_Wo);
       ox = r - oy * P.Wo;
+    }
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int m = m0 + cc + i * (NT / BK);
+      float v = 0.f;
+      if (rv && m < P.M) {
+        if (P.asplit) {
+          int co = m / P.asplit, kh = m - co * P.asplit;
+          int yy = oy - kh;
+          if (yy >= 0 && yy < P.Ha) v = a_n[((long)co * P.Ha + yy) * P.Wo + ox];
+        } else {
+          v = a_n[(long)m * HWo + r];
+        }
+      }
+      ra[i] = v;
     }
     const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
 #pragma unroll
@@ -183,19 +195,21 @@ static int wbm(int c) {
 }
 constexpr int WBN = 128;
 
-// out[co][ci][kh][kw] (+)= scale * sum_z slab[z][co][(kh*KS+kw)*Cs+ci]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int M, int Mpad,
-                                    int Jpad, int Cs, int KS, float scale, int accumulate) {
+// out[co][ci][kh][kw] (+)= scale * sum_z slab[z][co][(kh*KW+kw)*Cs+ci]
+// rowsplit: slab rows are m = co*KH + kh and columns j = kw*Cs + ci
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int Cout,
+                                    int Mpad, int Jpad, int Cs, int KH, int KW, int rowsplit, float scale,
+                                    int accumulate) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)M * Cs * KS * KS;
+  long total = (long)Cout * Cs * KH * KW;
   if (idx >= total) return;
-  int kw = (int)(idx % KS);
-  long t = idx / KS;
-  int kh = (int)(t % KS);
-  t /= KS;
+  int kw = (int)(idx % KW);
+  long t = idx / KW;
+  int kh = (int)(t % KH);
+  t /= KH;
   int ci = (int)(t % Cs);
   int co = (int)(t / Cs);
-  long off = (long)co * Jpad + (kh * KS + kw) * Cs + ci;
+  long off = rowsplit ? (long)(co * KH + kh) * Jpad + kw * Cs + ci : (long)co * Jpad + (kh * KW + kw) * Cs + ci;
   long zs = (long)Mpad * Jpad;
   float s = 0.f;
   for (int z = 0; z < nslab; ++z) s += slab[off + z * zs];
@@ -241,7 +255,7 @@ static int plan_splits(long tiles, int N, int HWo) {
 }
 
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
-                  int KS, int gmode, int stride, int pad, int up, int S, hipStream_t st) {
+                  int KH, int KW, int gmode, int stride, int pad, int up, int S, int asplit, int Ha, hipStream_t st) {
   WgParams P;
   P.a = a;
   P.src = src;
@@ -249,71 +263,99 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
   P.M = M;
   int c = wsel(M);
   P.Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
-  P.J = KS * KS * Cs;
+  P.J = KH * KW * Cs;
   P.Jpad = (P.J + WBN - 1) / WBN * WBN;
   P.Cs = Cs;
   P.Hs = Hs;
   P.Ws = Ws;
   P.Ho = Ho;
   P.Wo = Wo;
-  P.KS = KS;
+  P.KH = KH;
+  P.KW = KW;
   P.gmode = gmode;
   P.stride = stride;
   P.pad = pad;
   P.up = up;
   P.S = S;
+  P.asplit = asplit;
+  P.Ha = Ha;
   int HWo = Ho * Wo;
   P.chunk = ((HWo + S - 1) / S + BK - 1) / BK * BK;
   P.fd_Wo = make_fastdiv(Wo);
   P.fd_Cs = make_fastdiv(Cs);
-  P.fd_KS = make_fastdiv(KS);
+  P.fd_KW = make_fastdiv(KW);
   dim3 g(P.Jpad / WBN, P.Mpad / wbm(c), N * S);
   launch_wg(c, g, st, P);
   return vst_launch_status();
+}
+
+static int splits_for(int N, int M, long J, int HWo) {
+  int c = wsel(M);
+  long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
+  long Jpad = (J + WBN - 1) / WBN * WBN;
+  return plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo);
 }
 
 }  // namespace
 
 extern "C" {
 
-// workspace (floats) needed by vst_conv_wgrad / vst_gram for a given problem
+// workspace (floats) needed by vst_conv_wgrad / vst_conv_wgrad_rowsplit / vst_gram
 long vst_wgrad_workspace(int N, int M, int J, int HWo) {
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
   long Jpad = (J + WBN - 1) / WBN * WBN;
-  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo);
-  return (long)N * S * Mpad * Jpad;
+  return (long)N * splits_for(N, M, J, HWo) * Mpad * Jpad;
 }
 
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
-                   int Cout, int Ho, int Wo, int KS, int gmode, int stride, int pad, int up, int accumulate,
+                   int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
                    void* stream) {
-  VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0);
+  VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
-  int c = wsel(Cout);
-  long Mpad = (Cout + wbm(c) - 1) / wbm(c) * wbm(c);
-  long J = (long)KS * KS * Cin;
-  long Jpad = (J + WBN - 1) / WBN * WBN;
-  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, Ho * Wo);
+  long J = (long)KH * KW * Cin;
+  int S = splits_for(N, Cout, J, Ho * Wo);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(dy, x, workspace, N, Cout, Cin, Hs, Ws, Ho, Wo, KS, gmode, stride, pad, up, S, st);
+  int rc = run_wg(dy, x, workspace, N, Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, S, 0, 0, st);
   if (rc) return rc;
+  int c = wsel(Cout);
+  long Mpad = (Cout + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = (J + WBN - 1) / WBN * WBN;
   long total = (long)Cout * J;
-  wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * S, Cout, (int)Mpad, (int)Jpad, Cin, KS,
-                                                           1.0f, accumulate);
+  wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * S, Cout, (int)Mpad, (int)Jpad, Cin, KH,
+                                                           KW, 0, 1.0f, accumulate);
+  return vst_launch_status();
+}
+
+// Weight gradient of a stride-1 reflect-padded KxK conv with few output channels (ConvTanh 48->3,
+// k9, RC/network.py:169): GEMM rows m = (co, kh) (27 for 3x9 instead of 3 padded to 32), columns
+// j = (kw, ci), reduction over the (H+K-1) x W grid of padded rows q:
+//   dW[co][ci][kh][kw] = sum_q dy[co][q_y - kh][q_x] * Xpad[ci][q_y][q_x + kw]
+int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
+                            int W, int Cout, int K, int accumulate, void* stream) {
+  VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && K > 0 && (K & 1) && K / 2 < H &&
+                K / 2 < W);
+  const int M = Cout * K, J = K * Cin, Hq = H + K - 1;
+  int S = splits_for(N, M, J, Hq * W);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = run_wg(dy, x, workspace, N, M, Cin, H, W, Hq, W, 1, K, 0, 1, K / 2, 1, S, K, H, st);
+  if (rc) return rc;
+  int c = wsel(M);
+  long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = ((long)J + WBN - 1) / WBN * WBN;
+  long total = (long)Cout * Cin * K * K;
+  wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * S, Cout, (int)Mpad, (int)Jpad, Cin, K, K,
+                                                           1, 1.0f, accumulate);
   return vst_launch_status();
 }
 
 // G[n] = F[n] F[n]^T * scale,  F = [N][C][H*W]
 int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, void* stream) {
   VST_CHECK_ARG(f && g && workspace && N > 0 && C > 0 && HW > 0);
-  int c = wsel(C);
-  long Mpad = (C + wbm(c) - 1) / wbm(c) * wbm(c);
-  long Jpad = (C + WBN - 1) / WBN * WBN;
-  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HW);
+  int S = splits_for(N, C, C, HW);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(f, f, workspace, N, C, C, 1, HW, 1, HW, 1, 1, 1, 0, 1, S, st);
+  int rc = run_wg(f, f, workspace, N, C, C, 1, HW, 1, HW, 1, 1, 1, 1, 0, 1, S, 0, 0, st);
   if (rc) return rc;
+  int c = wsel(C);
+  long Mpad = (C + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = (C + WBN - 1) / WBN * WBN;
   long total = (long)N * C * C;
   gram_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, g, N, S, C, (int)Mpad, (int)Jpad, scale);
   return vst_launch_status();

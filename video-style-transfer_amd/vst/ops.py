@@ -51,18 +51,21 @@ def _cache_entry(w):
     return {}
 
 
-def packed_weight(w, transposed):
-    """Tap-major A[k][m] pack of a conv weight."""
-    key = (w._version, w.data_ptr(), bool(transposed))
+def packed_weight(w, transposed, split_kh=False):
+    """Tap-major A[k][m] pack of a conv weight (split_kh: rows (co, kh), k = (kw, ci))."""
+    key = (w._version, w.data_ptr(), bool(transposed), bool(split_kh))
     if not w.requires_grad:
         hit = _cache_entry(w).get(key)
         if hit is not None:
             return hit
-    Cout, Cin, KS, _ = w.shape
-    M, Ck = (Cin, Cout) if transposed else (Cout, Cin)
-    Mpad, Kpad = pack_dims(M, KS * KS * Ck)
+    Cout, Cin, KH, KW = w.shape
+    if split_kh:
+        M, K = Cout * KH, KW * Cin
+    else:
+        M, K = (Cin, KH * KW * Cout) if transposed else (Cout, KH * KW * Cin)
+    Mpad, Kpad = pack_dims(M, K)
     out = _empty((Kpad * Mpad,), w)
-    lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KS, int(transposed), Mpad, Kpad, stream())
+    lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, stream())
     if not w.requires_grad:
         entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
         entry[key] = out
@@ -76,13 +79,15 @@ def conv_out_hw(H, W, ks, stride, pad, up):
 
 
 def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=None, out=None, aux=None, gmask=None,
-              a_batch_stride=0, mask=None, algo_flops=None):
+              a_batch_stride=0, mask=None, algo_flops=None, kh=None):
+    """ks: kernel width; kh: kernel height (defaults to ks)."""
     N, Cs, Hs, Ws = src.shape
+    kh = ks if kh is None else kh
     if out is None:
         out = _empty((N, M, Ho, Wo), src)
-    tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * ks)
-    lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, ks * ks * Cs, Ho, Wo,
-                      ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
+    tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh)
+    lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho, Wo,
+                      kh, ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
     kprof.end(tok)
     return out
 
@@ -111,8 +116,33 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up):
     Ho, Wo = gz.shape[2:]
     ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
     dw = _empty(w_shape, x)
-    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks,
+    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
                        GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, 0, stream())
+    return dw
+
+
+def rowsplit_ok(Cout, ks, stride, pad_mode, up):
+    """Tiny-Cout stride-1 reflect convs (ConvTanh 48->3 k9) run as row-split GEMMs."""
+    return Cout * ks <= 32 and ks > 1 and stride == 1 and pad_mode == "reflect" and up == 1
+
+
+def conv_fwd_rowsplit(x, w, b, epi, aux):
+    N, Cin, H, W = x.shape
+    Cout, _, K, _ = w.shape
+    Hq = H + K - 1
+    P = conv_gemm(x, packed_weight(w, False, split_kh=True), Cout * K, K, Hq, W, GM_REFLECT, 1, K // 2, 1, kh=1,
+                  algo_flops=2.0 * N * Cout * H * W * Cin * K * K)
+    out = _empty((N, Cout, H, W), x)
+    lib.vst_rowsplit_reduce(ptr(P), ptr(b), ptr(out), ptr(aux), N, Cout, K, H, W, epi, stream())
+    return out
+
+
+def conv_wgrad_rowsplit(gz, x, w_shape):
+    N, Cin, H, W = x.shape
+    Cout, _, K, _ = w_shape
+    ws = _empty((lib.vst_wgrad_workspace(N, Cout * K, K * Cin, (H + K - 1) * W),), x)
+    dw = _empty(w_shape, x)
+    lib.vst_conv_wgrad_rowsplit(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, K, 0, stream())
     return dw
 
 
@@ -139,8 +169,12 @@ class Conv2dFn(Function):
         Ho, Wo = conv_out_hw(H, W, ks, stride, pad, up)
         epi = (EPI_BIAS if b is not None else 0) | (EPI_RELU if act == "relu" else 0) | (EPI_TANH if act == "tanh" else 0)
         aux = _empty((N, Cout, Ho, Wo), x) if act == "tanh" else None
-        out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
-                        stride, pad, up, epi=epi, bias=b.contiguous() if b is not None else None, aux=aux)
+        bias = b.contiguous() if b is not None else None
+        if rowsplit_ok(Cout, ks, stride, pad_mode, up) and pad == ks // 2:
+            out = conv_fwd_rowsplit(x, w, bias, epi, aux)
+        else:
+            out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
+                            stride, pad, up, epi=epi, bias=bias, aux=aux)
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
         ctx.has_bias = b is not None
         ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
@@ -165,7 +199,10 @@ class Conv2dFn(Function):
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up)
+            if rowsplit_ok(w.shape[0], ks, stride, pad_mode, up) and pad == ks // 2:
+                dw = conv_wgrad_rowsplit(gz, x, w.shape)
+            else:
+                dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = channel_sum(gz)
         return dx, dw, db, None, None, None, None, None
