@@ -92,6 +92,7 @@ def main():
 
     from vst import kprof, ops
     from vst.reconet import network as N
+    from vst.reconet.dist import shard_seed
     from vst.reconet.train import ReCoNetTrainer
     from vst.synthetic import frame_pair_batch, style_image
 
@@ -105,7 +106,7 @@ def main():
     def hip_mask(f01, f10):
         return ops.flow_warp_mask(f01.to(dev), f10.to(dev))
 
-    img1, img2, flow, mask = frame_pair_batch(1234 + rank, B, H, W, mask_fn=hip_mask, device=dev)
+    img1, img2, flow, mask = frame_pair_batch(shard_seed(1234, rank), B, H, W, mask_fn=hip_mask, device=dev)
     frames = torch.stack([img1, img2]).contiguous()
     del img1, img2
 

@@ -57,6 +57,15 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
  * (RC/network.py:169 deconv3 = ConvTanh(48, 3, 9): 27 GEMM rows instead of 3 padded to 32) */
 int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* aux, int N, int Cout, int KH, int H,
                         int W, int epi, void* stream);
+/* stride-2 data gradient by parity class (py, px) of the padded input grid: transposed pack of
+ * the taps kh = py+2i, kw = px+2j (k = (i*nkw+j)*Cout + co, m = cin); each class is then a
+ * stride-1 transposed vst_conv_gemm(pad=0, KH=nkh, KW=nkw) on the class grid, 4x fewer MACs than
+ * zero-stuffing (RC/network.py:158-159 conv2/conv3 backward) */
+int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,
+                           void* stream);
+/* adjoint of ReflectionPad2d(pad) from the 4 class planes [(0,0),(0,1),(1,0),(1,1)][NC][Hc][Wc] */
+int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws, int pad, int accumulate,
+                            void* stream);
 /* adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hs*up+2p][Ws*up+2p] -> dx [NC][Hs][Ws] */
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
                      void* stream);

@@ -377,6 +377,56 @@ __global__ void fold_reflect_kernel(const float* __restrict__ dpad, float* __res
   dx[idx] = s;
 }
 
+// Stride-2 data gradient, parity class (py, px): only taps kh = py + 2i, kw = px + 2j reach
+// padded-input pixels (2yy+py, 2xx+px), and they read dY[yy - i][xx - j].  Packed as a
+// transposed A: k = (i*nkw + j)*Cout + co, m = ci.
+__global__ void pack_parity_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
+                                   int py, int px, int Mpad, int Kpad) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)Mpad * Kpad) return;
+  int m = (int)(idx % Mpad);
+  int k = (int)(idx / Mpad);
+  const int nkh = (KS - py + 1) / 2, nkw = (KS - px + 1) / 2;
+  float v = 0.f;
+  if (m < Cin && k < nkh * nkw * Cout) {
+    int tap = k / Cout, co = k % Cout;
+    int i = tap / nkw, j = tap % nkw;
+    v = w[(((long)co * Cin + m) * KS + py + 2 * i) * KS + px + 2 * j];
+  }
+  out[apack_index(k, m, Mpad)] = v;
+}
+
+// fold_reflect over the 4 parity-class planes [class (a,b)][NC][Hc_a][Wc_b] of the padded grid
+__global__ void fold_reflect_parity_kernel(const float* __restrict__ cls, float* __restrict__ dx, long NC, int Hs,
+                                           int Ws, int pad, int accumulate) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = NC * Hs * Ws;
+  if (idx >= total) return;
+  int xs = (int)(idx % Ws);
+  long t = idx / Ws;
+  int ys = (int)(t % Hs);
+  long nc = t / Hs;
+  const int Hp = Hs + 2 * pad, Wp = Ws + 2 * pad;
+  const int Hc[2] = {(Hp + 1) / 2, Hp / 2}, Wc[2] = {(Wp + 1) / 2, Wp / 2};
+  long coff[4];
+  coff[0] = 0;
+  coff[1] = coff[0] + NC * Hc[0] * Wc[0];
+  coff[2] = coff[1] + NC * Hc[0] * Wc[1];
+  coff[3] = coff[2] + NC * Hc[1] * Wc[0];
+  int rows[3], cols[3];
+  int nr = reflect_sources(ys, Hs, pad, rows);
+  int ncl = reflect_sources(xs, Ws, pad, cols);
+  float s = 0.f;
+  for (int a = 0; a < nr; ++a)
+    for (int b = 0; b < ncl; ++b) {
+      const int yp = rows[a], xp = cols[b];
+      const int ca = yp & 1, cb = xp & 1;
+      s += cls[coff[ca * 2 + cb] + (nc * Hc[ca] + (yp >> 1)) * Wc[cb] + (xp >> 1)];
+    }
+  if (accumulate) s += dx[idx];
+  dx[idx] = s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -452,6 +502,24 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
     gmask ? launch_cfg<true, true>(cfg, grid, st, P) : launch_cfg<true, false>(cfg, grid, st, P);
   else
     gmask ? launch_cfg<false, true>(cfg, grid, st, P) : launch_cfg<false, false>(cfg, grid, st, P);
+  return vst_launch_status();
+}
+
+int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,
+                           void* stream) {
+  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && (py == 0 || py == 1) && (px == 0 || px == 1));
+  long total = (long)Mpad * Kpad;
+  pack_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, py, px, Mpad,
+                                                                            Kpad);
+  return vst_launch_status();
+}
+
+int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws, int pad, int accumulate,
+                            void* stream) {
+  VST_CHECK_ARG(cls && dx && NC > 0 && Hs > 0 && Ws > 0 && pad >= 0 && pad < Hs && pad < Ws);
+  long total = NC * Hs * Ws;
+  fold_reflect_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(cls, dx, NC, Hs, Ws, pad,
+                                                                                    accumulate);
   return vst_launch_status();
 }
 

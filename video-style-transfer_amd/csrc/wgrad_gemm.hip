@@ -27,16 +27,19 @@ struct WgParams {
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
-template <int WM, int TM, int WN, int TN>
-__global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
+template <int WM, int TM, int WN, int TN, bool AV, int MINW>
+__global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int A_PER = BM * BK / NT;
+  constexpr int LS = 20;                       // LDS row: [hi][s] (k = 2s + hi) + 4 pad floats
+  constexpr int A_F4 = BM * BK / 4;            // vector path: float4 per A tile
+  constexpr int A_PV = (A_F4 + NT - 1) / NT;
+  constexpr int A_PS = BM * BK / NT;           // scalar path: floats per thread
   constexpr int B_PER = BN * BK / NT;
-  constexpr int SA = BM + 1, SB = BN + 1;  // padded rows: transposed writes stay conflict-free
+  static_assert(BK == 16, "LDS layout assumes 16-pixel k-tiles");
 
-  __shared__ float As[2][BK][SA];
-  __shared__ float Bs[2][BK][SB];
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -49,13 +52,17 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
   const int HWo = P.Ho * P.Wo;
   const int r_begin = sidx * P.chunk;
   const int r_end = min(HWo, r_begin + P.chunk);
-  const long plane = (long)P.Hs * P.Ws;
+  const int plane = P.Hs * P.Ws;
   const long a_img = P.asplit ? (long)(P.M / P.asplit) * P.Ha * P.Wo : (long)P.M * HWo;
   const float* a_n = P.a + (long)n * a_img;
   const float* src_n = P.src + (long)n * P.Cs * plane;
+  constexpr int OOR = 0x7ffffff0;
+  const __amdgpu_buffer_rsrc_t asrd = __builtin_amdgcn_make_buffer_rsrc((void*)a_n, (short)0, (int)(a_img * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t bsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src_n, (short)0, (int)((long)P.Cs * plane * 4), 0x00020000);
 
-  const int rr = tid % BK;   // this thread's pixel row within a k-tile
-  const int cc = tid / BK;   // 0..7: base column (B) / base row (A)
+  const int rr = tid % BK;  // B: this thread's pixel within a k-tile
+  const int cc = tid / BK;  // B: base column
 
   // decode this thread's B columns once: (ci, kh, kw) packed, -1 if j >= J
   int jdesc[B_PER];
@@ -81,66 +88,82 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float ra[A_PER], rb[B_PER];
+  f32x4 rav[AV ? A_PV : 1];
+  float ras[AV ? 1 : A_PS];
+  float rb[B_PER];
   const int ntiles = r_end > r_begin ? (r_end - r_begin + BK - 1) / BK : 0;
   const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
+  const int sh = P.up - 1;
+
+  auto a_offset = [&](int m, int r) -> int {  // element offset of A[m][r] or OOR
+    if (m >= P.M || r >= r_end) return OOR;
+    if (!P.asplit) return m * HWo + r;
+    const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
+    const int co = m / P.asplit, kh = m - co * P.asplit;
+    const int yy = oy - kh;
+    return (yy >= 0 && yy < P.Ha) ? (co * P.Ha + yy) * P.Wo + ox : OOR;
+  };
 
   auto load_tile = [&](int t) {
-    const int r = r_begin + t * BK + rr;
-    const bool rv = r < r_end;
-    int oy = 0, ox = 0;
-    if (rv) {
-      oy = (int)fdiv((uint32_t)r, P.fd_Wo);
-      ox = r - oy * P.Wo;
-    }
+    const int rt = r_begin + t * BK;
+    if (AV) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int m = m0 + cc + i * (NT / BK);
-      float v = 0.f;
-      if (rv && m < P.M) {
-        if (P.asplit) {
-          int co = m / P.asplit, kh = m - co * P.asplit;
-          int yy = oy - kh;
-          if (yy >= 0 && yy < P.Ha) v = a_n[((long)co * P.Ha + yy) * P.Wo + ox];
-        } else {
-          v = a_n[(long)m * HWo + r];
+      for (int i = 0; i < A_PV; ++i) {
+        const int idx = tid + i * NT;
+        if (A_F4 % NT == 0 || idx < A_F4) {
+          const int off = a_offset(m0 + (idx >> 2), rt + 4 * (idx & 3));
+          rav[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, off == OOR ? OOR : off * 4, 0, 0));
         }
       }
-      ra[i] = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PS; ++i) {
+        const int off = a_offset(m0 + cc + i * (NT / BK), rt + rr);
+        ras[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(asrd, off == OOR ? OOR : off * 4, 0, 0));
+      }
     }
+    const int r = rt + rr;
+    const bool rv = r < r_end;
+    const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
     const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int d = jdesc[i];
-      float v = 0.f;
-      if (rv && d >= 0) {
-        int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
-        int y = by + kh, x = bx + kw;
-        bool ok = true;
-        if (P.gmode == 0) {
-          y = y < 0 ? -y : y;
-          y = y >= Hv ? 2 * Hv - 2 - y : y;
-          x = x < 0 ? -x : x;
-          x = x >= Wv ? 2 * Wv - 2 - x : x;
-        } else {
-          ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
-        }
-        if (ok) {
-          if (P.up == 2) {
-            y >>= 1;
-            x >>= 1;
-          }
-          v = src_n[(long)ci * plane + y * P.Ws + x];
-        }
+      const int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
+      int y = by + kh, x = bx + kw;
+      bool ok = rv && d >= 0;
+      if (P.gmode == 0) {
+        y = abs(y);
+        y = min(y, 2 * Hv - 2 - y);
+        x = abs(x);
+        x = min(x, 2 * Wv - 2 - x);
+      } else {
+        ok = ok && y >= 0 && y < Hv && x >= 0 && x < Wv;
       }
-      rb[i] = v;
+      const int vo = ok ? (ci * plane + (y >> sh) * P.Ws + (x >> sh)) * 4 : OOR;
+      rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
     }
   };
   auto store_tile = [&](int buf) {
+    if (AV) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) As[buf][rr][cc + i * (NT / BK)] = ra[i];
+      for (int i = 0; i < A_PV; ++i) {
+        const int idx = tid + i * NT;
+        if (A_F4 % NT == 0 || idx < A_F4) {
+          const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> (s, hi) = (2q,0),(2q,1),(2q+1,0),(2q+1,1)
+          float* row = &As[buf][m][0];
+          row[2 * q] = rav[i][0];
+          row[2 * q + 1] = rav[i][2];
+          row[8 + 2 * q] = rav[i][1];
+          row[8 + 2 * q + 1] = rav[i][3];
+        }
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) Bs[buf][rr][cc + i * (NT / BK)] = rb[i];
+      for (int i = 0; i < A_PS; ++i) As[buf][cc + i * (NT / BK)][(rr & 1) * 8 + (rr >> 1)] = ras[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) Bs[buf][cc + i * (NT / BK)][(rr & 1) * 8 + (rr >> 1)] = rb[i];
   };
 
   if (ntiles > 0) {
@@ -151,18 +174,26 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(WgParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
+    f32x4 a[TM][2], b[TN][2];
 #pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      float a[TM], b[TN];
+    for (int i = 0; i < TM; ++i) {
+      const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+      a[i][0] = *reinterpret_cast<const f32x4*>(r);
+      a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+    }
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[buf][2 * s + hi][(wm * TM + i) * 32 + lo];
+    for (int j = 0; j < TN; ++j) {
+      const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+      b[j][0] = *reinterpret_cast<const f32x4*>(r);
+      b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+    }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[buf][2 * s + hi][(wn * TN + j) * 32 + lo];
+    for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     if (t + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
   }
@@ -235,14 +266,25 @@ __global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __rest
   out[idx] = s * scale;
 }
 
-static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
+template <bool AV>
+static void launch_wg_t(int c, dim3 g, hipStream_t st, const WgParams& P) {
   switch (c) {
-    case W32: wgrad_kernel<1, 1, 4, 1><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad_kernel<1, 2, 4, 1><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad_kernel<1, 3, 4, 1><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad_kernel<2, 2, 2, 2><<<g, NT, 0, st>>>(P); break;
-    default: wgrad_kernel<2, 3, 2, 2><<<g, NT, 0, st>>>(P); break;
+    case W32: wgrad_kernel<1, 1, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad_kernel<1, 2, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad_kernel<1, 3, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad_kernel<2, 2, 2, 2, AV, 4><<<g, NT, 0, st>>>(P); break;
+    default: wgrad_kernel<2, 3, 2, 2, AV, 2><<<g, NT, 0, st>>>(P); break;
   }
+}
+
+static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
+  // float4 A loads need 4 consecutive pixels in one row segment (and, for the row-split gather,
+  // in one output row)
+  const bool av = (P.Ho * P.Wo) % 4 == 0 && (!P.asplit || P.Wo % 4 == 0);
+  if (av)
+    launch_wg_t<true>(c, g, st, P);
+  else
+    launch_wg_t<false>(c, g, st, P);
 }
 
 static int plan_splits(long tiles, int N, int HWo) {

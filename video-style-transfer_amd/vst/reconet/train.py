@@ -18,10 +18,10 @@ FTL/OTL denominators are rank-local nnz and TV is a sum, exactly as the referenc
 on its (per-rank) batch.
 """
 import torch
-import torch.distributed as dist
 
 from .. import ops
 from ._flat import FlatParams
+from .dist import allreduce_grads, world_info
 
 LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
 
@@ -37,7 +37,7 @@ class ReCoNetTrainer:
         self.flat = FlatParams(model)
         self.step_count = 0
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank, self.world = world_info(process_group)
         dev = self.flat.p.device
         self.chscale_cache = {}
         with torch.no_grad():
@@ -91,10 +91,7 @@ class ReCoNetTrainer:
         self.flat.zero_grad()
         out = self.losses(frames, flow, mask)
         out["loss"].backward()
-        gscale = 1.0
-        if self.world > 1:
-            dist.all_reduce(self.flat.g, op=dist.ReduceOp.SUM, group=self.pg)
-            gscale = 1.0 / self.world
+        gscale = allreduce_grads(self.flat.g, self.pg)
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}
