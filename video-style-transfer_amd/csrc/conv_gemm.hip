@@ -275,7 +275,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
 }
 
 // tile configurations (BM x BN)
-enum TileCfg { T32 = 0, T64, T96, T128, T192 };
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W };
 
 static int select_cfg(int M) {
   if (M <= 32) return T32;
@@ -285,10 +285,18 @@ static int select_cfg(int M) {
   return T128;
 }
 static int cfg_bm(int c) {
-  const int bm[] = {32, 64, 96, 128, 192};
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96};
   return bm[c];
 }
-static int cfg_bn(int c) { return c == T32 ? 256 : 128; }
+static int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
+#ifndef VST_WIDE
+#define VST_WIDE 1
+#endif
+// 64/96-row tiles on large pixel grids: 256-column tiles (twice the MFMAs per A fragment)
+static int widen_cfg(int c, long HWo) {
+  if (!VST_WIDE || HWo < 8192) return c;
+  return c == T64 ? T64W : (c == T96 ? T96W : c);
+}
 
 #ifndef VST_MINW_T128
 #define VST_MINW_T128 4
@@ -306,6 +314,8 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3><<<grid, NT, 0, st>>>(P); break;
     case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
     case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
+    case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3><<<grid, NT, 0, st>>>(P); break;
+    case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2><<<grid, NT, 0, st>>>(P); break;
     case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, VST_MINW_T128><<<grid, NT, 0, st>>>(P); break;
     default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192><<<grid, NT, 0, st>>>(P); break;
   }
@@ -478,7 +488,7 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   P.Hs = Hs;
   P.Ws = Ws;
   P.M = M;
-  int cfg = select_cfg(M);
+  int cfg = widen_cfg(select_cfg(M), (long)Ho * Wo);
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);
   P.Mpad = (M + bm - 1) / bm * bm;
   P.K = K;

@@ -138,14 +138,15 @@ def conv_dgrad_parity(gz, w, x_shape, ks, pad, gmask=None):
     return dx
 
 
-def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up):
+def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     N, Cin, H, W = x.shape
     Cout = w_shape[0]
     Ho, Wo = gz.shape[2:]
     ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
-    dw = _empty(w_shape, x)
+    acc = out is not None
+    dw = _empty(w_shape, x) if out is None else out
     lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
-                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, 0, stream())
+                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), stream())
     return dw
 
 
@@ -165,22 +166,36 @@ def conv_fwd_rowsplit(x, w, b, epi, aux):
     return out
 
 
-def conv_wgrad_rowsplit(gz, x, w_shape):
+def conv_wgrad_rowsplit(gz, x, w_shape, out=None):
     N, Cin, H, W = x.shape
     Cout, _, K, _ = w_shape
     ws = _empty((lib.vst_wgrad_workspace(N, Cout * K, K * Cin, (H + K - 1) * W),), x)
-    dw = _empty(w_shape, x)
-    lib.vst_conv_wgrad_rowsplit(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, K, 0, stream())
+    acc = out is not None
+    dw = _empty(w_shape, x) if out is None else out
+    lib.vst_conv_wgrad_rowsplit(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, K, int(acc), stream())
     return dw
 
 
-def channel_sum(x):
+def channel_sum(x, out=None):
     N, C = x.shape[:2]
     HW = x[0, 0].numel()
-    out = _empty((C,), x)
+    acc = out is not None
+    out = _empty((C,), x) if out is None else out
     part = _empty((N * C,), x)
-    lib.vst_channel_sum(ptr(x), ptr(out), ptr(part), N, C, HW, 0, stream())
+    lib.vst_channel_sum(ptr(x), ptr(out), ptr(part), N, C, HW, int(acc), stream())
     return out
+
+
+def grad_sink(p):
+    """The .grad buffer of a leaf parameter that kernels can accumulate into directly (and the
+    Function then returns None for it, skipping autograd's AccumulateGrad add); None otherwise.
+    FlatParams pre-creates these views into the flat gradient buffer."""
+    if p is None or not p.requires_grad or p.grad_fn is not None:
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != p.shape or not g.is_cuda:
+        return None
+    return g
 
 
 class Conv2dFn(Function):
@@ -205,6 +220,7 @@ class Conv2dFn(Function):
                             stride, pad, up, epi=epi, bias=bias, aux=aux)
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
         ctx.has_bias = b is not None
+        ctx.params = (w, b)  # leaves: weight gradients go straight into their .grad when possible
         ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
         return out
 
@@ -226,12 +242,16 @@ class Conv2dFn(Function):
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask)
         if ctx.needs_input_grad[1]:
+            sink = grad_sink(ctx.params[0])
             if rowsplit_ok(w.shape[0], ks, stride, pad_mode, up) and pad == ks // 2:
-                dw = conv_wgrad_rowsplit(gz, x, w.shape)
+                dw = conv_wgrad_rowsplit(gz, x, w.shape, out=sink)
             else:
-                dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up)
+                dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up, out=sink)
+            dw = None if sink is not None else dw
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = channel_sum(gz)
+            sink = grad_sink(ctx.params[1])
+            db = channel_sum(gz, out=sink)
+            db = None if sink is not None else db
         return dx, dw, db, None, None, None, None, None
 
 
@@ -253,6 +273,7 @@ class InstanceNormFn(Function):
                              H * W, float(eps), int(relu), stream())
         ctx.relu = relu
         ctx.has_res = res is not None
+        ctx.params = (w, b)
         ctx.save_for_backward(x, y if relu else None, stats, w)
         return y
 
@@ -262,12 +283,16 @@ class InstanceNormFn(Function):
         gy = gy.contiguous()
         N, C, H, W = x.shape
         gx = _empty(x.shape, x)
-        gw = _empty((C,), x)
-        gb = _empty((C,), x)
+        sw, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
+        direct = sw is not None and sb is not None
+        gw = sw if direct else _empty((C,), x)
+        gb = sb if direct else _empty((C,), x)
         part = _empty((N * C * 3,), x)
         lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(stats), ptr(w.contiguous()), ptr(gx), ptr(gw), ptr(gb), None,
-                             ptr(part), N, C, H * W, int(ctx.relu), 0, stream())
+                             ptr(part), N, C, H * W, int(ctx.relu), int(direct), stream())
         gres = gy if ctx.has_res else None
+        if direct:
+            gw = gb = None
         return gx, gw, gb, gres, None, None
 
 
