@@ -62,3 +62,21 @@ def vgg19():
     """AA/vgg19.py:8-41: torchvision VGG19 features[0:30] as slice1..5."""
     return _vgg([(1, 0, 64), (2, 2, 64), (2, 5, 128), (3, 7, 128), (3, 10, 256), (4, 12, 256), (4, 14, 256),
                  (4, 16, 256), (4, 19, 512), (5, 21, 512), (5, 23, 512), (5, 25, 512), (5, 28, 512)])
+
+
+ADAATTN_LEVELS = ((256, 64 + 128 + 256), (512, 64 + 128 + 256 + 512), (512, 64 + 128 + 256 + 512 + 512))
+DECODER = [("conv1", 512, 512, True), ("conv2", 512, 256, True), ("conv3.0", 512, 256, True), ("conv3.1", 256, 256, True),
+           ("conv3.2", 256, 256, True), ("conv4", 256, 128, True), ("conv5", 128, 128, True), ("conv6", 128, 64, True),
+           ("conv7", 64, 64, True), ("conv8", 64, 3, False)]
+
+
+def stylizing_network():
+    """AA/network.py:223-235 (AdaAttN x3 with 1x1 f/g/h, then Decoder AA/network.py:63-77)."""
+    s = []
+    for i, (vd, qd) in enumerate(ADAATTN_LEVELS):
+        for nm, c in (("f", qd), ("g", qd), ("h", vd)):
+            s += [(f"adaattn.{i}.{nm}.weight", (c, c, 1, 1)), (f"adaattn.{i}.{nm}.bias", (c,))]
+    for name, cin, cout, relu in DECODER:
+        key = f"decoder.{name}.conv.conv" if relu else f"decoder.{name}.conv"
+        s += [(key + ".weight", (cout, cin, 3, 3)), (key + ".bias", (cout,))]
+    return s

@@ -237,5 +237,103 @@ def gen_reconet():
     print("reconet fixtures written")
 
 
+# --------------------------------------------------------------------------------------------
+# AdaAttN (AA/)
+# --------------------------------------------------------------------------------------------
+def gen_adaattn():
+    _fresh_project(AA_DIR)
+    aa_util = _load("utilities", os.path.join(AA_DIR, "utilities.py"))
+    sys.modules["utilities"] = aa_util
+    aa_vgg = _load("vgg19", os.path.join(AA_DIR, "vgg19.py"))
+    sys.modules["vgg19"] = aa_vgg
+    aa_net = _load("network", os.path.join(AA_DIR, "network.py"))
+    sys.modules["network"] = aa_net
+    aa_loss = _load("lossfn", os.path.join(AA_DIR, "lossfn.py"))
+    sys.modules["lossfn"] = aa_loss
+
+    u = {}
+    rng = np.random.default_rng(300)
+    with torch.no_grad():
+        vgg = aa_vgg.VGG19()
+        seed_module(vgg, 31)
+        x = torch.from_numpy(rng.uniform(0, 255, (1, 3, 32, 64)).astype(f32))
+        s = torch.from_numpy(rng.uniform(0, 255, (1, 3, 32, 64)).astype(f32))
+        fx, fs = vgg(x), vgg(s)
+        u["x"], u["s"] = _np(x), _np(s)
+        for k, v in fx.items():
+            u[f"vgg19_x_{k}"] = _np(v)
+        lx, ls = list(fx.values()), list(fs.values())
+        for idx in (2, 3, 4):
+            u[f"fds_x_{idx}"] = _np(aa_util.feature_down_sample(lx, idx))
+        # AdaAttnNoConv (the local-feature-loss target) and AdaAttN modules, cosine activation
+        for i, (vd, qd) in enumerate(((256, 448), (512, 960), (512, 1472))):
+            idx = i + 2
+            c1x, s1x = aa_util.feature_down_sample(lx, idx), aa_util.feature_down_sample(ls, idx)
+            u[f"noconv{i}"] = _np(aa_net.AdaAttnNoConv(vd, qd, "cosine")(lx[idx], ls[idx], c1x, s1x))
+        net = aa_net.StylizingNetwork("cosine")
+        seed_module(net, 32)
+        u["stylized"] = _np(net(fx, fs))
+        for i in range(3):
+            idx = i + 2
+            c1x, s1x = aa_util.feature_down_sample(lx, idx), aa_util.feature_down_sample(ls, idx)
+            u[f"adaattn{i}"] = _np(net.adaattn[i](lx[idx], ls[idx], c1x, s1x))
+        # losses (AA/lossfn.py)
+        mse = torch.nn.MSELoss()
+        for k in ("relu2_1", "relu3_1", "relu4_1", "relu5_1"):
+            u[f"gsl_{k}"] = np.array(float(aa_loss.global_stylized_loss(fx[k], fs[k], mse)))
+        for k in ("relu2_1", "relu3_1", "relu4_1"):
+            u[f"cosd_{k}"] = _np(aa_loss.cosine_distance(fx[k], fs[k]))
+            u[f"isl_{k}"] = np.array(float(aa_loss.image_similarity_loss(fx[k], fs[k], fs[k] * 0.5 + 1.0, fx[k])))
+    np.savez_compressed(os.path.join(HERE, "aa_units.npz"), **u)
+
+    # full training step through the reference's own train_video.train()
+    step = {}
+    B, H, W, seeds = 2, 64, 128, (41, 42, 43)
+    rng = np.random.default_rng(seeds[2])
+    c1 = torch.from_numpy(rng.uniform(0, 255, (B, 3, H, W)).astype(f32))
+    c2 = torch.from_numpy(rng.uniform(0, 255, (B, 3, H, W)).astype(f32))
+    st = torch.from_numpy(rng.uniform(0, 255, (B, 3, H, W)).astype(f32))
+    fake_ds = types.ModuleType("datasets")
+    fake_ds.VidevoWikiArt = lambda *a, **k: None
+    sys.modules["datasets"] = fake_ds
+    tv = _load("aa_train_video", os.path.join(AA_DIR, "train_video.py"))
+    holder = {}
+
+    def net_factory(activation="softmax", _h=holder):
+        m = aa_net.StylizingNetwork(activation)
+        seed_module(m, seeds[0])
+        _h["model"] = m
+        tv.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(m.named_parameters())))
+        return m
+
+    def vgg_factory():
+        v = aa_vgg.VGG19()
+        seed_module(v, seeds[1])
+        return v
+
+    tv.EPOCH_START, tv.EPOCH_END = 1, 1
+    tv.DataLoader = lambda *a, **k: [(c1.clone(), c2.clone(), st.clone())]
+    tv.StylizingNetwork, tv.VGG19, tv.tqdm = net_factory, vgg_factory, _TqdmRecorder
+    _TqdmRecorder.records = []
+    save = torch.save
+    torch.save = lambda *a, **k: None
+    try:
+        tv.train()
+    finally:
+        torch.save = save
+    rec = _TqdmRecorder.records[-1]
+    step["c1"], step["c2"], step["style"], step["seeds"] = _np(c1), _np(c2), _np(st), np.array(seeds)
+    for k in ("loss", "loss_gs", "loss_lf", "loss_is"):
+        step[k] = np.array(rec[k], dtype=np.float64)
+    adam = tv.optim.Adam
+    _grad_summary("", adam.grads, adam.after, step, seed=seeds[0] + 1000)
+    np.savez_compressed(os.path.join(HERE, "aa_step.npz"), **step)
+    print("adaattn fixtures written")
+
+
 if __name__ == "__main__":
-    gen_reconet()
+    which = sys.argv[1:] or ["reconet", "adaattn"]
+    if "reconet" in which:
+        gen_reconet()
+    if "adaattn" in which:
+        gen_adaattn()

@@ -93,3 +93,56 @@ def test_train_step(golden, tag):
         gh = s[f"{tag}_ghead/{n}"]
         sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
         assert np.abs(params[n].reshape(-1)[:64].numpy() - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
+
+
+# ----------------------------------------------------------------------------- AdaAttN
+def test_adaattn_units(golden):
+    from oracle import adaattn_ref as A
+
+    u = golden("aa_units")
+    VP = oracle.seeded_params(shapes.vgg19(), 31)
+    with torch.no_grad():
+        fx, fs = A.vgg19(VP, T(u["x"])), A.vgg19(VP, T(u["s"]))
+        for k in A.FEATS:
+            assert rel_err(fx[k], u[f"vgg19_x_{k}"]) < 1e-4, k
+        lx, ls = list(fx.values()), list(fs.values())
+        for idx in (2, 3, 4):
+            assert rel_err(A.feature_down_sample(lx, idx), u[f"fds_x_{idx}"]) < 1e-5
+        for i in range(3):
+            idx = i + 2
+            c1, s1 = A.feature_down_sample(lx, idx), A.feature_down_sample(ls, idx)
+            assert rel_err(A.adaattn(None, None, lx[idx], ls[idx], c1, s1), u[f"noconv{i}"]) < 1e-4, i
+        P = oracle.seeded_params(shapes.stylizing_network(), 32)
+        for i in range(3):
+            idx = i + 2
+            c1, s1 = A.feature_down_sample(lx, idx), A.feature_down_sample(ls, idx)
+            assert rel_err(A.adaattn(P, f"adaattn.{i}", lx[idx], ls[idx], c1, s1), u[f"adaattn{i}"]) < 1e-4, i
+        assert rel_err(A.stylize(P, fx, fs), u["stylized"]) < 1e-4
+        for k in ("relu2_1", "relu3_1", "relu4_1", "relu5_1"):
+            assert rel_err(A.global_stylized_loss(fx[k], fs[k]).item(), u[f"gsl_{k}"]) < 1e-4, k
+        for k in ("relu2_1", "relu3_1", "relu4_1"):
+            assert rel_err(A.cosine_distance(fx[k], fs[k]), u[f"cosd_{k}"]) < 1e-5, k
+            got = A.image_similarity_loss(fx[k], fs[k], fs[k] * 0.5 + 1.0, fx[k]).item()
+            assert rel_err(got, u[f"isl_{k}"]) < 1e-4, k
+
+
+def test_adaattn_train_step(golden):
+    from oracle import adaattn_ref as A
+
+    s = golden("aa_step")
+    seeds = s["seeds"]
+    P = oracle.seeded_params(shapes.stylizing_network(), int(seeds[0]), requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg19(), int(seeds[1]))
+    L = A.adaattn_losses(P, VP, T(s["c1"]), T(s["c2"]), T(s["style"]))
+    for k in ("loss", "loss_gs", "loss_lf", "loss_is"):
+        assert rel_err(L[k].item(), s[k]) < 1e-3, k
+    L["loss"].backward()
+    names = list(s["names"])
+    assert sorted(names) == sorted(P)
+    gmax = max(float(s[f"gnorm/{n}"]) for n in names)
+    for n in names:
+        g = P[n].grad
+        gn = float(s[f"gnorm/{n}"])
+        assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"gidx/{n}"]
+        assert np.abs(g.reshape(-1)[idx].numpy() - s[f"gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
