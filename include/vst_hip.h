@@ -112,7 +112,11 @@ int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int 
 /* F.interpolate(mode="bilinear", align_corners=False) (RC/train_single/train_candy.py:91,97);
  * optional per-channel scale (chscale[C], device) and binarize (> 0) epilogues */
 int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
-                        const float* chscale, int binarize, void* stream);
+                        const float* chscale, int binarize, long out_bs, const float* addend, void* stream);
+/* adjoint (float-atomic scatter into gx, zero it first); gout images gout_bs floats apart (0: dense)
+ * (AA/network.py:59,80,85,90,94 decoder upsampling backward) */
+int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
+                            void* stream);
 
 /* ---- losses (RC/train_single/train_candy.py:90-145) ----------------------------------------
  * ws: >= 2048 floats; out: 3 floats {loss, weight/denom, denom count}.  Backward reads gout[0]
@@ -131,6 +135,61 @@ int vst_mse_bwd(const float* a, const float* b, long n, long nb, const float* go
 /* weight * sum of squared right/down differences (train_candy.py:141-145) */
 int vst_tv_fwd(const float* s, long NC, int H, int W, float weight, float* ws, float* out, void* stream);
 int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs, void* stream);
+
+/* out = {weight * sum(x[0:n]), weight, 0} */
+int vst_sum_scaled(const float* x, long n, float weight, float* ws, float* out, void* stream);
+
+/* ---- AdaAttN (AA/network.py:102-251, AA/lossfn.py:5-53) --------------------------------------
+ * Attention matrices are materialised per image ([N][Nc][Ns] fp32); the products run on the GEMM
+ * kernels: S = Q^T K and dA = [dM;dE2]^T [V;V^2] and dK = Q dS and d[V;V^2] = [dM;dE2] A as
+ * vst_conv_gemm 1x1 products with a per-image packed A, [M;E2] = A [V;V^2]^T-style and dQ = K dS^T
+ * as vst_gemm_abt. */
+/* out[n][m][j] = scale * sum_r a[n][m][r] b[n][j][r]; workspace = vst_wgrad_workspace(N, M, J, R) */
+int vst_gemm_abt(const float* a, const float* b, float* out, float* workspace, int N, int M, int J, int R, float scale,
+                 void* stream);
+/* packed A operand from row-major X[k][m] (transpose 0) or X[m][k] (transpose 1), per batch */
+int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int transpose, int Mpad, int Kpad, long x_bs,
+                    void* stream);
+/* out[n][p] = ||x[n][:][p]||_2 (LA.vector_norm over channels, AA/network.py:121-122) */
+int vst_channel_norm(const float* x, float* out, int N, int C, int P, void* stream);
+/* A = (S/(qn_i kn_j) + 1) / rowsum_i  (CosineSimilarity, AA/network.py:123-124) */
+int vst_cos_attn_rows(const float* S, const float* qn, const float* kn, float* A, float* rowsum, int N, int Nc, int Ns,
+                      void* stream);
+/* backward: dS = d(raw Q^T K), dqn, dkn; S_t overwritten; part = N*ceil(Nc/64)*Ns floats */
+int vst_cos_attn_rows_bwd(const float* dA, const float* A, float* S_t, const float* qn, const float* kn,
+                          const float* rowsum, float* dS, float* dqn, float* dkn, float* part, int N, int Nc, int Ns,
+                          void* stream);
+/* A = softmax(S) over rows of Ns (Softmax activation, AA/network.py:102-108) and its backward
+ * dS = A (dA - rowsum(dA A)); dS may alias dA */
+int vst_softmax_rows(const float* S, float* A, long rows, int Ns, void* stream);
+int vst_softmax_rows_bwd(const float* dA, const float* A, float* dS, long rows, int Ns, void* stream);
+/* x[n][c][p] += s[n][p] / nrm[n][p] * y[n][c][p] */
+int vst_norm_grad_add(float* x, const float* s, const float* nrm, const float* y, int N, int C, int P, void* stream);
+/* VV2[n] = [V[n]; V[n]^2] and its backward dV = dV + 2 V dV2 */
+int vst_square_concat(const float* V, float* VV2, int N, long per, void* stream);
+int vst_square_concat_bwd(const float* dVV2, const float* V, float* dV, int N, long per, void* stream);
+/* out = sqrt(clamp(E2 - M^2, 1e-6)) * IN(c_x) + M, MV[n] = [M; E2] (AA/network.py:209-220) */
+int vst_adaattn_out(const float* MV, const float* cn, float* out, int N, long per, void* stream);
+int vst_adaattn_out_bwd(const float* dout, const float* MV, const float* cn, float* dMV, int N, long per, void* stream);
+/* per-plane mean / unbiased std (global_stylized_loss, AA/lossfn.py:5-17) and backward */
+int vst_plane_meanstd(const float* x, float* mean, float* std_, long NC, int HW, void* stream);
+int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, const float* gmean, const float* gstd,
+                          float* gx, long NC, int HW, void* stream);
+/* per-plane L2 norm and its gradient add x += s/nrm * y */
+int vst_plane_norm(const float* x, float* out, long NC, int HW, void* stream);
+int vst_plane_norm_grad(float* x, const float* s, const float* nrm, const float* y, long NC, int HW, void* stream);
+/* image_similarity_loss (AA/lossfn.py:25-53) on precomputed C x C products and norms;
+ * partial[n] = sum |Dn_c - Dn_cs| / hw; backward w.r.t. the stylised side (dun zeroed first) */
+int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
+                const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream);
+int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
+                    const float* vns, const float* colc, const float* cols, const float* gout, float weight, float* dG,
+                    float* dun, float* dvn, int N, int C, int HW, void* stream);
+
+/* dst[n][0:per] = src[n][0:per] with batch strides (channel concat / split, AA/network.py:87) */
+int vst_copy_planes(const float* src, long src_bs, float* dst, long dst_bs, int N, long per, void* stream);
+/* D = 1 - G / (un_i vn_j + 1e-6) (cosine_distance forward) */
+int vst_cosdist(const float* G, const float* un, const float* vn, float* D, int N, int C, void* stream);
 
 /* ---- elementwise ---------------------------------------------------------------------------
  * vgg_normalize (RC/utilities.py:101-106): out = (x/255 - mean)/std, inplace_scale: x <- x/255 */

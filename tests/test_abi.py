@@ -10,7 +10,11 @@ from vst import _lib
 def test_header_parses_and_lists_entry_points():
     protos = _lib.parse_header()
     for name in ("vst_conv_gemm", "vst_conv_wgrad", "vst_gram", "vst_warp_fwd", "vst_warp_bwd", "vst_flow_warp_mask",
-                 "vst_instnorm_fwd", "vst_instnorm_bwd", "vst_masked_sqdiff_fwd", "vst_adam", "vst_strerror"):
+                 "vst_instnorm_fwd", "vst_instnorm_bwd", "vst_masked_sqdiff_fwd", "vst_adam", "vst_strerror",
+                 # AdaAttN path
+                 "vst_gemm_abt", "vst_pack_matrix", "vst_channel_norm", "vst_cos_attn_rows", "vst_cos_attn_rows_bwd",
+                 "vst_softmax_rows", "vst_softmax_rows_bwd", "vst_adaattn_out", "vst_adaattn_out_bwd",
+                 "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_copy_planes"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"
     assert len(protos["vst_conv_gemm"][1]) == 24
@@ -47,3 +51,13 @@ def test_product_fails_loudly_without_hip_tensors():
 
     with pytest.raises(_lib.VstError):
         ops.conv2d(torch.zeros(1, 3, 8, 8), torch.zeros(4, 3, 3, 3), None, pad=1)
+
+
+def test_adaattn_ops_fail_loudly_without_hip_tensors():
+    import torch
+
+    from vst.adaattn.attention import adaattn
+
+    q = torch.zeros(1, 8, 2, 2)
+    with pytest.raises(_lib.VstError):
+        adaattn(q, q, q, q, "cosine")

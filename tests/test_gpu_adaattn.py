@@ -1,0 +1,251 @@
+"""AdaAttN path: HIP kernels vs the oracle and the reference's golden
+vectors, on a real MI355X.
+
+Tolerances (north_star: "within 1e-3 relative fp32"):
+  * single ops vs the oracle (fp32 torch-CPU autograd): max|diff| <= 1e-4 * max|ref| forward,
+    1e-3 for gradients (long reductions through the attention matrix);
+  * module outputs vs golden: 1e-3 relative to the tensor's max magnitude;
+  * losses 1e-3 relative; gradients: per-tensor norm within 1e-3 (+1e-4 of the largest norm).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import adaattn_ref as A
+from oracle import reconet_ref as R
+from oracle import shapes
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def G(a):
+    return T(a).to(DEV) if isinstance(a, np.ndarray) else a.to(DEV)
+
+
+def C(t):
+    return t.detach().cpu()
+
+
+def _seeded(module, spec, seed):
+    params = oracle.seeded_params(spec, seed)
+    assert sorted(module.state_dict()) == sorted(params), "state_dict keys differ from the reference"
+    module.load_state_dict(params)
+    return module
+
+
+def test_state_dict_keys_match_reference():
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.vgg19 import VGG19
+
+    for mod, spec in ((StylizingNetwork("cosine"), shapes.stylizing_network()), (VGG19(), shapes.vgg19())):
+        sd = mod.state_dict()
+        assert [(k, tuple(v.shape)) for k, v in sd.items()] == [(k, tuple(s)) for k, s in spec]
+
+
+@pytest.mark.parametrize("activation", ["cosine", "softmax"])
+@pytest.mark.parametrize("dims", [(2, 40, 24, (5, 7), (6, 5)), (1, 64, 32, (8, 16), (8, 16)), (2, 16, 8, (1, 3), (2, 2))])
+def test_attention_fwd_bwd(activation, dims):
+    """AdaAttnFn vs a torch fp32 restatement of AA/network.py:191-220 (after the 1x1 convs)."""
+    from vst.adaattn.attention import adaattn
+
+    N, d, dv, (h, w), (hs, ws) = dims
+    g = torch.Generator().manual_seed(7)
+    Q = torch.randn(N, d, h, w, generator=g)
+    K = torch.randn(N, d, hs, ws, generator=g)
+    V = torch.rand(N, dv, hs, ws, generator=g) * 3
+    cn = torch.randn(N, dv, h, w, generator=g)
+    dout = torch.randn(N, dv, h, w, generator=g)
+
+    Qr, Kr, Vr = (t.clone().requires_grad_(True) for t in (Q, K, V))
+    qt = Qr.reshape(N, d, -1).permute(0, 2, 1)
+    km = Kr.reshape(N, d, -1)
+    vt = Vr.reshape(N, dv, -1).permute(0, 2, 1)
+    att = A.cosine_attention(qt, km) if activation == "cosine" else torch.softmax(torch.bmm(qt, km), dim=-1)
+    M = torch.bmm(att, vt)
+    S = torch.sqrt((torch.bmm(att, vt ** 2) - M ** 2).clamp(min=1e-6))
+    ref = (S.reshape(N, h, w, -1).permute(0, 3, 1, 2) * cn + M.reshape(N, h, w, -1).permute(0, 3, 1, 2))
+    ref.backward(dout)
+
+    Qg, Kg, Vg = (G(t).requires_grad_(True) for t in (Q, K, V))
+    out = adaattn(Qg, Kg, Vg, G(cn), activation)
+    out.backward(G(dout))
+    assert rel_err(C(out), ref.detach()) < 1e-4
+    for a, b, nm in ((Qg, Qr, "dQ"), (Kg, Kr, "dK"), (Vg, Vr, "dV")):
+        assert rel_err(C(a.grad), b.grad) < 1e-3, nm
+
+
+def test_resize_concat_ops_bwd():
+    """upsample2x(+addend), upsample_cat and feature_down_sample vs torch fp32 autograd."""
+    from vst import ops
+    from vst.adaattn.utilities import feature_down_sample
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 5, 3, 7, generator=g)
+    y = torch.randn(2, 4, 6, 14, generator=g)
+    xr, yr = x.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    up = A.upsample2(xr)
+    w1, w2 = torch.randn(2, 5, 6, 14, generator=g), torch.randn(2, 9, 6, 14, generator=g)
+    (up * w1).sum().backward()
+    xg = G(x).requires_grad_(True)
+    (ops.upsample2x(xg) * G(w1)).sum().backward()
+    assert rel_err(C(xg.grad), xr.grad) < 1e-5
+    # addend form: up(x5) + x4
+    a = torch.randn(2, 5, 6, 14, generator=g)
+    xg = G(x).requires_grad_(True)
+    ag = G(a).requires_grad_(True)
+    o = ops.upsample2x(xg, addend=ag)
+    assert rel_err(C(o), A.upsample2(x) + a) < 1e-5
+    (o * G(w1)).sum().backward()
+    assert rel_err(C(ag.grad), w1) == 0.0
+    # cat([up(x), y])
+    xr = x.clone().requires_grad_(True)
+    ref = torch.cat([A.upsample2(xr), yr], dim=1)
+    (ref * w2).sum().backward()
+    xg, yg = G(x).requires_grad_(True), G(y).requires_grad_(True)
+    o = ops.upsample_cat(xg, yg)
+    assert rel_err(C(o), ref.detach()) < 1e-5
+    (o * G(w2)).sum().backward()
+    assert rel_err(C(xg.grad), xr.grad) < 1e-5 and rel_err(C(yg.grad), yr.grad) == 0.0
+    # feature_down_sample with gradient to every level
+    feats = [torch.randn(2, c, hh, ww, generator=g) for c, hh, ww in ((3, 16, 20), (4, 8, 10), (5, 4, 5))]
+    fr = [f.clone().requires_grad_(True) for f in feats]
+    ref = A.feature_down_sample(fr, 2)
+    wt = torch.randn(ref.shape, generator=g)
+    (ref * wt).sum().backward()
+    fg = [G(f).requires_grad_(True) for f in feats]
+    o = feature_down_sample(fg, 2)
+    assert rel_err(C(o), ref.detach()) < 1e-5
+    (o * G(wt)).sum().backward()
+    for a_, b_ in zip(fg, fr):
+        assert rel_err(C(a_.grad), b_.grad) < 1e-5
+
+
+def test_losses_fwd_bwd():
+    from vst.adaattn import lossfn as L
+
+    g = torch.Generator().manual_seed(5)
+    fcs = torch.rand(2, 24, 6, 10, generator=g) * 2
+    fs = torch.rand(2, 24, 6, 10, generator=g)
+    fr = fcs.clone().requires_grad_(True)
+    ref = A.global_stylized_loss(fr, fs) * 10
+    ref.backward()
+    fg = G(fcs).requires_grad_(True)
+    got = L.global_stylized_loss(fg, G(fs), torch.nn.MSELoss(), weight=10.0)
+    got.backward()
+    assert rel_err(C(got), ref.detach()) < 1e-5 and rel_err(C(fg.grad), fr.grad) < 1e-4
+    # image similarity: gradient w.r.t. both stylised maps; cosine distance forward
+    c1, c2 = torch.rand(2, 24, 6, 10, generator=g), torch.rand(2, 24, 6, 10, generator=g)
+    s1, s2 = torch.rand(2, 24, 6, 10, generator=g), torch.rand(2, 24, 6, 10, generator=g)
+    s1r, s2r = s1.clone().requires_grad_(True), s2.clone().requires_grad_(True)
+    ref = A.image_similarity_loss(c1, c2, s1r, s2r) * 100
+    ref.backward()
+    s1g, s2g = G(s1).requires_grad_(True), G(s2).requires_grad_(True)
+    got = L.image_similarity_loss(G(c1), G(c2), s1g, s2g, weight=100.0)
+    got.backward()
+    assert rel_err(C(got), ref.detach()) < 1e-5
+    assert rel_err(C(s1g.grad), s1r.grad) < 1e-3 and rel_err(C(s2g.grad), s2r.grad) < 1e-3
+    assert rel_err(C(L.cosine_distance(G(c1), G(s2))), A.cosine_distance(c1, s2)) < 1e-5
+    # local feature loss = mse
+    got = L.local_feature_loss(G(s1), G(s2), torch.nn.MSELoss())
+    assert rel_err(C(got), torch.nn.functional.mse_loss(s1, s2)) < 1e-5
+
+
+def test_decoder_fwd_bwd():
+    """Decoder (AA/network.py:63-99) forward and input/weight gradients vs the oracle."""
+    from vst.adaattn.network import StylizingNetwork
+
+    P = oracle.seeded_params(shapes.stylizing_network(), 9, requires_grad=True)
+    g = torch.Generator().manual_seed(11)
+    x3 = torch.rand(1, 256, 8, 12, generator=g)
+    x4 = torch.rand(1, 512, 4, 6, generator=g)
+    x5 = torch.rand(1, 512, 2, 3, generator=g)
+    ins = [t.clone().requires_grad_(True) for t in (x5, x4, x3)]
+    ref = A.decoder(P, *ins)
+    wt = torch.randn(ref.shape, generator=g)
+    (ref * wt).sum().backward()
+    net = _seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), 9).to(DEV)
+    gi = [G(t).requires_grad_(True) for t in (x5, x4, x3)]
+    out = net.decoder(*gi)
+    assert rel_err(C(out), ref.detach()) < 1e-4
+    (out * G(wt)).sum().backward()
+    for a, b in zip(gi, ins):
+        assert rel_err(C(a.grad), b.grad) < 1e-3
+    named = dict(net.named_parameters())
+    for n in ("decoder.conv1.conv.conv.weight", "decoder.conv3.0.conv.conv.weight", "decoder.conv8.conv.bias"):
+        assert rel_err(C(named[n].grad), P[n].grad) < 1e-3, n
+
+
+def test_units_golden(golden):
+    """VGG19, feature_down_sample, AdaAttnNoConv, AdaAttN, StylizingNetwork and the loss
+    functions vs the reference's own outputs (tests/golden/aa_units.npz)."""
+    from vst.adaattn import lossfn as L
+    from vst.adaattn.network import AdaAttnNoConv, StylizingNetwork
+    from vst.adaattn.utilities import feature_down_sample
+    from vst.adaattn.vgg19 import VGG19
+
+    u = golden("aa_units")
+    vgg = _seeded(VGG19(), shapes.vgg19(), 31).to(DEV)
+    net = _seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), 32).to(DEV)
+    with torch.no_grad():
+        fx, fs = vgg(G(u["x"])), vgg(G(u["s"]))
+        for k in A.FEATS:
+            assert rel_err(C(fx[k]), u[f"vgg19_x_{k}"]) < 1e-3, k
+        lx, ls = list(fx.values()), list(fs.values())
+        for idx in (2, 3, 4):
+            assert rel_err(C(feature_down_sample(lx, idx)), u[f"fds_x_{idx}"]) < 1e-3
+        for i, (vd, qd) in enumerate(shapes.ADAATTN_LEVELS):
+            idx = i + 2
+            c1, s1 = feature_down_sample(lx, idx), feature_down_sample(ls, idx)
+            nc = AdaAttnNoConv(vd, qd, "cosine").to(DEV)
+            assert rel_err(C(nc(lx[idx], ls[idx], c1, s1)), u[f"noconv{i}"]) < 1e-3, i
+            assert rel_err(C(net.adaattn[i](lx[idx], ls[idx], c1, s1)), u[f"adaattn{i}"]) < 1e-3, i
+        assert rel_err(C(net(fx, fs)), u["stylized"]) < 1e-3
+        mse = torch.nn.MSELoss()
+        for k in ("relu2_1", "relu3_1", "relu4_1", "relu5_1"):
+            assert rel_err(L.global_stylized_loss(fx[k], fs[k], mse).item(), u[f"gsl_{k}"]) < 1e-3, k
+        for k in ("relu2_1", "relu3_1", "relu4_1"):
+            assert rel_err(C(L.cosine_distance(fx[k], fs[k])), u[f"cosd_{k}"]) < 1e-3, k
+            got = L.image_similarity_loss(fx[k], fs[k], fs[k] * 0.5 + 1.0, fx[k]).item()
+            assert rel_err(got, u[f"isl_{k}"]) < 1e-3, k
+
+
+def test_train_video_step_golden(golden):
+    """One full train_video step (losses, gradients, Adam update) vs the reference's own train()."""
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+
+    s = golden("aa_step")
+    seeds = s["seeds"]
+    model = _seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), int(seeds[0])).to(DEV)
+    vgg = _seeded(VGG19(), shapes.vgg19(), int(seeds[1])).to(DEV)
+    tr = AdaAttNTrainer(model, vgg, activation="cosine")
+    frames = torch.stack([G(s["c1"]), G(s["c2"]), G(s["style"])])
+    tr.flat.zero_grad()
+    out = tr.losses(frames)
+    for k in ("loss", "loss_gs", "loss_lf", "loss_is"):
+        assert rel_err(out[k].item(), s[k]) < 1e-3, k
+    out["loss"].backward()
+    names = list(s["names"])
+    named = dict(model.named_parameters())
+    gmax = max(float(s[f"gnorm/{n}"]) for n in names)
+    for n in names:
+        gr = C(named[n].grad).reshape(-1)
+        gn = float(s[f"gnorm/{n}"])
+        assert abs(float(gr.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"gidx/{n}"]
+        assert np.abs(gr[idx].numpy() - s[f"gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+    tr.flat.adam(1, tr.lr, tr.betas, tr.eps)
+    for n in names:
+        gh = s[f"ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        got = C(named[n]).reshape(-1)[:64].numpy()
+        assert np.abs(got - s[f"phead/{n}"])[sel].max(initial=0) < 1e-5, n

@@ -1,0 +1,501 @@
+// AdaAttN path kernels for gfx950 (AA/network.py:102-220, AA/lossfn.py:5-53, AA/utilities.py:98-109).
+//
+// The attention matrices are materialised (HBM is 288 GB): S = Q^T K and A = cosine-normalised S
+// per image, with the four products (S = Q^T K, [M; E2] = A [V; V^2], and the backward
+// dA = [dM; dE2]^T [V; V^2], d[V; V^2] = [dM; dE2] A, dQ = K dS^T, dK = Q dS) running on the
+// fp32-MFMA GEMM kernels (conv_gemm_kernel with 1x1 "convs", wgrad_kernel as A B^T); this file
+// holds the row/column/elementwise parts and the small C x C loss math.
+#include "vst_common.h"
+#include "vst_hip.h"
+
+namespace {
+
+constexpr int RT = 256;
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += sh[i];
+  return s;
+}
+
+// packed GEMM A operand from a row-major matrix per batch: X[k][m] (transpose=0) or X[m][k]
+__global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restrict__ out, int B, int M, int K,
+                                   int transpose, int Mpad, int Kpad, long x_bs) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long per = (long)Mpad * Kpad;
+  if (idx >= B * per) return;
+  int b = (int)(idx / per);
+  long t = idx - b * per;
+  int m = (int)(t % Mpad), k = (int)(t / Mpad);
+  float v = 0.f;
+  if (m < M && k < K) v = transpose ? x[b * x_bs + (long)m * K + k] : x[b * x_bs + (long)k * M + m];
+  out[b * per + apack_index(k, m, Mpad)] = v;
+}
+
+// out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
+__global__ void channel_norm_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int C, int P) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * P) return;
+  int n = (int)(idx / P), p = (int)(idx % P);
+  const float* xp = x + (long)n * C * P + p;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float v = xp[(long)c * P];
+    s += v * v;
+  }
+  out[idx] = sqrtf(s);
+}
+
+// cosine attention rows (AA/network.py:121-124): s = S/(qn_i kn_j) + 1, A = s / sum_j s
+__global__ void cos_rows_fwd_kernel(const float* __restrict__ S, const float* __restrict__ qn,
+                                    const float* __restrict__ kn, float* __restrict__ A, float* __restrict__ rowsum,
+                                    int Nc, int Ns) {
+  __shared__ double sh[RT / 64];
+  const long row = blockIdx.x;  // n * Nc + i
+  const int n = (int)(row / Nc);
+  const float q = qn[row];
+  const float* knn = kn + (long)n * Ns;
+  const float* Sr = S + row * Ns;
+  float* Ar = A + row * Ns;
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < Ns; j += RT) acc += Sr[j] / (q * knn[j]) + 1.0f;
+  const float tot = (float)block_sum_d(acc, sh);
+  for (int j = threadIdx.x; j < Ns; j += RT) Ar[j] = (Sr[j] / (q * knn[j]) + 1.0f) / tot;
+  if (threadIdx.x == 0) rowsum[row] = tot;
+}
+
+// backward through the row normalisation and the cosine scaling, per row i:
+//   r = sum_j dA A;  dSraw = (dA - r) / (rowsum * qn_i * kn_j);  t = dSraw * S (written over S)
+//   dqn_i = -(sum_j t) / qn_i
+__global__ void cos_rows_bwd_kernel(const float* __restrict__ dA, const float* __restrict__ A,
+                                    float* __restrict__ S_t, const float* __restrict__ qn,
+                                    const float* __restrict__ kn, const float* __restrict__ rowsum,
+                                    float* __restrict__ dS, float* __restrict__ dqn, int Nc, int Ns) {
+  __shared__ double sh[RT / 64];
+  const long row = blockIdx.x;
+  const int n = (int)(row / Nc);
+  const float* knn = kn + (long)n * Ns;
+  const float* dAr = dA + row * Ns;
+  const float* Ar = A + row * Ns;
+  double r = 0.0;
+  for (int j = threadIdx.x; j < Ns; j += RT) r += (double)dAr[j] * Ar[j];
+  const float rr = (float)block_sum_d(r, sh);
+  const float q = qn[row], inv = 1.0f / rowsum[row];
+  float* Sr = S_t + row * Ns;
+  float* dSr = dS + row * Ns;
+  double tsum = 0.0;
+  for (int j = threadIdx.x; j < Ns; j += RT) {
+    float d = (dAr[j] - rr) * inv / (q * knn[j]);
+    dSr[j] = d;
+    float t = d * Sr[j];
+    Sr[j] = t;
+    tsum += t;
+  }
+  const float ts = (float)block_sum_d(tsum, sh);
+  if (threadIdx.x == 0) dqn[row] = -ts / q;
+}
+
+// column sums of X [N][R][Cc] in row chunks: part[n][chunk][j]
+__global__ void colsum_part_kernel(const float* __restrict__ X, float* __restrict__ part, int R, int Cc, int chunk) {
+  const int j = blockIdx.x * RT + threadIdx.x;
+  const int ch = blockIdx.y, n = blockIdx.z;
+  if (j >= Cc) return;
+  const int r0 = ch * chunk, r1 = min(R, r0 + chunk);
+  const float* x = X + ((long)n * R) * Cc + j;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += x[(long)r * Cc];
+  part[((long)n * gridDim.y + ch) * Cc + j] = s;
+}
+
+// dkn_j = -(sum over chunks) / kn_j
+__global__ void colsum_finish_kernel(const float* __restrict__ part, const float* __restrict__ kn,
+                                     float* __restrict__ dkn, int N, int nch, int Cc) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * Cc) return;
+  int n = (int)(idx / Cc), j = (int)(idx % Cc);
+  double s = 0.0;
+  for (int c = 0; c < nch; ++c) s += part[((long)n * nch + c) * Cc + j];
+  dkn[idx] = -(float)s / kn[idx];
+}
+
+// X[n][c][p] += s[n][p] / nrm[n][p] * Y[n][c][p]   (gradient through a channel-axis norm)
+__global__ void norm_grad_add_kernel(float* __restrict__ X, const float* __restrict__ s, const float* __restrict__ nrm,
+                                     const float* __restrict__ Y, int N, int C, int P) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * C * P) return;
+  int p = (int)(idx % P);
+  long n = idx / ((long)C * P);
+  long q = n * P + p;
+  X[idx] += s[q] / nrm[q] * Y[idx];
+}
+
+// VV2[n] = [V[n]; V[n]^2]
+__global__ void square_concat_kernel(const float* __restrict__ V, float* __restrict__ VV2, int N, long per) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  float v = V[idx];
+  VV2[n * 2 * per + t] = v;
+  VV2[n * 2 * per + per + t] = v * v;
+}
+
+// dV = d[V] + 2 V d[V^2]
+__global__ void square_concat_bwd_kernel(const float* __restrict__ dVV2, const float* __restrict__ V,
+                                         float* __restrict__ dV, int N, long per) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  dV[idx] = dVV2[n * 2 * per + t] + 2.0f * V[idx] * dVV2[n * 2 * per + per + t];
+}
+
+// out = sqrt(clamp(E2 - M^2, 1e-6)) * cn + M   with MV[n] = [M; E2]  (AA/network.py:209-220)
+__global__ void adaattn_out_kernel(const float* __restrict__ MV, const float* __restrict__ cn, float* __restrict__ out,
+                                   int N, long per) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  const float m = MV[n * 2 * per + t], e2 = MV[n * 2 * per + per + t];
+  const float var = e2 - m * m;
+  out[idx] = sqrtf(fmaxf(var, 1e-6f)) * cn[idx] + m;
+}
+
+__global__ void adaattn_out_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ MV,
+                                       const float* __restrict__ cn, float* __restrict__ dMV, int N, long per) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  const float m = MV[n * 2 * per + t], e2 = MV[n * 2 * per + per + t];
+  const float var = e2 - m * m;
+  const float g = dout[idx];
+  // clamp(min) passes the gradient where var >= 1e-6 (torch clamp backward: x >= min)
+  const float dvar = var >= 1e-6f ? g * cn[idx] * 0.5f / sqrtf(var) : 0.f;
+  dMV[n * 2 * per + t] = g - 2.0f * m * dvar;
+  dMV[n * 2 * per + per + t] = dvar;
+}
+
+// per-plane mean and unbiased std (torch .mean / .std over (H, W))
+__global__ void plane_meanstd_kernel(const float* __restrict__ x, float* __restrict__ mean, float* __restrict__ std_,
+                                     int HW) {
+  __shared__ double sh[RT / 64];
+  const long plane = blockIdx.x;
+  const float* xp = x + plane * HW;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < HW; i += RT) s += xp[i];
+  const double mu = block_sum_d(s, sh) / HW;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < HW; i += RT) {
+    double d = xp[i] - mu;
+    q += d * d;
+  }
+  const double var = block_sum_d(q, sh) / (HW - 1);
+  if (threadIdx.x == 0) {
+    mean[plane] = (float)mu;
+    std_[plane] = (float)sqrt(var);
+  }
+}
+
+__global__ void plane_meanstd_bwd_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                         const float* __restrict__ std_, const float* __restrict__ gmean,
+                                         const float* __restrict__ gstd, float* __restrict__ gx, int HW) {
+  const long plane = blockIdx.x;
+  const float mu = mean[plane], sd = std_[plane];
+  const float a = gmean ? gmean[plane] / HW : 0.f;
+  const float b = (gstd && sd > 0.f) ? gstd[plane] / ((HW - 1) * sd) : 0.f;
+  const float* xp = x + plane * HW;
+  float* gp = gx + plane * HW;
+  for (int i = threadIdx.x; i < HW; i += RT) gp[i] = a + b * (xp[i] - mu);
+}
+
+// per-plane L2 norms: out[plane] = sqrt(sum x^2)
+__global__ void plane_norm_kernel(const float* __restrict__ x, float* __restrict__ out, int HW) {
+  __shared__ double sh[RT / 64];
+  const long plane = blockIdx.x;
+  const float* xp = x + plane * HW;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < HW; i += RT) s += (double)xp[i] * xp[i];
+  const double t = block_sum_d(s, sh);
+  if (threadIdx.x == 0) out[plane] = (float)sqrt(t);
+}
+
+// image_similarity_loss core (AA/lossfn.py:25-53) for one image n, both cosine distances:
+//   D = 1 - G / (un_i vn_j + 1e-6);  Dn = D / colsum_j(D);  loss_n = sum |Dn_c - Dn_cs| / hw
+// one block per image; grid-stride over C x C; writes Dn_cs and colsums for backward.
+__global__ void simloss_kernel(const float* __restrict__ Gc, const float* __restrict__ unc, const float* __restrict__ vnc,
+                               const float* __restrict__ Gs, const float* __restrict__ uns, const float* __restrict__ vns,
+                               float* __restrict__ colc, float* __restrict__ cols, float* __restrict__ partial, int C,
+                               float inv_hw) {
+  __shared__ double sh[RT / 64];
+  const int n = blockIdx.x;
+  const long o = (long)n * C * C;
+  // column sums (over rows i) of both distance matrices
+  for (int j = threadIdx.x; j < C; j += RT) {
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < C; ++i) {
+      a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f);
+      b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vns[n * C + j] + 1e-6f);
+    }
+    colc[n * C + j] = (float)a;
+    cols[n * C + j] = (float)b;
+  }
+  __syncthreads();
+  double acc = 0.0;
+  for (long t = threadIdx.x; t < (long)C * C; t += RT) {
+    const int i = (int)(t / C), j = (int)(t % C);
+    const float dc = (1.0f - Gc[o + t] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f)) / colc[n * C + j];
+    const float ds = (1.0f - Gs[o + t] / (uns[n * C + i] * vns[n * C + j] + 1e-6f)) / cols[n * C + j];
+    acc += fabsf(dc - ds);
+  }
+  const double tot = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) partial[n] = (float)tot * inv_hw;
+}
+
+// backward w.r.t. the stylised side: dG (C x C) plus dun (rows) and dvn (cols), scaled by gscale
+__global__ void simloss_bwd_kernel(const float* __restrict__ Gc, const float* __restrict__ unc,
+                                   const float* __restrict__ vnc, const float* __restrict__ Gs,
+                                   const float* __restrict__ uns, const float* __restrict__ vns,
+                                   const float* __restrict__ colc, const float* __restrict__ cols,
+                                   const float* __restrict__ gout, float weight, float* __restrict__ dG,
+                                   float* __restrict__ dun, float* __restrict__ dvn, int C, float inv_hw) {
+  // one block per (n, column j): dDn_ij = sign(Ds_n - Dc_n) * g / hw;  dD_ij = (dDn_ij - sum_i dDn Dn) / colsum_j
+  __shared__ double sh[RT / 64];
+  const int n = blockIdx.y, j = blockIdx.x;
+  const long o = (long)n * C * C;
+  const float g = gout[0] * weight * inv_hw;
+  const float cs = cols[n * C + j], cc = colc[n * C + j];
+  const float vj = vns[n * C + j];
+  double r = 0.0;
+  for (int i = threadIdx.x; i < C; i += RT) {
+    const float den = uns[n * C + i] * vj + 1e-6f;
+    const float ds = (1.0f - Gs[o + (long)i * C + j] / den) / cs;
+    const float dc = (1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f)) / cc;
+    const float sg = ds > dc ? g : (ds < dc ? -g : 0.f);
+    r += (double)sg * ds;
+  }
+  const float rr = (float)block_sum_d(r, sh);
+  double dvacc = 0.0;
+  for (int i = threadIdx.x; i < C; i += RT) {
+    const float den = uns[n * C + i] * vj + 1e-6f;
+    const float G = Gs[o + (long)i * C + j];
+    const float ds = (1.0f - G / den) / cs;
+    const float dc = (1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f)) / cc;
+    const float sg = ds > dc ? g : (ds < dc ? -g : 0.f);
+    const float dD = (sg - rr) / cs;  // grad w.r.t. D_ij (un-normalised distance)
+    // D = 1 - G/den: dG = -dD/den; d(den) = dD * G / den^2
+    dG[o + (long)i * C + j] = -dD / den;
+    const float dden = dD * G / (den * den);
+    atomicAdd(&dun[n * C + i], dden * vj);
+    dvacc += (double)dden * uns[n * C + i];
+  }
+  const double dv = block_sum_d(dvacc, sh);
+  if (threadIdx.x == 0) dvn[n * C + j] = (float)dv;
+}
+
+// x[plane][i] += s[plane] / nrm[plane] * y[plane][i]   (gradient through per-plane L2 norms)
+__global__ void plane_norm_grad_kernel(float* __restrict__ x, const float* __restrict__ s,
+                                       const float* __restrict__ nrm, const float* __restrict__ y, int HW) {
+  const long plane = blockIdx.x;
+  const float k = nrm[plane] > 0.f ? s[plane] / nrm[plane] : 0.f;
+  for (int i = threadIdx.x; i < HW; i += RT) x[plane * HW + i] += k * y[plane * HW + i];
+}
+
+}  // namespace
+
+extern "C" {
+
+int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int transpose, int Mpad, int Kpad, long x_bs,
+                    void* stream) {
+  VST_CHECK_ARG(x && packed && B > 0 && M > 0 && K > 0 && Mpad >= M && Kpad >= K);
+  long total = (long)B * Mpad * Kpad;
+  pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, packed, B, M, K, transpose, Mpad, Kpad,
+                                                                            x_bs);
+  return vst_launch_status();
+}
+
+int vst_channel_norm(const float* x, float* out, int N, int C, int P, void* stream) {
+  VST_CHECK_ARG(x && out && N > 0 && C > 0 && P > 0);
+  channel_norm_kernel<<<ceil_div((long)N * P, 256), 256, 0, (hipStream_t)stream>>>(x, out, N, C, P);
+  return vst_launch_status();
+}
+
+int vst_cos_attn_rows(const float* S, const float* qn, const float* kn, float* A, float* rowsum, int N, int Nc, int Ns,
+                      void* stream) {
+  VST_CHECK_ARG(S && qn && kn && A && rowsum && N > 0 && Nc > 0 && Ns > 0);
+  cos_rows_fwd_kernel<<<N * Nc, RT, 0, (hipStream_t)stream>>>(S, qn, kn, A, rowsum, Nc, Ns);
+  return vst_launch_status();
+}
+
+// S_t: S on entry, overwritten with t = dS*S; part: N * ceil(Nc/64) * Ns floats
+int vst_cos_attn_rows_bwd(const float* dA, const float* A, float* S_t, const float* qn, const float* kn,
+                          const float* rowsum, float* dS, float* dqn, float* dkn, float* part, int N, int Nc, int Ns,
+                          void* stream) {
+  VST_CHECK_ARG(dA && A && S_t && qn && kn && rowsum && dS && dqn && dkn && part && N > 0 && Nc > 0 && Ns > 0);
+  hipStream_t st = (hipStream_t)stream;
+  cos_rows_bwd_kernel<<<N * Nc, RT, 0, st>>>(dA, A, S_t, qn, kn, rowsum, dS, dqn, Nc, Ns);
+  const int chunk = 64, nch = ceil_div(Nc, chunk);
+  dim3 g(ceil_div(Ns, RT), nch, N);
+  colsum_part_kernel<<<g, RT, 0, st>>>(S_t, part, Nc, Ns, chunk);
+  colsum_finish_kernel<<<ceil_div((long)N * Ns, 256), 256, 0, st>>>(part, kn, dkn, N, nch, Ns);
+  return vst_launch_status();
+}
+
+int vst_norm_grad_add(float* x, const float* s, const float* nrm, const float* y, int N, int C, int P, void* stream) {
+  VST_CHECK_ARG(x && s && nrm && y && N > 0 && C > 0 && P > 0);
+  norm_grad_add_kernel<<<ceil_div((long)N * C * P, 256), 256, 0, (hipStream_t)stream>>>(x, s, nrm, y, N, C, P);
+  return vst_launch_status();
+}
+
+int vst_square_concat(const float* V, float* VV2, int N, long per, void* stream) {
+  VST_CHECK_ARG(V && VV2 && N > 0 && per > 0);
+  square_concat_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(V, VV2, N, per);
+  return vst_launch_status();
+}
+
+int vst_square_concat_bwd(const float* dVV2, const float* V, float* dV, int N, long per, void* stream) {
+  VST_CHECK_ARG(dVV2 && V && dV && N > 0 && per > 0);
+  square_concat_bwd_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(dVV2, V, dV, N, per);
+  return vst_launch_status();
+}
+
+int vst_adaattn_out(const float* MV, const float* cn, float* out, int N, long per, void* stream) {
+  VST_CHECK_ARG(MV && cn && out && N > 0 && per > 0);
+  adaattn_out_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(MV, cn, out, N, per);
+  return vst_launch_status();
+}
+
+int vst_adaattn_out_bwd(const float* dout, const float* MV, const float* cn, float* dMV, int N, long per,
+                        void* stream) {
+  VST_CHECK_ARG(dout && MV && cn && dMV && N > 0 && per > 0);
+  adaattn_out_bwd_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(dout, MV, cn, dMV, N, per);
+  return vst_launch_status();
+}
+
+int vst_plane_meanstd(const float* x, float* mean, float* std_, long NC, int HW, void* stream) {
+  VST_CHECK_ARG(x && mean && std_ && NC > 0 && HW > 1);
+  plane_meanstd_kernel<<<NC, RT, 0, (hipStream_t)stream>>>(x, mean, std_, HW);
+  return vst_launch_status();
+}
+
+int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, const float* gmean, const float* gstd,
+                          float* gx, long NC, int HW, void* stream) {
+  VST_CHECK_ARG(x && mean && std_ && gx && NC > 0 && HW > 1);
+  plane_meanstd_bwd_kernel<<<NC, RT, 0, (hipStream_t)stream>>>(x, mean, std_, gmean, gstd, gx, HW);
+  return vst_launch_status();
+}
+
+int vst_plane_norm(const float* x, float* out, long NC, int HW, void* stream) {
+  VST_CHECK_ARG(x && out && NC > 0 && HW > 0);
+  plane_norm_kernel<<<NC, RT, 0, (hipStream_t)stream>>>(x, out, HW);
+  return vst_launch_status();
+}
+
+int vst_plane_norm_grad(float* x, const float* s, const float* nrm, const float* y, long NC, int HW, void* stream) {
+  VST_CHECK_ARG(x && s && nrm && y && NC > 0 && HW > 0);
+  plane_norm_grad_kernel<<<NC, RT, 0, (hipStream_t)stream>>>(x, s, nrm, y, HW);
+  return vst_launch_status();
+}
+
+// partial: N floats (per-image loss, already / hw); colc, cols: N*C
+int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
+                const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream) {
+  VST_CHECK_ARG(Gc && unc && vnc && Gs && uns && vns && colc && cols && partial && N > 0 && C > 0 && HW > 0);
+  simloss_kernel<<<N, RT, 0, (hipStream_t)stream>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, partial, C, 1.0f / HW);
+  return vst_launch_status();
+}
+
+// dun must be zeroed (atomic accumulation); dG, dvn fully written
+int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
+                    const float* vns, const float* colc, const float* cols, const float* gout, float weight, float* dG,
+                    float* dun, float* dvn, int N, int C, int HW, void* stream) {
+  VST_CHECK_ARG(Gc && unc && vnc && Gs && uns && vns && colc && cols && gout && dG && dun && dvn && N > 0 && C > 0);
+  dim3 g(C, N);
+  simloss_bwd_kernel<<<g, RT, 0, (hipStream_t)stream>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, gout, weight, dG, dun,
+                                                        dvn, C, 1.0f / HW);
+  return vst_launch_status();
+}
+
+}  // extern "C"
+
+namespace {
+__global__ void copy_planes_kernel(const float* __restrict__ src, long src_bs, float* __restrict__ dst, long dst_bs,
+                                   int N, long per) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  dst[n * dst_bs + t] = src[n * src_bs + t];
+}
+
+// D = 1 - G / (un_i vn_j + 1e-6)  (cosine_distance, AA/lossfn.py:25-38)
+__global__ void cosdist_kernel(const float* __restrict__ G, const float* __restrict__ un, const float* __restrict__ vn,
+                               float* __restrict__ D, int N, int C) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * C * C) return;
+  int j = (int)(idx % C);
+  long t = idx / C;
+  int i = (int)(t % C);
+  long n = t / C;
+  D[idx] = 1.0f - G[idx] / (un[n * C + i] * vn[n * C + j] + 1e-6f);
+}
+}  // namespace
+
+extern "C" int vst_copy_planes(const float* src, long src_bs, float* dst, long dst_bs, int N, long per, void* stream) {
+  VST_CHECK_ARG(src && dst && N > 0 && per > 0);
+  copy_planes_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(src, src_bs, dst, dst_bs, N, per);
+  return vst_launch_status();
+}
+
+extern "C" int vst_cosdist(const float* G, const float* un, const float* vn, float* D, int N, int C, void* stream) {
+  VST_CHECK_ARG(G && un && vn && D && N > 0 && C > 0);
+  cosdist_kernel<<<ceil_div((long)N * C * C, 256), 256, 0, (hipStream_t)stream>>>(G, un, vn, D, N, C);
+  return vst_launch_status();
+}
+
+namespace {
+// row softmax (nn.Softmax(dim=-1), AA/network.py:102-108): A = exp(S - max) / sum
+__global__ void softmax_rows_kernel(const float* __restrict__ S, float* __restrict__ A, int Ns) {
+  __shared__ float shm[RT / 64];
+  __shared__ double sh[RT / 64];
+  const long row = blockIdx.x;
+  const float* Sr = S + row * Ns;
+  float* Ar = A + row * Ns;
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < Ns; j += RT) mx = fmaxf(mx, Sr[j]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = shm[0];
+  for (int i = 1; i < RT / 64; ++i) mx = fmaxf(mx, shm[i]);
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < Ns; j += RT) acc += expf(Sr[j] - mx);
+  const float inv = (float)(1.0 / block_sum_d(acc, sh));
+  for (int j = threadIdx.x; j < Ns; j += RT) Ar[j] = expf(Sr[j] - mx) * inv;
+}
+
+// dS = A * (dA - sum_j dA A)
+__global__ void softmax_rows_bwd_kernel(const float* dA, const float* __restrict__ A, float* dS, int Ns) {
+  __shared__ double sh[RT / 64];
+  const long row = blockIdx.x;
+  const float* dAr = dA + row * Ns;
+  const float* Ar = A + row * Ns;
+  double r = 0.0;
+  for (int j = threadIdx.x; j < Ns; j += RT) r += (double)dAr[j] * Ar[j];
+  const float rr = (float)block_sum_d(r, sh);
+  for (int j = threadIdx.x; j < Ns; j += RT) dS[row * Ns + j] = Ar[j] * (dAr[j] - rr);
+}
+}  // namespace
+
+extern "C" int vst_softmax_rows(const float* S, float* A, long rows, int Ns, void* stream) {
+  VST_CHECK_ARG(S && A && rows > 0 && Ns > 0);
+  softmax_rows_kernel<<<rows, RT, 0, (hipStream_t)stream>>>(S, A, Ns);
+  return vst_launch_status();
+}
+
+extern "C" int vst_softmax_rows_bwd(const float* dA, const float* A, float* dS, long rows, int Ns, void* stream) {
+  VST_CHECK_ARG(dA && A && dS && rows > 0 && Ns > 0);
+  softmax_rows_bwd_kernel<<<rows, RT, 0, (hipStream_t)stream>>>(dA, A, dS, Ns);
+  return vst_launch_status();
+}

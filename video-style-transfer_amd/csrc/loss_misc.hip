@@ -152,6 +152,13 @@ __global__ void sqdiff_bwd_kernel(const float* __restrict__ a, const float* __re
   }
 }
 
+// sum of a vector (for per-image partial losses)
+__global__ void vsum_kernel(const float* __restrict__ x, long n, float* partial) {
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < n; i += (long)gridDim.x * RT) s += x[i];
+  block_partial(s, 0.f, partial);
+}
+
 // TV: sum over y<H-1, x<W-1 of (s[y][x+1]-s[y][x])^2 + (s[y+1][x]-s[y][x])^2  (train_candy.py:141-145)
 __global__ void tv_kernel(const float* __restrict__ s, long NC, int H, int W, float* partial) {
   float acc = 0.f;
@@ -320,6 +327,16 @@ int vst_mse_bwd(const float* a, const float* b, long n, long nb, const float* go
                 float* gb, void* stream) {
   VST_CHECK_ARG(a && b && gout && out && n > 0 && nb > 0 && (!gb || nb == n));
   sqdiff_bwd_kernel<<<nblocks(n), RT, 0, (hipStream_t)stream>>>(a, b, n, nb, gout, out, ga, gb);
+  return vst_launch_status();
+}
+
+// out = {weight * sum(x), weight, 0}
+int vst_sum_scaled(const float* x, long n, float weight, float* ws, float* out, void* stream) {
+  VST_CHECK_ARG(x && ws && out && n > 0);
+  hipStream_t st = (hipStream_t)stream;
+  int g = nblocks(n);
+  vsum_kernel<<<g, RT, 0, st>>>(x, n, ws);
+  finish_kernel<<<1, RT, 0, st>>>(ws, g, out, weight, 1.0, 0);
   return vst_launch_status();
 }
 

@@ -166,9 +166,10 @@ __device__ __forceinline__ void resize_axis(int d, int n_in, int n_out, int& i0,
   l1 = src - (float)i0;
 }
 
-// out[nc] = resize(x[nc]) * chscale[c % C] ; binarize: out = out > 0
+// out[n][c] = resize(x[nc]) * chscale[c] (+ addend[n][c]); binarize: out = out > 0
+// out/addend images are out_bs floats apart (channel-concat targets, AA/utilities.py:98-109)
 __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ out, long NC, int C, int H, int W, int Ho,
-                              int Wo, const float* chscale, int binarize) {
+                              int Wo, const float* chscale, int binarize, long out_bs, const float* __restrict__ addend) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NC * Ho * Wo) return;
   int ox = (int)(idx % Wo);
@@ -184,7 +185,30 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
             ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
   if (chscale) v *= chscale[nc % C];
   if (binarize) v = v > 0.f ? 1.f : 0.f;
-  out[idx] = v;
+  const long o = (nc / C) * out_bs + (nc % C) * (long)Ho * Wo + (long)oy * Wo + ox;
+  if (addend) v += addend[o];
+  out[o] = v;
+}
+
+// adjoint of the bilinear resize: scatter each output gradient to its 4 sources (float atomics)
+__global__ void resize_bwd_kernel(const float* __restrict__ gout, float* __restrict__ gx, long NC, int C, int H, int W,
+                                  int Ho, int Wo, long gout_bs) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * Ho * Wo) return;
+  int ox = (int)(idx % Wo);
+  long t = idx / Wo;
+  int oy = (int)(t % Ho);
+  long nc = t / Ho;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  resize_axis(oy, H, Ho, y0, y1, ly);
+  resize_axis(ox, W, Wo, x0, x1, lx);
+  const float g = gout[(nc / C) * gout_bs + (nc % C) * (long)Ho * Wo + (long)oy * Wo + ox];
+  float* p = gx + nc * H * W;
+  atomicAdd(p + (long)y0 * W + x0, g * (1.f - ly) * (1.f - lx));
+  atomicAdd(p + (long)y0 * W + x1, g * (1.f - ly) * lx);
+  atomicAdd(p + (long)y1 * W + x0, g * ly * (1.f - lx));
+  atomicAdd(p + (long)y1 * W + x1, g * ly * lx);
 }
 
 }  // namespace
@@ -229,11 +253,21 @@ int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int 
 }
 
 int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
-                        const float* chscale, int binarize, void* stream) {
-  VST_CHECK_ARG(x && out && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0);
+                        const float* chscale, int binarize, long out_bs, const float* addend, void* stream) {
+  VST_CHECK_ARG(x && out && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
   long total = NC * Ho * Wo;
+  if (out_bs <= 0) out_bs = (long)C * Ho * Wo;
   resize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, NC, C, H, W, Ho, Wo, chscale,
-                                                                       binarize);
+                                                                       binarize, out_bs, addend);
+  return vst_launch_status();
+}
+
+int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
+                            void* stream) {
+  VST_CHECK_ARG(gout && gx && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
+  long total = NC * Ho * Wo;
+  if (gout_bs <= 0) gout_bs = (long)C * Ho * Wo;
+  resize_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, gx, NC, C, H, W, Ho, Wo, gout_bs);
   return vst_launch_status();
 }
 

@@ -249,16 +249,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
   out[idx] = s;
 }
 
-// out[n][i][j] = scale * sum_{s<S} slab[n*S+s][i][j]
-__global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int N, int S, int C,
+// out[n][i][j] = scale * sum_{s<S} slab[n*S+s][i][j],  i < M, j < J
+__global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int N, int S, int M, int J,
                                    int Mpad, int Jpad, float scale) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * C * C;
+  long total = (long)N * M * J;
   if (idx >= total) return;
-  int j = (int)(idx % C);
-  long t = idx / C;
-  int i = (int)(t % C);
-  int n = (int)(t / C);
+  int j = (int)(idx % J);
+  long t = idx / J;
+  int i = (int)(t % M);
+  int n = (int)(t / M);
   long zs = (long)Mpad * Jpad;
   const float* p = slab + (long)n * S * zs + (long)i * Jpad + j;
   float s = 0.f;
@@ -399,7 +399,23 @@ int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, f
   int c = wsel(C);
   long Mpad = (C + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = (C + WBN - 1) / WBN * WBN;
   long total = (long)N * C * C;
-  gram_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, g, N, S, C, (int)Mpad, (int)Jpad, scale);
+  gram_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, g, N, S, C, C, (int)Mpad, (int)Jpad, scale);
+  return vst_launch_status();
+}
+
+// out[n][m][j] = scale * sum_r a[n][m][r] * b[n][j][r]   (per-image A B^T; AdaAttN moments,
+// attention query gradient, cosine-distance C x C products)
+int vst_gemm_abt(const float* a, const float* b, float* out, float* workspace, int N, int M, int J, int R, float scale,
+                 void* stream) {
+  VST_CHECK_ARG(a && b && out && workspace && N > 0 && M > 0 && J > 0 && R > 0);
+  int S = splits_for(N, M, J, R);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = run_wg(a, b, workspace, N, M, J, 1, R, 1, R, 1, 1, 1, 1, 0, 1, S, 0, 0, st);
+  if (rc) return rc;
+  int c = wsel(M);
+  long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = ((long)J + WBN - 1) / WBN * WBN;
+  long total = (long)N * M * J;
+  gram_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, out, N, S, M, J, (int)Mpad, (int)Jpad, scale);
   return vst_launch_status();
 }
 

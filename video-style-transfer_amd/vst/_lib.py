@@ -100,5 +100,15 @@ def ptr(t):
     return t.data_ptr()
 
 
+def ptr_rows(t):
+    """(device pointer, batch stride) of a tensor whose per-sample slices t[n] are contiguous
+    (e.g. a channel slice of a concat buffer); the batch stride may exceed t[0].numel()."""
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise VstError("vst ops need fp32 HIP (cuda) tensors; there is no CPU path")
+    if not t[0].is_contiguous():
+        raise VstError("vst ops need per-sample contiguous tensors")
+    return t.data_ptr(), t.stride(0)
+
+
 def stream():
     return torch.cuda.current_stream().cuda_stream

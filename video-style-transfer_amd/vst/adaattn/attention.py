@@ -1,0 +1,172 @@
+"""AdaAttN attention on HIP kernels (AA/network.py:102-220).
+
+Layout per image n (all fp32, HBM-resident, contiguous):
+  Q [d][Nc], K [d][Ns], V [dv][Ns]  (channel-major feature planes, Nc = h*w, Ns = hs*ws)
+  S [Nc][Ns] raw Q^T K, A [Nc][Ns] attention rows, VV2 [2dv][Ns] = [V; V^2], MV [2dv][Nc] = [M; E2]
+The reference forms Q^T, V^T by permute and runs torch.bmm; here every product reads the
+channel-major planes directly:
+  S   = Q^T K        conv_gemm 1x1 "conv", per-image packed A = pack(Q)      (MFMA)
+  MV  = VV2 A^T      gemm_abt (split-K MFMA)
+backward:
+  dA   = dMV^T VV2   conv_gemm, A = pack(dMV)
+  dVV2 = dMV A       conv_gemm, A = pack(dMV^T)
+  dQ   = K dS^T      gemm_abt,  then + dqn/qn * Q   (cosine norms)
+  dK   = Q dS        conv_gemm, A = pack(Q^T),    then + dkn/kn * K
+"""
+import torch
+from torch.autograd import Function
+
+from .. import ops
+from .._lib import VstError, lib, ptr, stream
+
+COSINE, SOFTMAX = "cosine", "softmax"
+
+
+def _empty(shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+def packed_matrix(x, M, K, transpose):
+    """Per-image packed GEMM A operand from x[n] = X[K][M] (transpose=False) or X[M][K]."""
+    N = x.shape[0]
+    Mpad, Kpad = ops.pack_dims(M, K)
+    ap = _empty((N * Kpad * Mpad,), x)
+    lib.vst_pack_matrix(ptr(x), ptr(ap), N, M, K, int(transpose), Mpad, Kpad, M * K, stream())
+    return ap, Kpad * Mpad
+
+
+def bmm_at_b(x, M, K, transpose, b, P, out=None):
+    """out[n] = Aop[n]^T-as-packed @ b[n]:  out[n][m][p] = sum_k Aop[n][k][m] b[n][k][p], where
+    Aop[n][k][m] = x[n][k][m] (transpose=False) or x[n][m][k] (transpose=True)."""
+    N = b.shape[0]
+    ap, abs_ = packed_matrix(x, M, K, transpose)
+    o = ops.conv_gemm(b.view(N, K, 1, P), ap, M, 1, 1, P, ops.GM_ZERO, 1, 0, 1, a_batch_stride=abs_,
+                      out=None if out is None else out.view(N, M, 1, P))
+    return o.view(N, M, P)
+
+
+def gemm_abt(a, b, scale=1.0):
+    """out[n][m][j] = scale * sum_r a[n][m][r] b[n][j][r]."""
+    N, M, R = a.shape
+    J = b.shape[1]
+    if b.shape[0] != N or b.shape[2] != R:
+        raise VstError(f"gemm_abt: {tuple(a.shape)} x {tuple(b.shape)}^T")
+    out = _empty((N, M, J), a)
+    ws = _empty((lib.vst_wgrad_workspace(N, M, J, R),), a)
+    from .. import kprof
+
+    tok = kprof.begin(2.0 * N * M * J * R)
+    lib.vst_gemm_abt(ptr(a), ptr(b), ptr(out), ptr(ws), N, M, J, R, float(scale), stream())
+    kprof.end(tok, family="gemm_abt")
+    return out
+
+
+def channel_norm(x):
+    """||x[n][:][p]||_2 over channels -> [N][P] (LA.vector_norm, AA/network.py:121-122)."""
+    N, C, P = x.shape
+    out = _empty((N, P), x)
+    lib.vst_channel_norm(ptr(x), ptr(out), N, C, P, stream())
+    return out
+
+
+def attention_rows(S, activation, qn=None, kn=None):
+    N, Nc, Ns = S.shape
+    A = _empty(S.shape, S)
+    if activation == COSINE:
+        rowsum = _empty((N, Nc), S)
+        lib.vst_cos_attn_rows(ptr(S), ptr(qn), ptr(kn), ptr(A), ptr(rowsum), N, Nc, Ns, stream())
+        return A, rowsum
+    if activation == SOFTMAX:
+        lib.vst_softmax_rows(ptr(S), ptr(A), N * Nc, Ns, stream())
+        return A, None
+    raise ValueError(f"Unknown activation function: {activation}")
+
+
+class AdaAttnFn(Function):
+    """out = sqrt(clamp(A V^2 - (A V)^2, 1e-6)) * cn + A V  with A = activation(Q^T K)
+    (AA/network.py:191-220 after the 1x1 convs; cn = norm_v(c_x)).  Gradients for Q, K, V."""
+
+    @staticmethod
+    def forward(ctx, Q, K, V, cn, activation):
+        N, d, h, w = Q.shape
+        _, _, hs, ws = K.shape
+        dv = V.shape[1]
+        Nc, Ns = h * w, hs * ws
+        if K.shape[:2] != (N, d) or V.shape != (N, dv, hs, ws) or cn.shape != (N, dv, h, w):
+            raise VstError(f"adaattn: Q{tuple(Q.shape)} K{tuple(K.shape)} V{tuple(V.shape)} c{tuple(cn.shape)}")
+        Q, K, V, cn = (ops._check(t, "adaattn operand", 4) for t in (Q, K, V, cn))
+        Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
+        qn = kn = None
+        if activation == COSINE:
+            qn, kn = channel_norm(Qm), channel_norm(Km)
+        S = bmm_at_b(Qm, Nc, d, False, Km, Ns)  # [N][Nc][Ns]
+        A, rowsum = attention_rows(S, activation, qn, kn)
+        VV2 = _empty((N, 2 * dv, Ns), V)
+        lib.vst_square_concat(ptr(V), ptr(VV2), N, dv * Ns, stream())
+        MV = gemm_abt(VV2, A)  # [N][2dv][Nc]
+        out = _empty((N, dv, h, w), V)
+        lib.vst_adaattn_out(ptr(MV), ptr(cn), ptr(out), N, dv * Nc, stream())
+        ctx.activation = activation
+        ctx.dims = (N, d, dv, Nc, Ns)
+        if any(ctx.needs_input_grad[:3]):
+            ctx.save_for_backward(Q, K, V, cn, qn, kn, S, A, rowsum, VV2, MV)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        Q, K, V, cn, qn, kn, S, A, rowsum, VV2, MV = ctx.saved_tensors
+        N, d, dv, Nc, Ns = ctx.dims
+        dout = dout.contiguous()
+        dMV = _empty(MV.shape, MV)
+        lib.vst_adaattn_out_bwd(ptr(dout), ptr(MV), ptr(cn), ptr(dMV), N, dv * Nc, stream())
+        dQ = dK = dV = None
+        if ctx.needs_input_grad[2]:
+            dVV2 = bmm_at_b(dMV, 2 * dv, Nc, True, A, Ns)  # [N][2dv][Ns]
+            dV = _empty(V.shape, V)
+            lib.vst_square_concat_bwd(ptr(dVV2), ptr(V), ptr(dV), N, dv * Ns, stream())
+            del dVV2
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            dA = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns)  # [N][Nc][Ns]
+            Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
+            if ctx.activation == COSINE:
+                dS = _empty(S.shape, S)
+                dqn = _empty((N, Nc), S)
+                dkn = _empty((N, Ns), S)
+                part = _empty((N * ((Nc + 63) // 64) * Ns,), S)
+                lib.vst_cos_attn_rows_bwd(ptr(dA), ptr(A), ptr(S), ptr(qn), ptr(kn), ptr(rowsum), ptr(dS), ptr(dqn),
+                                          ptr(dkn), ptr(part), N, Nc, Ns, stream())
+                del dA, part
+            else:
+                dS = dA
+                lib.vst_softmax_rows_bwd(ptr(dA), ptr(A), ptr(dS), N * Nc, Ns, stream())
+            if ctx.needs_input_grad[0]:
+                dQ = gemm_abt(Km, dS)  # [N][d][Nc]
+                if ctx.activation == COSINE:
+                    lib.vst_norm_grad_add(ptr(dQ), ptr(dqn), ptr(qn), ptr(Qm), N, d, Nc, stream())
+                dQ = dQ.view(Q.shape)
+            if ctx.needs_input_grad[1]:
+                dK = bmm_at_b(Qm, d, Nc, True, dS, Ns)  # [N][d][Ns]
+                if ctx.activation == COSINE:
+                    lib.vst_norm_grad_add(ptr(dK), ptr(dkn), ptr(kn), ptr(Km), N, d, Ns, stream())
+                dK = dK.view(K.shape)
+        if ctx.needs_input_grad[3]:
+            raise VstError("adaattn: gradient w.r.t. the content features (norm_v(c_x)) is not on the reference path")
+        return dQ, dK, dV, None, None
+
+
+def adaattn(Q, K, V, cn, activation=COSINE):
+    return AdaAttnFn.apply(Q, K, V, cn, activation)
+
+
+_AFFINE_ID = {}
+
+
+def instance_norm_plain(x, eps=1e-5):
+    """nn.InstanceNorm2d(C, affine=False) (running stats off): the affine IN kernel with w=1, b=0."""
+    C = x.shape[1]
+    key = (x.device, C)
+    wb = _AFFINE_ID.get(key)
+    if wb is None:
+        wb = (torch.ones(C, device=x.device), torch.zeros(C, device=x.device))
+        _AFFINE_ID[key] = wb
+    return ops.instance_norm(x, wb[0], wb[1], eps=eps)

@@ -1,0 +1,85 @@
+"""AdaAttN video training step (AA/train_video.py:78-118) on MI355X, single- or multi-GPU.
+
+Per step, exactly the reference loop body:
+  fc1, fc2, fs = VGG19(content1), VGG19(content2), VGG19(style)          (no gradient: data)
+  cs1, cs2 = model(fc1, fs), model(fc2, fs);  fcs1, fcs2 = VGG19(cs1), VGG19(cs2)
+  loss_gs = LAMBDA_G  * sum_{relu2_1..relu5_1} global_stylized_loss(fcs1, fs)
+  loss_lf = LAMBDA_L  * sum_{i=0..2} mse(fcs1[relu{i+3}_1], AdaAttnNoConv_i(fc1, fs))
+  loss_is = LAMBDA_IS * sum_{relu2_1..relu4_1} image_similarity_loss(fc1, fc2, fcs1, fcs2)
+  backward, Adam(lr=1e-4).
+The loss weights are folded into the loss kernels' reductions.  The three data encodings run as
+one VGG19 pass of 3B when the inputs are handed over as one [3, B, 3, H, W] buffer.
+
+Multi-GPU: one process per GPU, (content1, content2, style) triples sharded across ranks, one
+RCCL all-reduce of the flat gradient per step; Adam applies the 1/world average.  Every loss term
+is a per-rank mean or per-rank sum exactly as the reference computes it on its own batch.
+"""
+import torch
+
+from ..reconet._flat import FlatParams
+from ..reconet.dist import allreduce_grads, world_info
+from .lossfn import global_stylized_loss, image_similarity_loss, local_feature_loss
+from .network import AdaAttnNoConv
+from .utilities import feature_down_sample
+from .vgg19 import FEATURES
+
+LOSS_WEIGHTS = dict(LAMBDA_G=10.0, LAMBDA_L=3.0, LAMBDA_IS=100.0)
+
+
+class AdaAttNTrainer:
+    def __init__(self, model, vgg, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weights=None, activation="cosine",
+                 process_group=None):
+        self.model, self.vgg = model, vgg
+        self.w = dict(LOSS_WEIGHTS if weights is None else weights)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.flat = FlatParams(model)
+        dev = self.flat.p.device
+        self.noconv = [AdaAttnNoConv(v, q, activation).to(dev).eval()
+                       for v, q in ((256, 64 + 128 + 256), (512, 64 + 128 + 256 + 512),
+                                    (512, 64 + 128 + 256 + 512 + 512))]
+        self.step_count = 0
+        self.pg = process_group
+        self.rank, self.world = world_info(process_group)
+
+    def encode(self, c1, c2=None, s=None):
+        """VGG19 features of the data images (no gradient).  c1 may be a [3, B, 3, H, W] buffer."""
+        with torch.no_grad():
+            if c2 is None:
+                T, B = c1.shape[:2]
+                f = self.vgg(c1.reshape(T * B, *c1.shape[2:]))
+                return tuple({k: v[t * B:(t + 1) * B] for k, v in f.items()} for t in range(T))
+            return self.vgg(c1), self.vgg(c2), self.vgg(s)
+
+    def losses(self, c1, c2=None, s=None):
+        w = self.w
+        fc1, fc2, fs = self.encode(c1, c2, s)
+        cs1 = self.model(fc1, fs)
+        cs2 = self.model(fc2, fs)
+        fcs1 = self.vgg(cs1)
+        fcs2 = self.vgg(cs2)
+        gs = None
+        for k in FEATURES[1:]:
+            t = global_stylized_loss(fcs1[k], fs[k], weight=w["LAMBDA_G"])
+            gs = t if gs is None else gs + t
+        l1, ls = list(fc1.values()), list(fs.values())
+        lf = None
+        for i in range(3):
+            idx = i + 2
+            with torch.no_grad():
+                target = self.noconv[i](l1[idx], ls[idx], feature_down_sample(l1, idx), feature_down_sample(ls, idx))
+            t = local_feature_loss(fcs1[FEATURES[idx]], target, weight=w["LAMBDA_L"])
+            lf = t if lf is None else lf + t
+        isl = None
+        for k in FEATURES[1:4]:
+            t = image_similarity_loss(fc1[k], fc2[k], fcs1[k], fcs2[k], weight=w["LAMBDA_IS"])
+            isl = t if isl is None else isl + t
+        return {"loss": gs + lf + isl, "loss_gs": gs, "loss_lf": lf, "loss_is": isl}
+
+    def step(self, c1, c2=None, s=None):
+        self.flat.zero_grad()
+        out = self.losses(c1, c2, s)
+        out["loss"].backward()
+        gscale = allreduce_grads(self.flat.g, self.pg)
+        self.step_count += 1
+        self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
+        return {k: v.detach() for k, v in out.items()}

@@ -12,7 +12,7 @@ _active = None
 
 class KernelTimer:
     def __init__(self):
-        self.records = []  # (start, stop, flops)
+        self.records = []  # (start, stop, flops, family)
 
     def __enter__(self):
         global _active
@@ -23,11 +23,12 @@ class KernelTimer:
         global _active
         _active = None
 
-    def summary(self):
+    def summary(self, family="conv_gemm"):
         torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
-        flops = sum(f for _, _, f in self.records)
-        n = len(self.records)
+        recs = [r for r in self.records if r[3] == family]
+        ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
+        flops = sum(f for _, _, f, _ in recs)
+        n = len(recs)
         return {"launches": n, "total_ms": ms, "avg_us": 1e3 * ms / max(n, 1), "flops": flops,
                 "tflops": flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0}
 
@@ -40,9 +41,9 @@ def begin(flops):
     return (s, flops)
 
 
-def end(tok):
+def end(tok, family="conv_gemm"):
     if tok is None:
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    _active.records.append((tok[0], e, tok[1]))
+    _active.records.append((tok[0], e, tok[1], family))

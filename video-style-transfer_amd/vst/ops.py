@@ -9,7 +9,7 @@ import torch
 from torch.autograd import Function
 
 from . import kprof
-from ._lib import VstError, lib, ptr, stream
+from ._lib import VstError, lib, ptr, ptr_rows, stream
 
 GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
 EPI_BIAS, EPI_RELU, EPI_TANH, EPI_MASK, EPI_ACCUM = 1, 2, 4, 8, 16
@@ -524,13 +524,101 @@ def tv_loss(s, weight):
     return TVFn.apply(s, weight)
 
 
-# ------------------------------------------------------------------ no-grad helpers
-def resize_bilinear(x, size, chscale=None, binarize=False):
+# ------------------------------------------------------------------ resize / concat
+def resize_bilinear(x, size, chscale=None, binarize=False, out=None, addend=None):
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) [* chscale[c]] [> 0] [+ addend].
+    `out` may be a per-sample-contiguous slice of a larger buffer (channel concat)."""
     x = _check(x, "resize input", 4)
     N, C, H, W = x.shape
-    out = _empty((N, C) + tuple(size), x)
-    lib.vst_resize_bilinear(ptr(x), ptr(out), N * C, C, H, W, size[0], size[1], ptr(chscale), int(binarize), stream())
+    Ho, Wo = size
+    if out is None:
+        out = _empty((N, C, Ho, Wo), x)
+    if tuple(out.shape) != (N, C, Ho, Wo):
+        raise VstError(f"resize: out shape {tuple(out.shape)} != {(N, C, Ho, Wo)}")
+    optr, obs = ptr_rows(out)
+    if addend is not None:
+        addend = _check(addend, "resize addend", 4)
+        if tuple(addend.shape) != (N, C, Ho, Wo) or obs != C * Ho * Wo:
+            raise VstError("resize: addend must match a dense output")
+    lib.vst_resize_bilinear(ptr(x), optr, N * C, C, H, W, Ho, Wo, ptr(chscale), int(binarize),
+                            obs if obs != C * Ho * Wo else 0, ptr(addend), stream())
     return out
+
+
+def resize_bilinear_bwd(gout, x_shape):
+    """Adjoint of resize_bilinear w.r.t. x; gout may be a per-sample-contiguous slice."""
+    N, C, H, W = x_shape
+    Ho, Wo = gout.shape[2:]
+    gptr, gbs = ptr_rows(gout)
+    gx = _zeros(x_shape, gout)
+    lib.vst_resize_bilinear_bwd(gptr, ptr(gx), N * C, C, H, W, Ho, Wo, gbs if gbs != C * Ho * Wo else 0, stream())
+    return gx
+
+
+def copy_into(src, dst):
+    """dst[n] = src[n] for per-sample-contiguous src/dst (slices of concat buffers)."""
+    if tuple(src.shape) != tuple(dst.shape):
+        raise VstError(f"copy: shape {tuple(src.shape)} != {tuple(dst.shape)}")
+    sp, sbs = ptr_rows(src)
+    dp, dbs = ptr_rows(dst)
+    lib.vst_copy_planes(sp, sbs, dp, dbs, src.shape[0], src[0].numel(), stream())
+    return dst
+
+
+class Upsample2xFn(Function):
+    """F.interpolate(x, scale_factor=2, mode='bilinear', align_corners=False) [+ addend]
+    (AA/network.py:59, 80; the decoder's `self.upsample(x5) + x4`)."""
+
+    @staticmethod
+    def forward(ctx, x, addend):
+        x = _check(x, "upsample input", 4)
+        N, C, H, W = x.shape
+        ctx.shape = x.shape
+        ctx.has_add = addend is not None
+        return resize_bilinear(x, (2 * H, 2 * W), addend=addend)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        gx = resize_bilinear_bwd(g, ctx.shape) if ctx.needs_input_grad[0] else None
+        return gx, (g if ctx.has_add and ctx.needs_input_grad[1] else None)
+
+
+def upsample2x(x, addend=None):
+    return Upsample2xFn.apply(x, addend)
+
+
+class UpsampleCatFn(Function):
+    """torch.cat([upsample2x(x), y], dim=1) written straight into one buffer (AA/network.py:85-87)."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        x = _check(x, "upsample-cat x", 4)
+        y = _check(y, "upsample-cat y", 4)
+        N, C1, H, W = x.shape
+        C2 = y.shape[1]
+        if tuple(y.shape) != (N, C2, 2 * H, 2 * W):
+            raise VstError("upsample-cat: skip tensor shape mismatch")
+        out = _empty((N, C1 + C2, 2 * H, 2 * W), x)
+        resize_bilinear(x, (2 * H, 2 * W), out=out[:, :C1])
+        copy_into(y, out[:, C1:])
+        ctx.dims = (x.shape, C1)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        xs, C1 = ctx.dims
+        gx = resize_bilinear_bwd(g[:, :C1], xs) if ctx.needs_input_grad[0] else None
+        gy = None
+        if ctx.needs_input_grad[1]:
+            gs = g[:, C1:]
+            gy = copy_into(gs, _empty(gs.shape, g))
+        return gx, gy
+
+
+def upsample_cat(x, y):
+    return UpsampleCatFn.apply(x, y)
 
 
 def flow_warp_mask(flo01, flo10, threshold=2.0):
