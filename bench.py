@@ -36,7 +36,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="frame pairs per GPU")
+    ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn"),
+                    help="reconet: BASELINE configs 2/3 (the metric); adaattn: config 4's train_video step")
+    ap.add_argument("--batch", type=int, default=None, help="frame pairs per GPU (default 8 reconet, 4 adaattn)")
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3))
@@ -79,24 +81,47 @@ def cpu_baseline(args):
                       f"config {args.config}, oracle/reconet_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+def cpu_baseline_adaattn(args):
+    """Oracle AdaAttN train_video step (oracle/adaattn_ref.py) on B=1 triple at full size."""
+    import oracle
+    from oracle import adaattn_ref as A
+    from oracle import shapes
+    from vst.synthetic import content_style_batch
 
-    from vst import kprof, ops
+    torch.set_num_threads(args.cpu_threads)
+    H, W = args.height, args.width
+    P = oracle.seeded_params(shapes.stylizing_network(), 1, requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg19(), 2)
+    c1, c2, s = content_style_batch(99, 1, H, W)
+    from oracle import reconet_ref as R
+
+    state = {}
+
+    def one():
+        L = A.adaattn_losses(P, VP, c1, c2, s)
+        for p in P.values():
+            p.grad = None
+        L["loss"].backward()
+        with torch.no_grad():
+            R.adam_step(P, {k: p.grad for k, p in P.items()}, state, lr=1e-4)
+
+    steps = max(1, args.cpu_steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": 1.0 / dt, "unit": "frame-pairs/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{steps} timed step(s) (no warm-up) of B=1 synthetic 3x{H}x{W} (content1, content2, style) "
+                      f"triple, oracle/adaattn_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
+
+
+def build_reconet(args, dev, rank):
+    from vst import ops
     from vst.reconet import network as N
     from vst.reconet.dist import shard_seed
     from vst.reconet.train import ReCoNetTrainer
     from vst.synthetic import frame_pair_batch, style_image
 
-    torch.manual_seed(0)  # identical random-init replicas on every rank
     model = N.ReCoNet().to(dev)
     vgg = N.Vgg16().to(dev)
     B, H, W = args.batch, args.height, args.width
@@ -109,9 +134,46 @@ def main():
     img1, img2, flow, mask = frame_pair_batch(shard_seed(1234, rank), B, H, W, mask_fn=hip_mask, device=dev)
     frames = torch.stack([img1, img2]).contiguous()
     del img1, img2
+    return lambda: trainer.step(frames, flow, mask)
+
+
+def build_adaattn(args, dev, rank):
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+    from vst.reconet.dist import shard_seed
+    from vst.synthetic import content_style_batch
+
+    model = StylizingNetwork("cosine").to(dev)
+    vgg = VGG19().to(dev)
+    trainer = AdaAttNTrainer(model, vgg, activation="cosine")
+    c1, c2, s = content_style_batch(shard_seed(1234, rank), args.batch, args.height, args.width, device=dev)
+    triple = torch.stack([c1, c2, s]).contiguous()
+    del c1, c2, s
+    return lambda: trainer.step(triple)
+
+
+def main():
+    args = parse()
+    if args.batch is None:
+        args.batch = 8 if args.model == "reconet" else 4
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from vst import kprof
+
+    torch.manual_seed(0)  # identical random-init replicas on every rank
+    B, H, W = args.batch, args.height, args.width
+    step = (build_reconet if args.model == "reconet" else build_adaattn)(args, dev, rank)
 
     for _ in range(args.warmup):
-        out = trainer.step(frames, flow, mask)
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -120,7 +182,7 @@ def main():
     t0 = time.perf_counter()
     with timer:
         for _ in range(args.steps):
-            out = trainer.step(frames, flow, mask)
+            out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -136,8 +198,18 @@ def main():
     if rank == 0:
         value = B * world * args.steps / elapsed
         achieved = ks["tflops"]
+        if args.model == "reconet":
+            metric = "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs"
+            workload = (f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), B={B} frame pairs/GPU, "
+                        f"3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}")
+            data = "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights"
+        else:
+            metric = "training frame-pairs/sec at 256\u00d7512, AdaAttN train_video step (VGG19 encoder/loss)"
+            workload = (f"config4 shape: AdaAttN train_video step (cosine attention, gs+lf+is losses), "
+                        f"B={B} (content1, content2, style) triples/GPU, 3x{H}x{W}")
+            data = "synthetic (numpy PCG64 images U[0,255)); random-init weights"
         result = {
-            "metric": "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs",
+            "metric": metric,
             "value": value,
             "unit": "frame-pairs/s",
             "n_gpus": world,
@@ -148,9 +220,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights",
-            "config": {"workload": f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), "
-                                   f"B={B} frame pairs/GPU, 3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}",
+            "data": data,
+            "config": {"workload": workload,
                        "global_batch": B * world, "height": H, "width": W, "parallelism": f"dp{world}"},
             "frames_per_s": 2 * value,
             "loss_last_step": loss,
@@ -162,7 +233,7 @@ def main():
                          "share_of_step": ks["total_ms"] / (1e3 * elapsed)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args)
+            result["cpu_baseline"] = (cpu_baseline if args.model == "reconet" else cpu_baseline_adaattn)(args)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

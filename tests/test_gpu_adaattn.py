@@ -77,7 +77,8 @@ def test_attention_fwd_bwd(activation, dims):
     Qg, Kg, Vg = (G(t).requires_grad_(True) for t in (Q, K, V))
     out = adaattn(Qg, Kg, Vg, G(cn), activation)
     out.backward(G(dout))
-    assert rel_err(C(out), ref.detach()) < 1e-4
+    # softmax of raw dot products (std ~ sqrt(d)) turns S's fp32 rounding into relative output error
+    assert rel_err(C(out), ref.detach()) < (1e-4 if activation == "cosine" else 5e-4)
     for a, b, nm in ((Qg, Qr, "dQ"), (Kg, Kr, "dK"), (Vg, Vr, "dV")):
         assert rel_err(C(a.grad), b.grad) < 1e-3, nm
 

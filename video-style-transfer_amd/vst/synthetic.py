@@ -38,3 +38,11 @@ def frame_pair_batch(seed, B, H, W, mask_fn=None, device="cpu"):
 def style_image(seed, H, W, device="cpu"):
     rng = np.random.default_rng(seed)
     return torch.from_numpy(rng.uniform(0.0, 255.0, (1, 3, H, W)).astype(np.float32)).to(device)
+
+
+def content_style_batch(seed, B, H, W, device="cpu"):
+    """(content1, content2, style) images in [0, 255) as `VidevoWikiArt` yields them
+    (AA/datasets.py), B per tensor."""
+    rng = np.random.default_rng(seed)
+    out = [torch.from_numpy(rng.uniform(0.0, 255.0, (B, 3, H, W)).astype(np.float32)).to(device) for _ in range(3)]
+    return tuple(out)
