@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-vgg19", action="store_true", help="skip the VGG19 fwd+dgrad north-star sub-benchmark")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=2)
     return ap.parse_args()
@@ -113,6 +114,46 @@ def cpu_baseline_adaattn(args):
     return {"value": 1.0 / dt, "unit": "frame-pairs/s", "cores": args.cpu_threads, "kind": "port",
             "sample": f"{steps} timed step(s) (no warm-up) of B=1 synthetic 3x{H}x{W} (content1, content2, style) "
                       f"triple, oracle/adaattn_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
+
+
+def vgg19_subbench(dev, reps=3, B=8, H=256, W=512):
+    """SURVEY.md §8(d) north-star sub-metric: VGG19 features[0:21] (to relu4_1) forward + input
+    gradient on B=8x3x256x512, random-init frozen weights.  Returns conv-kernel TFLOP/s (HIP events
+    around every conv_gemm launch) and the wall-clock rate of the whole fwd+dgrad pass."""
+    from vst import kprof
+    from vst.adaattn.vgg19 import VGG19
+    from vst.reconet.network import run_vgg_slice
+
+    vgg = VGG19().to(dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(B, 3, H, W, device=dev, generator=g).requires_grad_(True)
+    cfg = [(3, 64, H, W), (64, 64, H, W), (64, 128, H // 2, W // 2), (128, 128, H // 2, W // 2),
+           (128, 256, H // 4, W // 4), (256, 256, H // 4, W // 4), (256, 256, H // 4, W // 4),
+           (256, 256, H // 4, W // 4), (256, 512, H // 8, W // 8)]
+    fwd_flops = sum(2.0 * B * co * h * w * ci * 9 for ci, co, h, w in cfg)
+
+    def one():
+        f = x
+        for s in range(1, 5):
+            f = run_vgg_slice(getattr(vgg, f"slice{s}"), f)
+        f.backward(torch.ones_like(f))
+        x.grad = None
+
+    one()
+    torch.cuda.synchronize()
+    timer = kprof.KernelTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(reps):
+            one()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ks = timer.summary()
+    return {"workload": f"VGG19 features[0:21] (relu4_1) fwd + input grad, B={B}x3x{H}x{W}",
+            "algo_gflop": 2 * fwd_flops / 1e9, "conv_tflops": ks["tflops"],
+            "conv_frac": ks["tflops"] / FP32_MFMA_PEAK_TFLOPS, "wall_tflops": 2 * fwd_flops / wall / 1e12,
+            "wall_frac": 2 * fwd_flops / wall / 1e12 / FP32_MFMA_PEAK_TFLOPS, "ms": wall * 1e3,
+            "target_frac": 0.60}
 
 
 def build_reconet(args, dev, rank):
@@ -232,6 +273,8 @@ def main():
                          "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
                          "share_of_step": ks["total_ms"] / (1e3 * elapsed)},
         }
+        if world == 1 and not args.no_vgg19:
+            result["north_star_vgg19"] = vgg19_subbench(dev)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = (cpu_baseline if args.model == "reconet" else cpu_baseline_adaattn)(args)
         print(json.dumps(result), flush=True)

@@ -113,7 +113,7 @@ int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int 
  * optional per-channel scale (chscale[C], device) and binarize (> 0) epilogues */
 int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
                         const float* chscale, int binarize, long out_bs, const float* addend, void* stream);
-/* adjoint (float-atomic scatter into gx, zero it first); gout images gout_bs floats apart (0: dense)
+/* adjoint, as a deterministic gather (gx fully written); gout images gout_bs floats apart (0: dense)
  * (AA/network.py:59,80,85,90,94 decoder upsampling backward) */
 int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
                             void* stream);
@@ -179,7 +179,7 @@ int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, 
 int vst_plane_norm(const float* x, float* out, long NC, int HW, void* stream);
 int vst_plane_norm_grad(float* x, const float* s, const float* nrm, const float* y, long NC, int HW, void* stream);
 /* image_similarity_loss (AA/lossfn.py:25-53) on precomputed C x C products and norms;
- * partial[n] = sum |Dn_c - Dn_cs| / hw; backward w.r.t. the stylised side (dun zeroed first) */
+ * partial[n][i] = sum_j |Dn_c - Dn_cs|_ij / hw (N*C floats); backward w.r.t. the stylised side (dun zeroed first) */
 int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
                 const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream);
 int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,

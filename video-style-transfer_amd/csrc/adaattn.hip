@@ -38,17 +38,30 @@ __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restric
 }
 
 // out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
+// block = 64 consecutive pixels x 4 channel quarters; coalesced 256-B row reads, LDS combine
 __global__ void channel_norm_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int C, int P) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)N * P) return;
-  int n = (int)(idx / P), p = (int)(idx % P);
-  const float* xp = x + (long)n * C * P + p;
-  float s = 0.f;
-  for (int c = 0; c < C; ++c) {
-    float v = xp[(long)c * P];
-    s += v * v;
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int tiles = (P + 63) / 64;
+  const int n = blockIdx.x / tiles;
+  const int p = (blockIdx.x % tiles) * 64 + lane;
+  float s0 = 0.f, s1 = 0.f;
+  if (p < P) {
+    const float* xp = x + (long)n * C * P + p;
+    int c = grp;
+    for (; c + 4 < C; c += 8) {
+      const float a = xp[(long)c * P], b = xp[(long)(c + 4) * P];
+      s0 += a * a;
+      s1 += b * b;
+    }
+    for (; c < C; c += 4) {
+      const float a = xp[(long)c * P];
+      s0 += a * a;
+    }
   }
-  out[idx] = sqrtf(s);
+  part[grp][lane] = s0 + s1;
+  __syncthreads();
+  if (grp == 0 && p < P) out[(long)n * P + p] = sqrtf(part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
 }
 
 // cosine attention rows (AA/network.py:121-124): s = S/(qn_i kn_j) + 1, A = s / sum_j s
@@ -222,36 +235,44 @@ __global__ void plane_norm_kernel(const float* __restrict__ x, float* __restrict
   if (threadIdx.x == 0) out[plane] = (float)sqrt(t);
 }
 
-// image_similarity_loss core (AA/lossfn.py:25-53) for one image n, both cosine distances:
+// image_similarity_loss core (AA/lossfn.py:25-53), both cosine distances:
 //   D = 1 - G / (un_i vn_j + 1e-6);  Dn = D / colsum_j(D);  loss_n = sum |Dn_c - Dn_cs| / hw
-// one block per image; grid-stride over C x C; writes Dn_cs and colsums for backward.
-__global__ void simloss_kernel(const float* __restrict__ Gc, const float* __restrict__ unc, const float* __restrict__ vnc,
-                               const float* __restrict__ Gs, const float* __restrict__ uns, const float* __restrict__ vns,
-                               float* __restrict__ colc, float* __restrict__ cols, float* __restrict__ partial, int C,
-                               float inv_hw) {
-  __shared__ double sh[RT / 64];
-  const int n = blockIdx.x;
+// pass 1: column sums (grid ceil(C/RT) x N, coalesced over j)
+__global__ void simloss_colsum_kernel(const float* __restrict__ Gc, const float* __restrict__ unc,
+                                      const float* __restrict__ vnc, const float* __restrict__ Gs,
+                                      const float* __restrict__ uns, const float* __restrict__ vns,
+                                      float* __restrict__ colc, float* __restrict__ cols, int C) {
+  const int n = blockIdx.y, j = blockIdx.x * RT + threadIdx.x;
+  if (j >= C) return;
   const long o = (long)n * C * C;
-  // column sums (over rows i) of both distance matrices
-  for (int j = threadIdx.x; j < C; j += RT) {
-    double a = 0.0, b = 0.0;
-    for (int i = 0; i < C; ++i) {
-      a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f);
-      b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vns[n * C + j] + 1e-6f);
-    }
-    colc[n * C + j] = (float)a;
-    cols[n * C + j] = (float)b;
+  const float vc = vnc[n * C + j], vs = vns[n * C + j];
+  double a = 0.0, b = 0.0;
+  for (int i = 0; i < C; ++i) {
+    a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vc + 1e-6f);
+    b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vs + 1e-6f);
   }
-  __syncthreads();
+  colc[n * C + j] = (float)a;
+  cols[n * C + j] = (float)b;
+}
+
+// pass 2: one block per row (i, n): rowpart[n][i] = sum_j |Dn_c - Dn_cs| / hw
+__global__ void simloss_rows_kernel(const float* __restrict__ Gc, const float* __restrict__ unc,
+                                    const float* __restrict__ vnc, const float* __restrict__ Gs,
+                                    const float* __restrict__ uns, const float* __restrict__ vns,
+                                    const float* __restrict__ colc, const float* __restrict__ cols,
+                                    float* __restrict__ rowpart, int C, float inv_hw) {
+  __shared__ double sh[RT / 64];
+  const int i = blockIdx.x, n = blockIdx.y;
+  const long o = (long)n * C * C + (long)i * C;
+  const float uc = unc[n * C + i], us = uns[n * C + i];
   double acc = 0.0;
-  for (long t = threadIdx.x; t < (long)C * C; t += RT) {
-    const int i = (int)(t / C), j = (int)(t % C);
-    const float dc = (1.0f - Gc[o + t] / (unc[n * C + i] * vnc[n * C + j] + 1e-6f)) / colc[n * C + j];
-    const float ds = (1.0f - Gs[o + t] / (uns[n * C + i] * vns[n * C + j] + 1e-6f)) / cols[n * C + j];
+  for (int j = threadIdx.x; j < C; j += RT) {
+    const float dc = (1.0f - Gc[o + j] / (uc * vnc[n * C + j] + 1e-6f)) / colc[n * C + j];
+    const float ds = (1.0f - Gs[o + j] / (us * vns[n * C + j] + 1e-6f)) / cols[n * C + j];
     acc += fabsf(dc - ds);
   }
   const double tot = block_sum_d(acc, sh);
-  if (threadIdx.x == 0) partial[n] = (float)tot * inv_hw;
+  if (threadIdx.x == 0) rowpart[(long)n * C + i] = (float)tot * inv_hw;
 }
 
 // backward w.r.t. the stylised side: dG (C x C) plus dun (rows) and dvn (cols), scaled by gscale
@@ -318,7 +339,7 @@ int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int tran
 
 int vst_channel_norm(const float* x, float* out, int N, int C, int P, void* stream) {
   VST_CHECK_ARG(x && out && N > 0 && C > 0 && P > 0);
-  channel_norm_kernel<<<ceil_div((long)N * P, 256), 256, 0, (hipStream_t)stream>>>(x, out, N, C, P);
+  channel_norm_kernel<<<N * ceil_div(P, 64), 256, 0, (hipStream_t)stream>>>(x, out, N, C, P);
   return vst_launch_status();
 }
 
@@ -399,11 +420,13 @@ int vst_plane_norm_grad(float* x, const float* s, const float* nrm, const float*
   return vst_launch_status();
 }
 
-// partial: N floats (per-image loss, already / hw); colc, cols: N*C
+// partial: N*C floats (per-row loss, already / hw); colc, cols: N*C
 int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
                 const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream) {
   VST_CHECK_ARG(Gc && unc && vnc && Gs && uns && vns && colc && cols && partial && N > 0 && C > 0 && HW > 0);
-  simloss_kernel<<<N, RT, 0, (hipStream_t)stream>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, partial, C, 1.0f / HW);
+  hipStream_t st = (hipStream_t)stream;
+  simloss_colsum_kernel<<<dim3(ceil_div(C, RT), N), RT, 0, st>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, C);
+  simloss_rows_kernel<<<dim3(C, N), RT, 0, st>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, partial, C, 1.0f / HW);
   return vst_launch_status();
 }
 

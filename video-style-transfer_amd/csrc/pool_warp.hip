@@ -190,25 +190,49 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
   out[o] = v;
 }
 
-// adjoint of the bilinear resize: scatter each output gradient to its 4 sources (float atomics)
+// weight with which input index i enters output index d along one axis (0 if it does not)
+__device__ __forceinline__ float resize_weight(int d, int i, int n_in, int n_out) {
+  int i0, i1;
+  float l1;
+  resize_axis(d, n_in, n_out, i0, i1, l1);
+  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+// output index range [lo, hi] that can read input index i (src(d) in [i-1, i+1], with slack)
+__device__ __forceinline__ void resize_span(int i, int n_in, int n_out, int& lo, int& hi) {
+  const float inv = (float)n_out / (float)n_in;
+  lo = (int)floorf(((float)i - 0.5f) * inv - 0.5f) - 1;
+  hi = (int)ceilf(((float)i + 1.5f) * inv - 0.5f) + 1;
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > n_out - 1 ? n_out - 1 : hi;
+}
+
+// adjoint of the bilinear resize as a gather: each input element sums the output gradients that
+// read it, with the forward's own weights (deterministic, no atomics, every gx written once)
 __global__ void resize_bwd_kernel(const float* __restrict__ gout, float* __restrict__ gx, long NC, int C, int H, int W,
                                   int Ho, int Wo, long gout_bs) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= NC * Ho * Wo) return;
-  int ox = (int)(idx % Wo);
-  long t = idx / Wo;
-  int oy = (int)(t % Ho);
-  long nc = t / Ho;
-  int y0, y1, x0, x1;
-  float ly, lx;
-  resize_axis(oy, H, Ho, y0, y1, ly);
-  resize_axis(ox, W, Wo, x0, x1, lx);
-  const float g = gout[(nc / C) * gout_bs + (nc % C) * (long)Ho * Wo + (long)oy * Wo + ox];
-  float* p = gx + nc * H * W;
-  atomicAdd(p + (long)y0 * W + x0, g * (1.f - ly) * (1.f - lx));
-  atomicAdd(p + (long)y0 * W + x1, g * (1.f - ly) * lx);
-  atomicAdd(p + (long)y1 * W + x0, g * ly * (1.f - lx));
-  atomicAdd(p + (long)y1 * W + x1, g * ly * lx);
+  if (idx >= NC * H * W) return;
+  int ix = (int)(idx % W);
+  long t = idx / W;
+  int iy = (int)(t % H);
+  long nc = t / H;
+  int ylo, yhi, xlo, xhi;
+  resize_span(iy, H, Ho, ylo, yhi);
+  resize_span(ix, W, Wo, xlo, xhi);
+  const float* g = gout + (nc / C) * gout_bs + (nc % C) * (long)Ho * Wo;
+  float acc = 0.f;
+  for (int oy = ylo; oy <= yhi; ++oy) {
+    const float wy = resize_weight(oy, iy, H, Ho);
+    if (wy == 0.f) continue;
+    float row = 0.f;
+    for (int ox = xlo; ox <= xhi; ++ox) {
+      const float wx = resize_weight(ox, ix, W, Wo);
+      if (wx != 0.f) row += wx * g[(long)oy * Wo + ox];
+    }
+    acc += wy * row;
+  }
+  gx[idx] = acc;
 }
 
 }  // namespace
@@ -265,7 +289,7 @@ int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W
 int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
                             void* stream) {
   VST_CHECK_ARG(gout && gx && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
-  long total = NC * Ho * Wo;
+  long total = NC * H * W;
   if (gout_bs <= 0) gout_bs = (long)C * Ho * Wo;
   resize_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, gx, NC, C, H, W, Ho, Wo, gout_bs);
   return vst_launch_status();

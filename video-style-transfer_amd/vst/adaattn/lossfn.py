@@ -101,12 +101,12 @@ class ImageSimilarityFn(Function):
         Gc, Gs = gemm_abt(c1, c2), gemm_abt(s1, s2)
         unc, vnc, uns, vns = plane_norm(c1), plane_norm(c2), plane_norm(s1), plane_norm(s2)
         colc, cols = _empty((N, C), c1), _empty((N, C), c1)
-        partial = _empty((N,), c1)
+        partial = _empty((N * C,), c1)
         lib.vst_simloss(ptr(Gc), ptr(unc), ptr(vnc), ptr(Gs), ptr(uns), ptr(vns), ptr(colc), ptr(cols), ptr(partial),
                         N, C, P, stream())
         st = _empty((3,), c1)
         ws = _empty((ops.LOSS_WS,), c1)
-        lib.vst_sum_scaled(ptr(partial), N, float(weight), ptr(ws), ptr(st), stream())
+        lib.vst_sum_scaled(ptr(partial), N * C, float(weight), ptr(ws), ptr(st), stream())
         ctx.weight = float(weight)
         ctx.save_for_backward(Gc, unc, vnc, Gs, uns, vns, colc, cols, s1, s2)
         ctx.shape = fcs1.shape

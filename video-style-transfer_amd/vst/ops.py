@@ -550,7 +550,7 @@ def resize_bilinear_bwd(gout, x_shape):
     N, C, H, W = x_shape
     Ho, Wo = gout.shape[2:]
     gptr, gbs = ptr_rows(gout)
-    gx = _zeros(x_shape, gout)
+    gx = _empty(x_shape, gout)
     lib.vst_resize_bilinear_bwd(gptr, ptr(gx), N * C, C, H, W, Ho, Wo, gbs if gbs != C * Ho * Wo else 0, stream())
     return gx
 
