@@ -116,6 +116,22 @@ def cpu_baseline_adaattn(args):
                       f"triple, oracle/adaattn_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
 
 
+def pmc_traffic(model, family="conv_gemm_kernel"):
+    """HBM bytes per launch of the roofline kernel from the committed PMC summary of the same
+    workload (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/pmc_traffic.py; counters cannot
+    be read from inside the timed run).  None if no summary is committed."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_traffic_{model}.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    fam = d["families"].get(family)
+    if fam is None:
+        return None, None
+    return fam["bytes_per_launch"], os.path.relpath(files[-1], REPO) + " (" + d["method"] + ")"
+
+
 def vgg19_subbench(dev, reps=3, B=8, H=256, W=512):
     """SURVEY.md §8(d) north-star sub-metric: VGG19 features[0:21] (to relu4_1) forward + input
     gradient on B=8x3x256x512, random-init frozen weights.  Returns conv-kernel TFLOP/s (HIP events
@@ -239,6 +255,7 @@ def main():
     if rank == 0:
         value = B * world * args.steps / elapsed
         achieved = ks["tflops"]
+        traffic, traffic_src = pmc_traffic(args.model)
         if args.model == "reconet":
             metric = "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs"
             workload = (f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), B={B} frame pairs/GPU, "
@@ -268,7 +285,9 @@ def main():
             "loss_last_step": loss,
             "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (conv fwd + dgrad implicit GEMM, all tile variants)",
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algo_bytes_per_launch": ks["bytes"] / max(ks["launches"], 1),
                          "launches": ks["launches"], "avg_launch_us": ks["avg_us"],
                          "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
                          "share_of_step": ks["total_ms"] / (1e3 * elapsed)},

@@ -1,0 +1,51 @@
+"""HBM traffic per kernel launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+gfx950 correction (MI355X_MICROARCH.md "HBM"; re-measured here with tools/calib/hbm_calib.hip
+on a 1 GiB stream: FETCH_SIZE = 0.500 GiB for dword, dwordx4 and buffer_load_dword reads,
+WRITE_SIZE = 1.000 GiB for dword and dwordx4 stores):  bytes = 2 * FETCH_SIZE_KB * 1024 + WRITE_SIZE_KB * 1024.
+FETCH counts L2 misses to the fabric, so Infinity-Cache (MALL) hits are included: an upper bound on
+true HBM bytes.
+
+usage: python tools/pmc_traffic.py <model> [out.json]     (reads gpurun_out/pmc_<model>_{FETCH,WRITE}_SIZE)
+"""
+import collections
+import csv
+import json
+import sys
+
+FETCH_CORRECTION = 2.0
+
+
+def load(model, counter):
+    path = f"gpurun_out/pmc_{model}_{counter}/run_counter_collection.csv"
+    return {r["Dispatch_Id"]: r for r in csv.DictReader(open(path))}
+
+
+def family(name):
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").split("<")[0]
+
+
+def main():
+    model = sys.argv[1] if len(sys.argv) > 1 else "reconet"
+    F, W = load(model, "FETCH_SIZE"), load(model, "WRITE_SIZE")
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+    for d, r in F.items():
+        a = agg[family(r["Kernel_Name"])]
+        a[0] += 1
+        a[1] += float(r["Counter_Value"]) * 1024 * FETCH_CORRECTION
+        a[2] += float(W[d]["Counter_Value"]) * 1024 if d in W else 0.0
+    fams = {k: {"launches": n, "read_bytes_per_launch": f / n, "write_bytes_per_launch": w / n,
+                "bytes_per_launch": (f + w) / n} for k, (n, f, w) in agg.items()}
+    for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["bytes_per_launch"] * kv[1]["launches"])[:15]:
+        print(f"{k[:36]:36s} n={v['launches']:4d} read={v['read_bytes_per_launch']/1e6:9.1f} MB "
+              f"write={v['write_bytes_per_launch']/1e6:8.1f} MB per launch")
+    if len(sys.argv) > 2:
+        out = {"model": model, "fetch_correction": FETCH_CORRECTION,
+               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (with --kernel-trace), "
+                         "bench.py --steps 1 --warmup 1; bytes = 2*FETCH + WRITE (calibrated, tools/calib)",
+               "families": fams}
+        json.dump(out, open(sys.argv[2], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

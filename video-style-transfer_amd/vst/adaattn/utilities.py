@@ -3,6 +3,7 @@ import torch
 
 from .. import ops
 from .._lib import VstError
+from ..reconet.utilities import flow_warp_mask, warp  # noqa: F401  (AA/utilities.py:112-163, same arithmetic)
 
 
 def vgg_normalize(batch):

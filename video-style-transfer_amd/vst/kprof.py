@@ -3,7 +3,7 @@
 `conv_gemm` launches (forward + data-gradient implicit GEMM, `conv_gemm_kernel<...>`) record a
 start/stop event pair on the stream they are launched on, plus their algorithmic FLOPs
 (2 * N * Cout * Ho * Wo * Cin * k^2 of the reference convolution they implement, no padding or
-stride-2 zero-tap redundancy counted).
+stride-2 zero-tap redundancy counted) and algorithmic bytes (source + packed weights + output, once).
 """
 import torch
 
@@ -12,7 +12,7 @@ _active = None
 
 class KernelTimer:
     def __init__(self):
-        self.records = []  # (start, stop, flops, family)
+        self.records = []  # (start, stop, flops, family, algorithmic bytes)
 
     def __enter__(self):
         global _active
@@ -26,19 +26,21 @@ class KernelTimer:
     def summary(self, family="conv_gemm"):
         torch.cuda.synchronize()
         recs = [r for r in self.records if r[3] == family]
-        ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
-        flops = sum(f for _, _, f, _ in recs)
+        ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+        flops = sum(r[2] for r in recs)
+        nbytes = sum(r[4] for r in recs)
         n = len(recs)
-        return {"launches": n, "total_ms": ms, "avg_us": 1e3 * ms / max(n, 1), "flops": flops,
+        return {"launches": n, "total_ms": ms, "avg_us": 1e3 * ms / max(n, 1), "flops": flops, "bytes": nbytes,
                 "tflops": flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0}
 
 
-def begin(flops):
+def begin(flops, nbytes=0.0):
+    """nbytes: algorithmic HBM bytes of the launch (each operand read once, output written once)."""
     if _active is None:
         return None
     s = torch.cuda.Event(enable_timing=True)
     s.record()
-    return (s, flops)
+    return (s, flops, nbytes)
 
 
 def end(tok, family="conv_gemm"):
@@ -46,4 +48,4 @@ def end(tok, family="conv_gemm"):
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    _active.records.append((tok[0], e, tok[1], family))
+    _active.records.append((tok[0], e, tok[1], family, tok[2]))

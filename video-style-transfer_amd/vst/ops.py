@@ -85,7 +85,8 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     kh = ks if kh is None else kh
     if out is None:
         out = _empty((N, M, Ho, Wo), src)
-    tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh)
+    tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh,
+                      4.0 * (src.numel() + wpack.numel() + out.numel()))
     lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho, Wo,
                       kh, ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
     kprof.end(tok)
