@@ -352,39 +352,50 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
 }
 
 // adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hv+2p][Wv+2p] -> dx [NC][Hs][Ws]
-__device__ __forceinline__ int reflect_sources(int u, int n_v, int pad, int* src) {
-  int c = 0;
-  src[c++] = u + pad;
-  if (u >= 1 && u <= pad) src[c++] = pad - u;
-  if (u >= n_v - 1 - pad && u <= n_v - 2) src[c++] = 2 * (n_v - 1) - u + pad;
-  return c;
+// padded-grid sources of virtual coordinate u: the direct one and up to two reflections
+// (fixed register slots, -1 = none: no dynamically indexed arrays -> no scratch)
+struct Src3 {
+  int a, b, c;
+};
+__device__ __forceinline__ Src3 reflect_sources(int u, int n_v, int pad) {
+  Src3 s;
+  s.a = u + pad;
+  s.b = (u >= 1 && u <= pad) ? pad - u : -1;
+  s.c = (u >= n_v - 1 - pad && u <= n_v - 2) ? 2 * (n_v - 1) - u + pad : -1;
+  return s;
 }
 
-__global__ void fold_reflect_kernel(const float* __restrict__ dpad, float* __restrict__ dx, long NC, int Hs, int Ws,
+__device__ __forceinline__ float fold_row(const float* __restrict__ r, const Src3& cx) {
+  float v = r[cx.a];
+  if (cx.b >= 0) v += r[cx.b];
+  if (cx.c >= 0) v += r[cx.c];
+  return v;
+}
+
+// grid: x over the pixels of one plane, y over planes (grid-stride)
+__global__ void fold_reflect_kernel(const float* __restrict__ dpad, float* __restrict__ dx, int NC, int Hs, int Ws,
                                     int pad, int up, int accumulate) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = NC * Hs * Ws;
-  if (idx >= total) return;
-  int xs = (int)(idx % Ws);
-  long t = idx / Ws;
-  int ys = (int)(t % Hs);
-  long nc = t / Hs;
-  int Hv = Hs * up, Wv = Ws * up;
-  int Hp = Hv + 2 * pad, Wp = Wv + 2 * pad;
-  const float* d = dpad + nc * Hp * Wp;
-  float s = 0.f;
-  for (int dy = 0; dy < up; ++dy) {
-    int rows[3];
-    int nr = reflect_sources(ys * up + dy, Hv, pad, rows);
-    for (int dxx = 0; dxx < up; ++dxx) {
-      int cols[3];
-      int ncl = reflect_sources(xs * up + dxx, Wv, pad, cols);
-      for (int a = 0; a < nr; ++a)
-        for (int b = 0; b < ncl; ++b) s += d[(long)rows[a] * Wp + cols[b]];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= Hs * Ws) return;
+  const int xs = p % Ws, ys = p / Ws;
+  const int Hv = Hs * up, Wv = Ws * up;
+  const int Hp = Hv + 2 * pad, Wp = Wv + 2 * pad;
+  for (int nc = blockIdx.y; nc < NC; nc += gridDim.y) {
+    const float* d = dpad + (long)nc * Hp * Wp;
+    float s = 0.f;
+    for (int dy = 0; dy < up; ++dy) {
+      const Src3 ry = reflect_sources(ys * up + dy, Hv, pad);
+      for (int dxx = 0; dxx < up; ++dxx) {
+        const Src3 cx = reflect_sources(xs * up + dxx, Wv, pad);
+        s += fold_row(d + (long)ry.a * Wp, cx);
+        if (ry.b >= 0) s += fold_row(d + (long)ry.b * Wp, cx);
+        if (ry.c >= 0) s += fold_row(d + (long)ry.c * Wp, cx);
+      }
     }
+    float* o = dx + (long)nc * Hs * Ws + p;
+    if (accumulate) s += *o;
+    *o = s;
   }
-  if (accumulate) s += dx[idx];
-  dx[idx] = s;
 }
 
 // Stride-2 data gradient, parity class (py, px): only taps kh = py + 2i, kw = px + 2j reach
@@ -407,34 +418,45 @@ __global__ void pack_parity_kernel(const float* __restrict__ w, float* __restric
 }
 
 // fold_reflect over the 4 parity-class planes [class (a,b)][NC][Hc_a][Wc_b] of the padded grid
-__global__ void fold_reflect_parity_kernel(const float* __restrict__ cls, float* __restrict__ dx, long NC, int Hs,
+struct Cls4 {
+  const float *c00, *c01, *c10, *c11;
+  int w0, w1;
+};
+__device__ __forceinline__ float parity_at(const Cls4& c, int yp, int xp) {
+  const bool ya = yp & 1, xb = xp & 1;
+  const float* base = ya ? (xb ? c.c11 : c.c10) : (xb ? c.c01 : c.c00);
+  return base[(yp >> 1) * (xb ? c.w1 : c.w0) + (xp >> 1)];
+}
+
+// grid: x over the pixels of one plane, y over planes (grid-stride)
+__global__ void fold_reflect_parity_kernel(const float* __restrict__ cls, float* __restrict__ dx, int NC, int Hs,
                                            int Ws, int pad, int accumulate) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = NC * Hs * Ws;
-  if (idx >= total) return;
-  int xs = (int)(idx % Ws);
-  long t = idx / Ws;
-  int ys = (int)(t % Hs);
-  long nc = t / Hs;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= Hs * Ws) return;
+  const int xs = p % Ws, ys = p / Ws;
   const int Hp = Hs + 2 * pad, Wp = Ws + 2 * pad;
-  const int Hc[2] = {(Hp + 1) / 2, Hp / 2}, Wc[2] = {(Wp + 1) / 2, Wp / 2};
-  long coff[4];
-  coff[0] = 0;
-  coff[1] = coff[0] + NC * Hc[0] * Wc[0];
-  coff[2] = coff[1] + NC * Hc[0] * Wc[1];
-  coff[3] = coff[2] + NC * Hc[1] * Wc[0];
-  int rows[3], cols[3];
-  int nr = reflect_sources(ys, Hs, pad, rows);
-  int ncl = reflect_sources(xs, Ws, pad, cols);
-  float s = 0.f;
-  for (int a = 0; a < nr; ++a)
-    for (int b = 0; b < ncl; ++b) {
-      const int yp = rows[a], xp = cols[b];
-      const int ca = yp & 1, cb = xp & 1;
-      s += cls[coff[ca * 2 + cb] + (nc * Hc[ca] + (yp >> 1)) * Wc[cb] + (xp >> 1)];
-    }
-  if (accumulate) s += dx[idx];
-  dx[idx] = s;
+  const int Hc0 = (Hp + 1) / 2, Hc1 = Hp / 2;
+  const int Wc0 = (Wp + 1) / 2, Wc1 = Wp / 2;
+  const long s01 = (long)NC * Hc0 * Wc0, s10 = s01 + (long)NC * Hc0 * Wc1, s11 = s10 + (long)NC * Hc1 * Wc0;
+  const Src3 ry = reflect_sources(ys, Hs, pad), cx = reflect_sources(xs, Ws, pad);
+  for (int nc = blockIdx.y; nc < NC; nc += gridDim.y) {
+    const Cls4 c = {cls + (long)nc * Hc0 * Wc0, cls + s01 + (long)nc * Hc0 * Wc1, cls + s10 + (long)nc * Hc1 * Wc0,
+                    cls + s11 + (long)nc * Hc1 * Wc1, Wc0, Wc1};
+    float s = 0.f;
+#define VST_ROW(yp)                                         \
+  {                                                         \
+    s += parity_at(c, yp, cx.a);                        \
+    if (cx.b >= 0) s += parity_at(c, yp, cx.b);         \
+    if (cx.c >= 0) s += parity_at(c, yp, cx.c);         \
+  }
+    VST_ROW(ry.a);
+    if (ry.b >= 0) VST_ROW(ry.b);
+    if (ry.c >= 0) VST_ROW(ry.c);
+#undef VST_ROW
+    float* o = dx + (long)nc * Hs * Ws + p;
+    if (accumulate) s += *o;
+    *o = s;
+  }
 }
 
 }  // namespace
@@ -527,18 +549,16 @@ int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int
 int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws, int pad, int accumulate,
                             void* stream) {
   VST_CHECK_ARG(cls && dx && NC > 0 && Hs > 0 && Ws > 0 && pad >= 0 && pad < Hs && pad < Ws);
-  long total = NC * Hs * Ws;
-  fold_reflect_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(cls, dx, NC, Hs, Ws, pad,
-                                                                                    accumulate);
+  dim3 g(ceil_div((long)Hs * Ws, 256), (unsigned)(NC < 65535 ? NC : 65535));
+  fold_reflect_parity_kernel<<<g, 256, 0, (hipStream_t)stream>>>(cls, dx, (int)NC, Hs, Ws, pad, accumulate);
   return vst_launch_status();
 }
 
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
                      void* stream) {
   VST_CHECK_ARG(dpad && dx && NC > 0 && Hs > 0 && Ws > 0 && pad >= 0 && (up == 1 || up == 2));
-  long total = NC * Hs * Ws;
-  fold_reflect_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(dpad, dx, NC, Hs, Ws, pad, up,
-                                                                             accumulate);
+  dim3 g(ceil_div((long)Hs * Ws, 256), (unsigned)(NC < 65535 ? NC : 65535));
+  fold_reflect_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dpad, dx, (int)NC, Hs, Ws, pad, up, accumulate);
   return vst_launch_status();
 }
 

@@ -10,9 +10,9 @@ namespace {
 
 constexpr int NTN = 512;
 
-template <typename T>
+template <typename T, int NB = NTN>
 __device__ __forceinline__ T block_sum(T v, T* sh) {
-  // sh: NTN/64 entries
+  // sh: NB/64 entries
   v = (sizeof(T) == 8) ? (T)wave_sum_d((double)v) : (T)wave_sum((float)v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
@@ -20,7 +20,7 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
   __syncthreads();
   T s = 0;
 #pragma unroll
-  for (int i = 0; i < NTN / 64; ++i) s += sh[i];
+  for (int i = 0; i < NB / 64; ++i) s += sh[i];
   return s;
 }
 
@@ -105,13 +105,34 @@ __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ g
   const float* xp = x + plane * HW;
   const float* yp = y + plane * HW;
   const float mean = stats[2 * plane], rstd = stats[2 * plane + 1];
+  const bool v4 = (HW & 3) == 0;
+  auto load_g = [&](int i) -> float4 {  // masked gradient, 4 consecutive elements
+    float4 g = reinterpret_cast<const float4*>(gp)[i];
+    if (relu) {
+      const float4 yv = reinterpret_cast<const float4*>(yp)[i];
+      g.x = yv.x > 0.f ? g.x : 0.f;
+      g.y = yv.y > 0.f ? g.y : 0.f;
+      g.z = yv.z > 0.f ? g.z : 0.f;
+      g.w = yv.w > 0.f ? g.w : 0.f;
+    }
+    return g;
+  };
   double sg = 0.0, sgx = 0.0;
-  for (int i = threadIdx.x; i < HW; i += NTN) {
-    float g = gp[i];
-    if (relu && !(yp[i] > 0.f)) g = 0.f;
-    float xh = (xp[i] - mean) * rstd;
-    sg += g;
-    sgx += (double)g * xh;
+  if (v4) {
+    for (int i = threadIdx.x; i < HW / 4; i += NTN) {
+      const float4 g = load_g(i), xv = reinterpret_cast<const float4*>(xp)[i];
+      sg += (double)g.x + (double)g.y + (double)g.z + (double)g.w;
+      sgx += (double)g.x * ((xv.x - mean) * rstd) + (double)g.y * ((xv.y - mean) * rstd) +
+             (double)g.z * ((xv.z - mean) * rstd) + (double)g.w * ((xv.w - mean) * rstd);
+    }
+  } else {
+    for (int i = threadIdx.x; i < HW; i += NTN) {
+      float g = gp[i];
+      if (relu && !(yp[i] > 0.f)) g = 0.f;
+      float xh = (xp[i] - mean) * rstd;
+      sg += g;
+      sgx += (double)g * xh;
+    }
   }
   sg = block_sum(sg, sh[0]);
   sgx = block_sum(sgx, sh[1]);
@@ -119,15 +140,150 @@ __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ g
   const float k = rstd * w[c];
   float* gxp = gx + plane * HW;
   double sgo = 0.0;
-  for (int i = threadIdx.x; i < HW; i += NTN) {
-    float g = gp[i];
-    if (relu && !(yp[i] > 0.f)) g = 0.f;
-    float xh = (xp[i] - mean) * rstd;
-    float o = k * (g - mg - xh * mgx);
-    gxp[i] = o;
-    sgo += o;
+  if (v4) {
+    for (int i = threadIdx.x; i < HW / 4; i += NTN) {
+      const float4 g = load_g(i), xv = reinterpret_cast<const float4*>(xp)[i];
+      const float4 o = make_float4(k * (g.x - mg - (xv.x - mean) * rstd * mgx), k * (g.y - mg - (xv.y - mean) * rstd * mgx),
+                                   k * (g.z - mg - (xv.z - mean) * rstd * mgx), k * (g.w - mg - (xv.w - mean) * rstd * mgx));
+      reinterpret_cast<float4*>(gxp)[i] = o;
+      sgo += (double)o.x + (double)o.y + (double)o.z + (double)o.w;
+    }
+  } else {
+    for (int i = threadIdx.x; i < HW; i += NTN) {
+      float g = gp[i];
+      if (relu && !(yp[i] > 0.f)) g = 0.f;
+      float xh = (xp[i] - mean) * rstd;
+      float o = k * (g - mg - xh * mgx);
+      gxp[i] = o;
+      sgo += o;
+    }
   }
   sgo = block_sum(sgo, sh[2]);
+  if (threadIdx.x == 0) {
+    partial[3 * plane] = (float)sgx;
+    partial[3 * plane + 1] = (float)sg;
+    partial[3 * plane + 2] = (float)sgo;
+  }
+}
+
+// Register-resident variants for planes of HW <= NT*4*V4 (HW % 4 == 0): every element is read
+// from HBM once (the two-pass kernels above read the plane twice).  Backward only for <= 8192
+// (a 1024-thread, 32768-element backward spills).
+template <int NT, int V4>
+__global__ __launch_bounds__(NT) void in_fwd_reg_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, const float* __restrict__ res,
+                                                         float* __restrict__ y, float* __restrict__ stats, int C,
+                                                         int HW, float eps, int relu) {
+  __shared__ double sh[2][NT / 64];
+  const long plane = blockIdx.x;
+  const int c = (int)(plane % C);
+  const int n4 = HW >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x + plane * HW);
+  float4 v[V4];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int i = threadIdx.x + j * NT;
+    v[j] = i < n4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s1 += (double)v[j].x + (double)v[j].y + (double)v[j].z + (double)v[j].w;
+    s2 += (double)v[j].x * v[j].x + (double)v[j].y * v[j].y + (double)v[j].z * v[j].z + (double)v[j].w * v[j].w;
+  }
+  s1 = block_sum<double, NT>(s1, sh[0]);
+  s2 = block_sum<double, NT>(s2, sh[1]);
+  const double mean_d = s1 / HW;
+  double var_d = s2 / HW - mean_d * mean_d;
+  var_d = var_d < 0.0 ? 0.0 : var_d;
+  const float mean = (float)mean_d;
+  const float rstd = (float)(1.0 / sqrt(var_d + (double)eps));
+  if (threadIdx.x == 0) {
+    stats[2 * plane] = mean;
+    stats[2 * plane + 1] = rstd;
+  }
+  const float wc = w[c], bc = b[c];
+  float4* y4 = reinterpret_cast<float4*>(y + plane * HW);
+  const float4* r4 = res ? reinterpret_cast<const float4*>(res + plane * HW) : nullptr;
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int i = threadIdx.x + j * NT;
+    if (i >= n4) break;
+    float o0 = (v[j].x - mean) * rstd * wc + bc, o1 = (v[j].y - mean) * rstd * wc + bc;
+    float o2 = (v[j].z - mean) * rstd * wc + bc, o3 = (v[j].w - mean) * rstd * wc + bc;
+    if (relu) {
+      o0 = fmaxf(o0, 0.f);
+      o1 = fmaxf(o1, 0.f);
+      o2 = fmaxf(o2, 0.f);
+      o3 = fmaxf(o3, 0.f);
+    }
+    if (r4) {
+      const float4 r = r4[i];
+      o0 += r.x;
+      o1 += r.y;
+      o2 += r.z;
+      o3 += r.w;
+    }
+    y4[i] = make_float4(o0, o1, o2, o3);
+  }
+}
+
+template <int NT, int V4, bool KEEPX>
+__global__ __launch_bounds__(NT) void in_bwd_reg_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                                                         const float* __restrict__ y, const float* __restrict__ stats,
+                                                         const float* __restrict__ w, float* __restrict__ gx,
+                                                         float* __restrict__ partial, int C, int HW, int relu) {
+  __shared__ double sh[3][NT / 64];
+  const long plane = blockIdx.x;
+  const int c = (int)(plane % C);
+  const int n4 = HW >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(gy + plane * HW);
+  const float4* x4 = reinterpret_cast<const float4*>(x + plane * HW);
+  const float4* y4 = reinterpret_cast<const float4*>(y + plane * HW);
+  const float mean = stats[2 * plane], rstd = stats[2 * plane + 1];
+  float4 g[V4], xh[KEEPX ? V4 : 1];
+  double sg = 0.0, sgx = 0.0;
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int i = threadIdx.x + j * NT;
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), xv = gv;
+    if (i < n4) {
+      gv = g4[i];
+      xv = x4[i];
+      if (relu) {
+        const float4 yv = y4[i];
+        gv.x = yv.x > 0.f ? gv.x : 0.f;
+        gv.y = yv.y > 0.f ? gv.y : 0.f;
+        gv.z = yv.z > 0.f ? gv.z : 0.f;
+        gv.w = yv.w > 0.f ? gv.w : 0.f;
+      }
+      xv = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
+    }
+    g[j] = gv;
+    if (KEEPX) xh[KEEPX ? j : 0] = xv;
+    sg += (double)gv.x + (double)gv.y + (double)gv.z + (double)gv.w;
+    sgx += (double)gv.x * xv.x + (double)gv.y * xv.y + (double)gv.z * xv.z + (double)gv.w * xv.w;
+  }
+  sg = block_sum<double, NT>(sg, sh[0]);
+  sgx = block_sum<double, NT>(sgx, sh[1]);
+  const float mg = (float)(sg / HW), mgx = (float)(sgx / HW);
+  const float k = rstd * w[c];
+  float4* o4 = reinterpret_cast<float4*>(gx + plane * HW);
+  double sgo = 0.0;
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int i = threadIdx.x + j * NT;
+    if (i >= n4) break;
+    float4 h;
+    if (KEEPX) {
+      h = xh[KEEPX ? j : 0];
+    } else {
+      const float4 xv = x4[i];
+      h = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
+    }
+    const float4 o = make_float4(k * (g[j].x - mg - h.x * mgx), k * (g[j].y - mg - h.y * mgx),
+                                 k * (g[j].z - mg - h.z * mgx), k * (g[j].w - mg - h.w * mgx));
+    o4[i] = o;
+    sgo += (double)o.x + (double)o.y + (double)o.z + (double)o.w;
+  }
+  sgo = block_sum<double, NT>(sgo, sh[2]);
   if (threadIdx.x == 0) {
     partial[3 * plane] = (float)sgx;
     partial[3 * plane + 1] = (float)sg;
@@ -167,7 +323,13 @@ extern "C" {
 int vst_instnorm_fwd(const float* x, const float* w, const float* b, const float* res, float* y, float* stats, int N,
                      int C, int HW, float eps, int relu, void* stream) {
   VST_CHECK_ARG(x && w && b && y && stats && N > 0 && C > 0 && HW > 0);
-  in_fwd_kernel<<<N * C, NTN, 0, (hipStream_t)stream>>>(x, w, b, res, y, stats, C, HW, eps, relu);
+  hipStream_t st = (hipStream_t)stream;
+  if ((HW & 3) == 0 && HW <= NTN * 4 * 4)
+    in_fwd_reg_kernel<512, 4><<<N * C, 512, 0, st>>>(x, w, b, res, y, stats, C, HW, eps, relu);
+  else if ((HW & 3) == 0 && HW <= 1024 * 4 * 8)
+    in_fwd_reg_kernel<1024, 8><<<N * C, 1024, 0, st>>>(x, w, b, res, y, stats, C, HW, eps, relu);
+  else
+    in_fwd_kernel<<<N * C, NTN, 0, st>>>(x, w, b, res, y, stats, C, HW, eps, relu);
   return vst_launch_status();
 }
 
@@ -179,7 +341,10 @@ int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const floa
   VST_CHECK_ARG(gy && x && stats && w && gx && partial && N > 0 && C > 0 && HW > 0);
   VST_CHECK_ARG(!relu || y);
   hipStream_t st = (hipStream_t)stream;
-  in_bwd_kernel<<<N * C, NTN, 0, st>>>(gy, x, y, stats, w, gx, partial, C, HW, relu);
+  if ((HW & 3) == 0 && HW <= NTN * 4 * 4)
+    in_bwd_reg_kernel<512, 4, true><<<N * C, 512, 0, st>>>(gy, x, y, stats, w, gx, partial, C, HW, relu);
+  else
+    in_bwd_kernel<<<N * C, NTN, 0, st>>>(gy, x, y, stats, w, gx, partial, C, HW, relu);
   sum_over_n_kernel<<<ceil_div(C, 256), 256, 0, st>>>(partial, N, C, 3, gw, gb, gbias_prev, accumulate);
   return vst_launch_status();
 }

@@ -55,7 +55,7 @@ def gemm_abt(a, b, scale=1.0):
     ws = _empty((lib.vst_wgrad_workspace(N, M, J, R),), a)
     from .. import kprof
 
-    tok = kprof.begin(2.0 * N * M * J * R, 4.0 * (a.numel() + b.numel() + out.numel()))
+    tok = kprof.begin(2.0 * N * M * J * R, 4.0 * (a.numel() + b.numel() + out.numel()), ("abt", N, M, J, R))
     lib.vst_gemm_abt(ptr(a), ptr(b), ptr(out), ptr(ws), N, M, J, R, float(scale), stream())
     kprof.end(tok, family="gemm_abt")
     return out

@@ -11,8 +11,9 @@ _active = None
 
 
 class KernelTimer:
-    def __init__(self):
-        self.records = []  # (start, stop, flops, family, algorithmic bytes)
+    def __init__(self, detail=False):
+        self.detail = detail
+        self.records = []  # (start, stop, flops, family, algorithmic bytes, tag)
 
     def __enter__(self):
         global _active
@@ -34,13 +35,28 @@ class KernelTimer:
                 "tflops": flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0}
 
 
-def begin(flops, nbytes=0.0):
-    """nbytes: algorithmic HBM bytes of the launch (each operand read once, output written once)."""
+    def by_tag(self, family="conv_gemm"):
+        """{tag: [launches, ms, flops]} (detail mode)."""
+        torch.cuda.synchronize()
+        out = {}
+        for r in self.records:
+            if r[3] != family:
+                continue
+            a = out.setdefault(r[5], [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += r[0].elapsed_time(r[1])
+            a[2] += r[2]
+        return out
+
+
+def begin(flops, nbytes=0.0, tag=None):
+    """nbytes: algorithmic HBM bytes of the launch (each operand read once, output written once);
+    tag: launch shape, kept only when the timer was created with detail=True."""
     if _active is None:
         return None
     s = torch.cuda.Event(enable_timing=True)
     s.record()
-    return (s, flops, nbytes)
+    return (s, flops, nbytes, tag if _active.detail else None)
 
 
 def end(tok, family="conv_gemm"):
@@ -48,4 +64,4 @@ def end(tok, family="conv_gemm"):
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    _active.records.append((tok[0], e, tok[1], family, tok[2]))
+    _active.records.append((tok[0], e, tok[1], family, tok[2], tok[3]))

@@ -86,7 +86,8 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     if out is None:
         out = _empty((N, M, Ho, Wo), src)
     tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh,
-                      4.0 * (src.numel() + wpack.numel() + out.numel()))
+                      4.0 * (src.numel() + wpack.numel() + out.numel()),
+                      (N, Cs, Hs, Ws, M, Ho, Wo, kh, ks, gmode, stride, pad, up))
     lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho, Wo,
                       kh, ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
     kprof.end(tok)
@@ -146,8 +147,11 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
+    tok = kprof.begin(2.0 * N * Cout * Ho * Wo * Cin * ks * ks, 4.0 * (gz.numel() + x.numel() + dw.numel()),
+                      ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up))
     lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
                        GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), stream())
+    kprof.end(tok, family="wgrad")
     return dw
 
 
@@ -205,12 +209,16 @@ class Conv2dFn(Function):
     torchvision VGG Conv2d+ReLU pairs (RC/network.py:17-24, AA/vgg19.py:19-37)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act):
+    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act, bias_const=None):
+        """bias_const: a bias added in the epilogue whose gradient another Function produces
+        (conv -> InstanceNorm: the norm's backward already sums the conv-output gradient)."""
         x = _check(x, "conv input", 4)
         w = w.contiguous()
         N, Cin, H, W = x.shape
         Cout, _, ks, _ = w.shape
         Ho, Wo = conv_out_hw(H, W, ks, stride, pad, up)
+        if bias_const is not None:
+            b = bias_const
         epi = (EPI_BIAS if b is not None else 0) | (EPI_RELU if act == "relu" else 0) | (EPI_TANH if act == "tanh" else 0)
         aux = _empty((N, Cout, Ho, Wo), x) if act == "tanh" else None
         bias = b.contiguous() if b is not None else None
@@ -220,7 +228,7 @@ class Conv2dFn(Function):
             out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
                             stride, pad, up, epi=epi, bias=bias, aux=aux)
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
-        ctx.has_bias = b is not None
+        ctx.has_bias = b is not None and bias_const is None
         ctx.params = (w, b)  # leaves: weight gradients go straight into their .grad when possible
         ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
         return out
@@ -253,7 +261,7 @@ class Conv2dFn(Function):
             sink = grad_sink(ctx.params[1])
             db = channel_sum(gz, out=sink)
             db = None if sink is not None else db
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, pad_mode="zero", up=1, act=None):
@@ -264,7 +272,9 @@ class InstanceNormFn(Function):
     """InstanceNorm2d(C, affine=True) [-> ReLU] [+ residual] (RC/network.py:91-97, 126-132, 140-150)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res, relu, eps):
+    def forward(ctx, x, w, b, res, relu, eps, conv_bias=None):
+        """conv_bias: bias of the conv producing x (added in that conv's epilogue); its gradient,
+        sum of dx over (n, h, w), falls out of this backward's per-plane partials."""
         x = _check(x, "instance_norm input", 4)
         N, C, H, W = x.shape
         y = _empty(x.shape, x)
@@ -274,7 +284,7 @@ class InstanceNormFn(Function):
                              H * W, float(eps), int(relu), stream())
         ctx.relu = relu
         ctx.has_res = res is not None
-        ctx.params = (w, b)
+        ctx.params = (w, b, conv_bias)
         ctx.save_for_backward(x, y if relu else None, stats, w)
         return y
 
@@ -285,20 +295,34 @@ class InstanceNormFn(Function):
         N, C, H, W = x.shape
         gx = _empty(x.shape, x)
         sw, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
-        direct = sw is not None and sb is not None
+        need_c = ctx.params[2] is not None and ctx.needs_input_grad[6]
+        sc = grad_sink(ctx.params[2]) if need_c else None
+        direct = sw is not None and sb is not None and (not need_c or sc is not None)
         gw = sw if direct else _empty((C,), x)
         gb = sb if direct else _empty((C,), x)
+        gc = (sc if direct else _empty((C,), x)) if need_c else None
         part = _empty((N * C * 3,), x)
-        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(stats), ptr(w.contiguous()), ptr(gx), ptr(gw), ptr(gb), None,
-                             ptr(part), N, C, H * W, int(ctx.relu), int(direct), stream())
+        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(stats), ptr(w.contiguous()), ptr(gx), ptr(gw), ptr(gb),
+                             ptr(gc), ptr(part), N, C, H * W, int(ctx.relu), int(direct), stream())
         gres = gy if ctx.has_res else None
         if direct:
-            gw = gb = None
-        return gx, gw, gb, gres, None, None
+            gw = gb = gc = None
+        return gx, gw, gb, gres, None, None, gc
 
 
 def instance_norm(x, w, b, relu=False, res=None, eps=1e-5):
     return InstanceNormFn.apply(x, w, b, res, relu, eps)
+
+
+def conv_instance_norm(x, w, b, gamma, beta, stride=1, pad=0, pad_mode="reflect", up=1, relu=False, res=None,
+                       eps=1e-5):
+    """conv [+bias] -> InstanceNorm(affine) [-> ReLU] [+ res] (ConvInstRelu, UpsampleConvInstRelu,
+    ResidualBlock halves).  The conv bias gradient comes out of the norm's backward partials, so
+    no separate channel-sum pass re-reads the gradient."""
+    if b is None:
+        return instance_norm(conv2d(x, w, None, stride, pad, pad_mode, up), gamma, beta, relu, res, eps)
+    y = Conv2dFn.apply(x, w, None, stride, pad, pad_mode, up, None, b.detach())
+    return InstanceNormFn.apply(y, gamma, beta, res, relu, eps, b)
 
 
 class MaxPool2x2Fn(Function):

@@ -149,8 +149,9 @@ class ConvInstRelu(ConvLayer):
         self.relu = nn.ReLU()
 
     def forward(self, x):
-        y = self._conv(x)
-        return ops.instance_norm(y, self.instance.weight, self.instance.bias, relu=True, eps=self.instance.eps)
+        c = self.conv2d
+        return ops.conv_instance_norm(x, c.weight, c.bias, self.instance.weight, self.instance.bias, c.stride[0],
+                                      self.reflection_padding, "reflect", 1, relu=True, eps=self.instance.eps)
 
 
 class UpsampleConvLayer(nn.Module):
@@ -182,8 +183,10 @@ class UpsampleConvInstRelu(UpsampleConvLayer):
         self.relu = nn.ReLU()
 
     def forward(self, x):
-        y = self._conv(x)
-        return ops.instance_norm(y, self.instance.weight, self.instance.bias, relu=True, eps=self.instance.eps)
+        c = self.conv2d
+        return ops.conv_instance_norm(x, c.weight, c.bias, self.instance.weight, self.instance.bias, c.stride[0],
+                                      self.reflection_padding, "reflect", self.upsample or 1, relu=True,
+                                      eps=self.instance.eps)
 
 
 class ResidualBlock(nn.Module):
@@ -198,8 +201,12 @@ class ResidualBlock(nn.Module):
         self.relu = nn.ReLU()
 
     def forward(self, x):
-        out = ops.instance_norm(self.conv1(x), self.in1.weight, self.in1.bias, relu=True, eps=self.in1.eps)
-        return ops.instance_norm(self.conv2(out), self.in2.weight, self.in2.bias, relu=False, res=x, eps=self.in2.eps)
+        c1, c2 = self.conv1.conv2d, self.conv2.conv2d
+        p1, p2 = self.conv1.reflection_padding, self.conv2.reflection_padding
+        out = ops.conv_instance_norm(x, c1.weight, c1.bias, self.in1.weight, self.in1.bias, c1.stride[0], p1,
+                                     relu=True, eps=self.in1.eps)
+        return ops.conv_instance_norm(out, c2.weight, c2.bias, self.in2.weight, self.in2.bias, c2.stride[0], p2,
+                                      relu=False, res=x, eps=self.in2.eps)
 
 
 class ReCoNet(nn.Module):
