@@ -606,3 +606,183 @@ extern "C" int vst_rowsplit_reduce(const float* P, const float* bias, float* out
                                                                                 epi);
   return vst_launch_status();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Reflect-pad data gradient without the padded grid (RC/network.py:72-75 ConvLayer and
+// :114-120 UpsampleConvLayer backward).  dXpad = full correlation of dY with the flipped
+// weights over the padded (virtual, upsampled) grid; dX = fold of dXpad.  Split:
+//   * core: the directly-mapped part, one GEMM on the UNPADDED grid (rows aligned with the
+//     activations; for nearest x2 upsampling the 2x2 fold is folded into a stride-2 GEMM with
+//     (KS+1)^2 tap-summed weights, 2.25x fewer MACs than the upsampled-grid GEMM);
+//   * ring: the p-wide border of dXpad (reflected copies), computed here and folded into the
+//     2p-wide border band of dX.
+namespace {
+
+// Summed-tap packed weight for the up=2 core: W'[jh][jw] = sum W[kh][kw] over
+// kh in {KS-1-jh, KS-jh}, kw in {KS-1-jw, KS-jw} (valid ones); transposed A: m = ci, k = (jh*(KS+1)+jw)*Cout + co
+__global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
+                                  int Mpad, int Kpad) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)Mpad * Kpad) return;
+  const int m = (int)(idx % Mpad);
+  const int k = (int)(idx / Mpad);
+  const int KU = KS + 1;
+  float v = 0.f;
+  if (m < Cin && k < KU * KU * Cout) {
+    const int tap = k / Cout, co = k % Cout;
+    const int jh = tap / KU, jw = tap % KU;
+    const float* wp = w + ((long)co * Cin + m) * KS * KS;
+    for (int a = 0; a < 2; ++a) {
+      const int kh = KS - 1 - jh + a;
+      if (kh < 0 || kh >= KS) continue;
+      for (int b = 0; b < 2; ++b) {
+        const int kw = KS - 1 - jw + b;
+        if (kw < 0 || kw >= KS) continue;
+        v += wp[kh * KS + kw];
+      }
+    }
+  }
+  out[apack_index(k, m, Mpad)] = v;
+}
+
+// ring position r of a (Hv+2p) x (Wv+2p) padded plane -> (u, v); layout: p top rows, p bottom rows,
+// then the Hv core rows' p left and p right columns
+__device__ __forceinline__ void ring_pos(int r, int Hv, int Wv, int p, int& u, int& v) {
+  const int Wp = Wv + 2 * p;
+  if (r < 2 * p * Wp) {
+    const int row = r / Wp;
+    v = r - row * Wp;
+    u = row < p ? row : Hv + row;  // rows [0,p) and [Hv+p, Hv+2p)
+  } else {
+    r -= 2 * p * Wp;
+    const int side = r / (Hv * p);
+    r -= side * Hv * p;
+    u = p + r / p;
+    const int c = r % p;
+    v = side == 0 ? c : Wv + p + c;
+  }
+}
+
+__device__ __forceinline__ int ring_index(int u, int v, int Hv, int Wv, int p) {
+  const int Wp = Wv + 2 * p;
+  if (u < p) return u * Wp + v;
+  if (u >= Hv + p) return (u - Hv) * Wp + v;
+  if (v < p) return 2 * p * Wp + (u - p) * p + v;
+  if (v >= Wv + p) return 2 * p * Wp + Hv * p + (u - p) * p + (v - Wv - p);
+  return -1;
+}
+
+// ring[n][ci][r] = sum_{co,kh,kw} W[co][ci][kh][kw] dY[n][co][u-kh][v-kw]   (dY: Hv x Wv)
+// block: 64 ring positions x 4 output-channel groups, LDS combine
+__global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
+                                                         float* __restrict__ ring, int Cout, int Cin, int KS, int Hv,
+                                                         int Wv, int R) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int r = blockIdx.x * 64 + lane;
+  const int ci = blockIdx.y, n = blockIdx.z;
+  const int p = KS / 2;
+  float acc = 0.f;
+  if (r < R) {
+    int u, v;
+    ring_pos(r, Hv, Wv, p, u, v);
+    const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
+    const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
+    for (int co = grp; co < Cout; co += 4) {
+      const float* wp = w + ((long)co * Cin + ci) * KS * KS;
+      const float* dp = dy + ((long)n * Cout + co) * Hv * Wv;
+      for (int kh = kh0; kh <= kh1; ++kh)
+        for (int kw = kw0; kw <= kw1; ++kw) acc += wp[kh * KS + kw] * dp[(u - kh) * Wv + (v - kw)];
+    }
+  }
+  part[grp][lane] = acc;
+  __syncthreads();
+  if (grp == 0 && r < R)
+    ring[((long)n * Cin + ci) * R + r] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+}
+
+// dx (+)= ring contributions, for the border band of dX only (each element written by one thread)
+__global__ void fold_ring_kernel(const float* __restrict__ ring, float* __restrict__ dx, int NC, int Hs, int Ws,
+                                 int p, int up, int bt, int bb, int ct, int cb, int R) {
+  const int nb = (bt + bb) * Ws + (Hs - bt - bb) * (ct + cb);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb) return;
+  int y, x;
+  if (t < bt * Ws) {
+    y = t / Ws;
+    x = t % Ws;
+  } else if (t < (bt + bb) * Ws) {
+    y = Hs - bb + (t - bt * Ws) / Ws;
+    x = (t - bt * Ws) % Ws;
+  } else {
+    const int q = t - (bt + bb) * Ws;
+    y = bt + q / (ct + cb);
+    const int c = q % (ct + cb);
+    x = c < ct ? c : Ws - cb + (c - ct);
+  }
+  const int Hv = Hs * up, Wv = Ws * up;
+  for (int nc = blockIdx.y; nc < NC; nc += gridDim.y) {
+    const float* rp = ring + (long)nc * R;
+    float s = 0.f;
+    for (int dy = 0; dy < up; ++dy) {
+      const Src3 ry = reflect_sources(y * up + dy, Hv, p);
+      for (int dxx = 0; dxx < up; ++dxx) {
+        const Src3 cx = reflect_sources(x * up + dxx, Wv, p);
+        const int us[3] = {ry.a, ry.b, ry.c};
+        const int vs[3] = {cx.a, cx.b, cx.c};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            if (us[i] < 0 || vs[j] < 0) continue;
+            const int ri = ring_index(us[i], vs[j], Hv, Wv, p);
+            if (ri >= 0) s += rp[ri];
+          }
+      }
+    }
+    dx[((long)nc * Hs + y) * Ws + x] += s;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream) {
+  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= Cin && Kpad >= (KS + 1) * (KS + 1) * Cout);
+  long total = (long)Mpad * Kpad;
+  pack_upsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, Mpad, Kpad);
+  return vst_launch_status();
+}
+
+long vst_dgrad_ring_size(int Hv, int Wv, int KS) {
+  const int p = KS / 2;
+  return 2L * p * (Wv + 2 * p) + 2L * Hv * p;
+}
+
+int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
+                   void* stream) {
+  VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
+  VST_CHECK_ARG(Cin <= 65535 && N <= 65535);
+  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
+  dim3 g(ceil_div(R, 64), Cin, N);
+  dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, Cout, Cin, KS, Hv, Wv, R);
+  return vst_launch_status();
+}
+
+int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream) {
+  const int p = KS / 2;
+  VST_CHECK_ARG(ring && dx && NC > 0 && (up == 1 || up == 2) && (KS & 1) && KS > 1);
+  const int Hv = Hs * up, Wv = Ws * up;
+  // virtual rows with reflected sources: [1, p] and [Hv-1-p, Hv-2]
+  const int bt = p / up + 1, bb = Hs - (Hv - 1 - p) / up;
+  const int ct = p / up + 1, cb = Ws - (Wv - 1 - p) / up;
+  VST_CHECK_ARG(bt + bb <= Hs && ct + cb <= Ws && Hv > 2 * p + 1 && Wv > 2 * p + 1);
+  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
+  const int nb = (bt + bb) * Ws + (Hs - bt - bb) * (ct + cb);
+  dim3 g(ceil_div(nb, 256), (unsigned)(NC < 65535 ? NC : 65535));
+  fold_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(ring, dx, (int)NC, Hs, Ws, p, up, bt, bb, ct, cb, R);
+  return vst_launch_status();
+}
+
+}  // extern "C"

@@ -100,17 +100,41 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None):
     Cout = w.shape[0]
     Ho, Wo = gz.shape[2:]
     flops = 2.0 * N * Cout * Ho * Wo * Cin * ks * ks
-    wp = packed_weight(w, transposed=True)
     if pad_mode == "zero" and up == 1:
-        return conv_gemm(gz, wp, Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1, gmask=gmask, algo_flops=flops)
+        return conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1,
+                         gmask=gmask, algo_flops=flops)
     if pad_mode != "reflect":
         raise VstError("dgrad: zero padding with upsampling is not on the reference path")
     if stride == 2 and up == 1:
         return conv_dgrad_parity(gz, w, x_shape, ks, pad, gmask)
+    if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
+        return conv_dgrad_ring(gz, w, x_shape, ks, up, flops)
     Hp, Wp = H * up + 2 * pad, W * up + 2 * pad
-    dpad = conv_gemm(gz, wp, Cin, ks, Hp, Wp, GM_TRANSPOSED, stride, 0, 1, gmask=gmask, algo_flops=flops)
+    dpad = conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, Hp, Wp, GM_TRANSPOSED, stride, 0, 1, gmask=gmask,
+                     algo_flops=flops)
     dx = _empty(x_shape, gz)
     lib.vst_fold_reflect(ptr(dpad), ptr(dx), N * Cin, H, W, pad, up, 0, stream())
+    return dx
+
+
+def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
+    """Stride-1 reflect-pad (optionally nearest-x2-upsampled) conv input gradient on the unpadded
+    grid: core GEMM + the padded grid's border ring folded into dx's border band."""
+    N, Cin, H, W = x_shape
+    Cout = w.shape[0]
+    p = ks // 2
+    w = w.contiguous()
+    if up == 1:
+        dx = conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, 1, p, 1, algo_flops=flops)
+    else:
+        Mpad, Kpad = pack_dims(Cin, (ks + 1) * (ks + 1) * Cout)
+        wp = _empty((Kpad * Mpad,), w)
+        lib.vst_pack_weight_upsum(ptr(w), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
+        dx = conv_gemm(gz, wp, Cin, ks + 1, H, W, GM_ZERO, 2, ks - 1 - p, 1, algo_flops=flops)
+    Hv, Wv = H * up, W * up
+    ring = _empty((N * Cin * lib.vst_dgrad_ring_size(Hv, Wv, ks),), gz)
+    lib.vst_dgrad_ring(ptr(gz), ptr(w), ptr(ring), N, Cout, Cin, ks, Hv, Wv, stream())
+    lib.vst_fold_ring(ptr(ring), ptr(dx), N * Cin, H, W, ks, up, stream())
     return dx
 
 
