@@ -673,32 +673,28 @@ __device__ __forceinline__ int ring_index(int u, int v, int Hv, int Wv, int p) {
 }
 
 // ring[n][ci][r] = sum_{co,kh,kw} W[co][ci][kh][kw] dY[n][co][u-kh][v-kw]   (dY: Hv x Wv)
-// block: 64 ring positions x 4 output-channel groups, LDS combine
+// one wave per ring position (wave-uniform dY reads: one line per load), lanes over ci
 __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
                                                          float* __restrict__ ring, int Cout, int Cin, int KS, int Hv,
                                                          int Wv, int R) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int r = blockIdx.x * 64 + lane;
-  const int ci = blockIdx.y, n = blockIdx.z;
+  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int ci = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int n = blockIdx.z;
+  if (r >= R) return;
   const int p = KS / 2;
+  int u, v;
+  ring_pos(r, Hv, Wv, p, u, v);
+  const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
+  const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
+  const int cic = ci < Cin ? ci : Cin - 1;
   float acc = 0.f;
-  if (r < R) {
-    int u, v;
-    ring_pos(r, Hv, Wv, p, u, v);
-    const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
-    const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
-    for (int co = grp; co < Cout; co += 4) {
-      const float* wp = w + ((long)co * Cin + ci) * KS * KS;
-      const float* dp = dy + ((long)n * Cout + co) * Hv * Wv;
-      for (int kh = kh0; kh <= kh1; ++kh)
-        for (int kw = kw0; kw <= kw1; ++kw) acc += wp[kh * KS + kw] * dp[(u - kh) * Wv + (v - kw)];
-    }
+  for (int co = 0; co < Cout; ++co) {
+    const float* wp = w + ((long)co * Cin + cic) * KS * KS;
+    const float* dp = dy + ((long)n * Cout + co) * Hv * Wv;
+    for (int kh = kh0; kh <= kh1; ++kh)
+      for (int kw = kw0; kw <= kw1; ++kw) acc += wp[kh * KS + kw] * dp[(u - kh) * Wv + (v - kw)];
   }
-  part[grp][lane] = acc;
-  __syncthreads();
-  if (grp == 0 && r < R)
-    ring[((long)n * Cin + ci) * R + r] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+  if (ci < Cin) ring[((long)n * Cin + ci) * R + r] = acc;
 }
 
 // dx (+)= ring contributions, for the border band of dX only (each element written by one thread)
@@ -765,7 +761,7 @@ int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout
   VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
   VST_CHECK_ARG(Cin <= 65535 && N <= 65535);
   const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
-  dim3 g(ceil_div(R, 64), Cin, N);
+  dim3 g(ceil_div(R, 4), ceil_div(Cin, 64), N);
   dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, Cout, Cin, KS, Hv, Wv, R);
   return vst_launch_status();
 }
