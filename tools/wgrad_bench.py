@@ -1,0 +1,76 @@
+"""Microbenchmark of the split-K weight-gradient kernel (vst_conv_wgrad) on the step's layer
+shapes, optionally across library builds.  Interleaved rounds, HIP-event timing.
+
+    python tools/wgrad_bench.py [lib.so ...]
+"""
+import ctypes
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, "video-style-transfer_amd")
+from vst._lib import LIB_PATH, _CTYPES, parse_header  # noqa: E402
+
+# name, N, Cin, H, W, Cout, k, stride, gmode(0 reflect / 1 zero), pad, up
+SHAPES = [
+    ("res", 16, 192, 64, 128, 192, 3, 1, 0, 1, 1),
+    ("deconv1", 16, 192, 64, 128, 96, 3, 1, 0, 1, 2),
+    ("deconv2", 16, 96, 128, 256, 48, 3, 1, 0, 1, 2),
+    ("conv2", 16, 48, 256, 512, 96, 3, 2, 0, 1, 1),
+    ("conv3", 16, 96, 128, 256, 192, 3, 2, 0, 1, 1),
+    ("conv1", 16, 3, 256, 512, 48, 9, 1, 0, 4, 1),
+]
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    for name, (rt, argts) in parse_header().items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype = _CTYPES[rt] if rt != "char*" else ctypes.c_char_p
+            fn.argtypes = [_CTYPES[a] for a in argts]
+    return lib
+
+
+def main():
+    paths = sys.argv[1:] or [LIB_PATH]
+    libs = [load(p) for p in paths]
+    st = torch.cuda.current_stream().cuda_stream
+    res = {(p, s[0]): [] for p in paths for s in SHAPES}
+    bufs = {}
+    for s in SHAPES:
+        name, N, Cin, H, W, Cout, k, stride, gm, pad, up = s
+        Ho = (H * up + 2 * pad - k) // stride + 1
+        Wo = (W * up + 2 * pad - k) // stride + 1
+        x = torch.randn(N, Cin, H, W, device="cuda")
+        dy = torch.randn(N, Cout, Ho, Wo, device="cuda")
+        dw = torch.empty(Cout, Cin, k, k, device="cuda")
+        ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout, k * k * Cin, Ho * Wo), device="cuda")
+        bufs[name] = (x, dy, dw, ws, Ho, Wo, 2.0 * N * Cout * Ho * Wo * Cin * k * k)
+    for _ in range(5):
+        for p, lib in zip(paths, libs):
+            for s in SHAPES:
+                name, N, Cin, H, W, Cout, k, stride, gm, pad, up = s
+                x, dy, dw, ws, Ho, Wo, fl = bufs[name]
+                args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, Ho, Wo, k, k, gm,
+                        stride, pad, up, 0, st)
+                lib.vst_conv_wgrad(*args)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    lib.vst_conv_wgrad(*args)
+                e1.record()
+                torch.cuda.synchronize()
+                res[(p, name)].append(e0.elapsed_time(e1) / 5)
+    for s in SHAPES:
+        fl = bufs[s[0]][-1]
+        line = f"{s[0]:10s}"
+        for p in paths:
+            ms = statistics.median(res[(p, s[0])])
+            line += f"  {ms:7.3f} ms {fl / ms / 1e9:6.1f} TF"
+        print(line)
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,7 @@ struct ConvParams {
   int M, Mpad, K, Kpad;
   int Ho, Wo;
   int KH, KW, gmode, stride, pad, up;
+  int pad_x;  // column padding (= pad except for the dgrad ring segments)
   int epi;
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
@@ -54,7 +55,7 @@ enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16 };
 // (select-only arithmetic: no divergent branches inside the k loop)
 __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox, int kh, int kw) {
   if (P.gmode == GM_TRANSPOSED) {
-    int ty = oy + P.pad - kh, tx = ox + P.pad - kw;
+    int ty = oy + P.pad - kh, tx = ox + P.pad_x - kw;
     bool ok = ty >= 0 && tx >= 0;
     if (P.stride == 2) {
       ok = ok && !((ty | tx) & 1);
@@ -65,7 +66,7 @@ __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox
     return ok ? ty * P.Ws + tx : -1;
   }
   const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
-  int y = oy * P.stride + kh - P.pad, x = ox * P.stride + kw - P.pad;
+  int y = oy * P.stride + kh - P.pad, x = ox * P.stride + kw - P.pad_x;
   bool ok = true;
   if (P.gmode == GM_REFLECT) {
     y = abs(y);
@@ -489,14 +490,12 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
   return vst_launch_status();
 }
 
-int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
-                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream) {
-  VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
-  VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
-  VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
-  VST_CHECK_ARG(!((epi & EPI_BIAS) && !bias) && !((epi & EPI_MASK) && !mask));
-  if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad < Ws * up);
+}  // extern "C"
+
+static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
+                            int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
+                            int stride, int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux,
+                            const float* gmask, void* stream) {
   ConvParams P;
   P.src = src;
   P.wpack = wpack;
@@ -522,6 +521,7 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   P.gmode = gmode;
   P.stride = stride;
   P.pad = pad;
+  P.pad_x = pad_x;
   P.up = up;
   P.epi = epi;
   P.fd_Wo = make_fastdiv(Wo);
@@ -535,6 +535,20 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   else
     gmask ? launch_cfg<false, true>(cfg, grid, st, P) : launch_cfg<false, false>(cfg, grid, st, P);
   return vst_launch_status();
+}
+
+extern "C" {
+
+int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
+                  int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream) {
+  VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
+  VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
+  VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
+  VST_CHECK_ARG(!((epi & EPI_BIAS) && !bias) && !((epi & EPI_MASK) && !mask));
+  if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad < Ws * up);
+  return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad, up,
+                          epi, a_batch_stride, aux, gmask, stream);
 }
 
 int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,
@@ -645,61 +659,33 @@ __global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict
   out[apack_index(k, m, Mpad)] = v;
 }
 
-// ring position r of a (Hv+2p) x (Wv+2p) padded plane -> (u, v); layout: p top rows, p bottom rows,
-// then the Hv core rows' p left and p right columns
-__device__ __forceinline__ void ring_pos(int r, int Hv, int Wv, int p, int& u, int& v) {
-  const int Wp = Wv + 2 * p;
-  if (r < 2 * p * Wp) {
-    const int row = r / Wp;
-    v = r - row * Wp;
-    u = row < p ? row : Hv + row;  // rows [0,p) and [Hv+p, Hv+2p)
+// The ring of the padded-grid gradient, stored as four segments (each written by one GEMM):
+// top [NC][p][Wv+2p], bottom [NC][p][Wv+2p], left [NC][Hv][p], right [NC][Hv][p].
+struct Ring {
+  const float *top, *bot, *left, *right;
+  int Hv, Wv, p;
+};
+
+// value of padded-grid position (u, v) if it lies on the ring (returns false for core positions)
+__device__ __forceinline__ bool ring_at(const Ring& R, long nc, int u, int v, float& val) {
+  const int p = R.p, Wp = R.Wv + 2 * p;
+  if (u < p) {
+    val = R.top[(nc * p + u) * Wp + v];
+  } else if (u >= R.Hv + p) {
+    val = R.bot[(nc * p + (u - R.Hv - p)) * Wp + v];
+  } else if (v < p) {
+    val = R.left[(nc * R.Hv + (u - p)) * p + v];
+  } else if (v >= R.Wv + p) {
+    val = R.right[(nc * R.Hv + (u - p)) * p + (v - R.Wv - p)];
   } else {
-    r -= 2 * p * Wp;
-    const int side = r / (Hv * p);
-    r -= side * Hv * p;
-    u = p + r / p;
-    const int c = r % p;
-    v = side == 0 ? c : Wv + p + c;
+    return false;
   }
-}
-
-__device__ __forceinline__ int ring_index(int u, int v, int Hv, int Wv, int p) {
-  const int Wp = Wv + 2 * p;
-  if (u < p) return u * Wp + v;
-  if (u >= Hv + p) return (u - Hv) * Wp + v;
-  if (v < p) return 2 * p * Wp + (u - p) * p + v;
-  if (v >= Wv + p) return 2 * p * Wp + Hv * p + (u - p) * p + (v - Wv - p);
-  return -1;
-}
-
-// ring[n][ci][r] = sum_{co,kh,kw} W[co][ci][kh][kw] dY[n][co][u-kh][v-kw]   (dY: Hv x Wv)
-// one wave per ring position (wave-uniform dY reads: one line per load), lanes over ci
-__global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
-                                                         float* __restrict__ ring, int Cout, int Cin, int KS, int Hv,
-                                                         int Wv, int R) {
-  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int ci = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int n = blockIdx.z;
-  if (r >= R) return;
-  const int p = KS / 2;
-  int u, v;
-  ring_pos(r, Hv, Wv, p, u, v);
-  const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
-  const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
-  const int cic = ci < Cin ? ci : Cin - 1;
-  float acc = 0.f;
-  for (int co = 0; co < Cout; ++co) {
-    const float* wp = w + ((long)co * Cin + cic) * KS * KS;
-    const float* dp = dy + ((long)n * Cout + co) * Hv * Wv;
-    for (int kh = kh0; kh <= kh1; ++kh)
-      for (int kw = kw0; kw <= kw1; ++kw) acc += wp[kh * KS + kw] * dp[(u - kh) * Wv + (v - kw)];
-  }
-  if (ci < Cin) ring[((long)n * Cin + ci) * R + r] = acc;
+  return true;
 }
 
 // dx (+)= ring contributions, for the border band of dX only (each element written by one thread)
-__global__ void fold_ring_kernel(const float* __restrict__ ring, float* __restrict__ dx, int NC, int Hs, int Ws,
-                                 int p, int up, int bt, int bb, int ct, int cb, int R) {
+__global__ void fold_ring_kernel(Ring RG, float* __restrict__ dx, int NC, int Hs, int Ws, int up, int bt, int bb,
+                                 int ct, int cb) {
   const int nb = (bt + bb) * Ws + (Hs - bt - bb) * (ct + cb);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nb) return;
@@ -716,23 +702,21 @@ __global__ void fold_ring_kernel(const float* __restrict__ ring, float* __restri
     const int c = q % (ct + cb);
     x = c < ct ? c : Ws - cb + (c - ct);
   }
-  const int Hv = Hs * up, Wv = Ws * up;
+  const int p = RG.p;
   for (int nc = blockIdx.y; nc < NC; nc += gridDim.y) {
-    const float* rp = ring + (long)nc * R;
     float s = 0.f;
     for (int dy = 0; dy < up; ++dy) {
-      const Src3 ry = reflect_sources(y * up + dy, Hv, p);
+      const Src3 ry = reflect_sources(y * up + dy, RG.Hv, p);
       for (int dxx = 0; dxx < up; ++dxx) {
-        const Src3 cx = reflect_sources(x * up + dxx, Wv, p);
+        const Src3 cx = reflect_sources(x * up + dxx, RG.Wv, p);
         const int us[3] = {ry.a, ry.b, ry.c};
         const int vs[3] = {cx.a, cx.b, cx.c};
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            if (us[i] < 0 || vs[j] < 0) continue;
-            const int ri = ring_index(us[i], vs[j], Hv, Wv, p);
-            if (ri >= 0) s += rp[ri];
+            float v;
+            if (us[i] >= 0 && vs[j] >= 0 && ring_at(RG, nc, us[i], vs[j], v)) s += v;
           }
       }
     }
@@ -756,14 +740,29 @@ long vst_dgrad_ring_size(int Hv, int Wv, int KS) {
   return 2L * p * (Wv + 2 * p) + 2L * Hv * p;
 }
 
-int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
+// ring = N*Cin*vst_dgrad_ring_size floats; wpack_t: vst_pack_weight(w, transposed=1) of the conv
+int vst_dgrad_ring(const float* dy, const float* wpack_t, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream) {
-  VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
-  VST_CHECK_ARG(Cin <= 65535 && N <= 65535);
-  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
-  dim3 g(ceil_div(R, 4), ceil_div(Cin, 64), N);
-  dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, Cout, Cin, KS, Hv, Wv, R);
-  return vst_launch_status();
+  VST_CHECK_ARG(dy && wpack_t && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
+  const int p = KS / 2, Wp = Wv + 2 * p, K = KS * KS * Cout;
+  const long NC = (long)N * Cin;
+  float* top = ring;
+  float* bot = top + NC * p * Wp;
+  float* left = bot + NC * p * Wp;
+  float* right = left + NC * Hv * p;
+  // each segment is a transposed conv evaluated on its own output grid: ty = oy + pad_y - kh, tx = ox + pad_x - kw
+  int rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, top, N, Cout, Hv, Wv, Cin, K, p, Wp, KS, KS, GM_TRANSPOSED, 1,
+                            0, 0, 1, 0, 0, nullptr, nullptr, stream);
+  if (!rc)
+    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, bot, N, Cout, Hv, Wv, Cin, K, p, Wp, KS, KS, GM_TRANSPOSED, 1,
+                          Hv + p, 0, 1, 0, 0, nullptr, nullptr, stream);
+  if (!rc)
+    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, left, N, Cout, Hv, Wv, Cin, K, Hv, p, KS, KS, GM_TRANSPOSED, 1,
+                          p, 0, 1, 0, 0, nullptr, nullptr, stream);
+  if (!rc)
+    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, right, N, Cout, Hv, Wv, Cin, K, Hv, p, KS, KS, GM_TRANSPOSED, 1,
+                          p, Wv + p, 1, 0, 0, nullptr, nullptr, stream);
+  return rc;
 }
 
 int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream) {
@@ -774,10 +773,18 @@ int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS,
   const int bt = p / up + 1, bb = Hs - (Hv - 1 - p) / up;
   const int ct = p / up + 1, cb = Ws - (Wv - 1 - p) / up;
   VST_CHECK_ARG(bt + bb <= Hs && ct + cb <= Ws && Hv > 2 * p + 1 && Wv > 2 * p + 1);
-  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
+  const int Wp = Wv + 2 * p;
+  Ring RG;
+  RG.top = ring;
+  RG.bot = RG.top + NC * p * Wp;
+  RG.left = RG.bot + NC * p * Wp;
+  RG.right = RG.left + NC * Hv * p;
+  RG.Hv = Hv;
+  RG.Wv = Wv;
+  RG.p = p;
   const int nb = (bt + bb) * Ws + (Hs - bt - bb) * (ct + cb);
   dim3 g(ceil_div(nb, 256), (unsigned)(NC < 65535 ? NC : 65535));
-  fold_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(ring, dx, (int)NC, Hs, Ws, p, up, bt, bb, ct, cb, R);
+  fold_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(RG, dx, (int)NC, Hs, Ws, up, bt, bb, ct, cb);
   return vst_launch_status();
 }
 
