@@ -70,12 +70,12 @@ int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of
  * vst_pack_weight_upsum), ring = the KS/2-wide border of the padded-grid gradient
- * (vst_dgrad_ring: four small transposed-conv GEMMs, one per ring segment, over the transposed
- * pack of vst_pack_weight; ring = N*Cin*vst_dgrad_ring_size floats), folded into dx's border
- * band by vst_fold_ring (accumulates). */
+ * (vst_dgrad_ring over the [Cout][Cin][KS][KS] weight; ring = N*Cin*vst_dgrad_ring_size floats in
+ * four segments top/bottom/left/right), folded into dx's border band by vst_fold_ring
+ * (accumulates). */
 int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream);
 long vst_dgrad_ring_size(int Hv, int Wv, int KS);
-int vst_dgrad_ring(const float* dy, const float* wpack_t, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
+int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream);
 int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream);
 

@@ -724,6 +724,68 @@ __global__ void fold_ring_kernel(Ring RG, float* __restrict__ dx, int NC, int Hs
   }
 }
 
+// ring value at padded-grid (u, v) = sum_{co,kh,kw} W[co][ci][kh][kw] dY[n][co][u-kh][v-kw]:
+// one wave per ring position (dY reads wave-uniform: one line per load), lanes over ci,
+// taps outer and 8 output channels per batch of independent loads (latency hiding)
+__global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
+                                                         float* __restrict__ ring, int N, int Cout, int Cin, int KS,
+                                                         int Hv, int Wv) {
+  const int p = KS / 2, Wp = Wv + 2 * p;
+  const int segtb = p * Wp, seglr = Hv * p, R = 2 * segtb + 2 * seglr;
+  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (r >= R) return;
+  const int ci = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int n = blockIdx.z;
+  const long NC = (long)N * Cin;
+  int u, v;
+  long o;  // output offset of (n, ci, r) in the segment layout
+  const long nc = (long)n * Cin + (ci < Cin ? ci : 0);
+  if (r < segtb) {
+    u = r / Wp;
+    v = r - u * Wp;
+    o = nc * segtb + r;
+  } else if (r < 2 * segtb) {
+    const int q = r - segtb;
+    u = Hv + p + q / Wp;
+    v = q % Wp;
+    o = NC * segtb + nc * segtb + q;
+  } else if (r < 2 * segtb + seglr) {
+    const int q = r - 2 * segtb;
+    u = p + q / p;
+    v = q % p;
+    o = 2 * NC * segtb + nc * seglr + q;
+  } else {
+    const int q = r - 2 * segtb - seglr;
+    u = p + q / p;
+    v = Wv + p + q % p;
+    o = 2 * NC * segtb + NC * seglr + nc * seglr + q;
+  }
+  const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
+  const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
+  const int cic = ci < Cin ? ci : Cin - 1;
+  const long wstride = (long)Cin * KS * KS;  // between output channels
+  const long dstride = (long)Hv * Wv;
+  float acc = 0.f;
+  for (int kh = kh0; kh <= kh1; ++kh)
+    for (int kw = kw0; kw <= kw1; ++kw) {
+      const float* wp = w + (long)cic * KS * KS + kh * KS + kw;
+      const float* dp = dy + (long)n * Cout * dstride + (u - kh) * Wv + (v - kw);
+      int co = 0;
+      for (; co + 8 <= Cout; co += 8) {
+        float wv[8], dv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          wv[i] = wp[(co + i) * wstride];
+          dv[i] = dp[(co + i) * dstride];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += wv[i] * dv[i];
+      }
+      for (; co < Cout; ++co) acc += wp[co * wstride] * dp[co * dstride];
+    }
+  if (ci < Cin) ring[o] = acc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -740,29 +802,15 @@ long vst_dgrad_ring_size(int Hv, int Wv, int KS) {
   return 2L * p * (Wv + 2 * p) + 2L * Hv * p;
 }
 
-// ring = N*Cin*vst_dgrad_ring_size floats; wpack_t: vst_pack_weight(w, transposed=1) of the conv
-int vst_dgrad_ring(const float* dy, const float* wpack_t, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
+// ring = N*Cin*vst_dgrad_ring_size floats (segment layout of fold_ring_kernel)
+int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream) {
-  VST_CHECK_ARG(dy && wpack_t && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
-  const int p = KS / 2, Wp = Wv + 2 * p, K = KS * KS * Cout;
-  const long NC = (long)N * Cin;
-  float* top = ring;
-  float* bot = top + NC * p * Wp;
-  float* left = bot + NC * p * Wp;
-  float* right = left + NC * Hv * p;
-  // each segment is a transposed conv evaluated on its own output grid: ty = oy + pad_y - kh, tx = ox + pad_x - kw
-  int rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, top, N, Cout, Hv, Wv, Cin, K, p, Wp, KS, KS, GM_TRANSPOSED, 1,
-                            0, 0, 1, 0, 0, nullptr, nullptr, stream);
-  if (!rc)
-    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, bot, N, Cout, Hv, Wv, Cin, K, p, Wp, KS, KS, GM_TRANSPOSED, 1,
-                          Hv + p, 0, 1, 0, 0, nullptr, nullptr, stream);
-  if (!rc)
-    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, left, N, Cout, Hv, Wv, Cin, K, Hv, p, KS, KS, GM_TRANSPOSED, 1,
-                          p, 0, 1, 0, 0, nullptr, nullptr, stream);
-  if (!rc)
-    rc = conv_gemm_launch(dy, wpack_t, nullptr, nullptr, right, N, Cout, Hv, Wv, Cin, K, Hv, p, KS, KS, GM_TRANSPOSED, 1,
-                          p, Wv + p, 1, 0, 0, nullptr, nullptr, stream);
-  return rc;
+  VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
+  VST_CHECK_ARG(N <= 65535);
+  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
+  dim3 g(ceil_div(R, 4), ceil_div(Cin, 64), N);
+  dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, N, Cout, Cin, KS, Hv, Wv);
+  return vst_launch_status();
 }
 
 int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream) {

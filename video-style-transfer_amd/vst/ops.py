@@ -124,9 +124,8 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
     Cout = w.shape[0]
     p = ks // 2
     w = w.contiguous()
-    wt = packed_weight(w, transposed=True)
     if up == 1:
-        dx = conv_gemm(gz, wt, Cin, ks, H, W, GM_TRANSPOSED, 1, p, 1, algo_flops=flops)
+        dx = conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, 1, p, 1, algo_flops=flops)
     else:
         Mpad, Kpad = pack_dims(Cin, (ks + 1) * (ks + 1) * Cout)
         wp = _empty((Kpad * Mpad,), w)
@@ -134,7 +133,7 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
         dx = conv_gemm(gz, wp, Cin, ks + 1, H, W, GM_ZERO, 2, ks - 1 - p, 1, algo_flops=flops)
     Hv, Wv = H * up, W * up
     ring = _empty((N * Cin * lib.vst_dgrad_ring_size(Hv, Wv, ks),), gz)
-    lib.vst_dgrad_ring(ptr(gz), ptr(wt), ptr(ring), N, Cout, Cin, ks, Hv, Wv, stream())
+    lib.vst_dgrad_ring(ptr(gz), ptr(w), ptr(ring), N, Cout, Cin, ks, Hv, Wv, stream())
     lib.vst_fold_ring(ptr(ring), ptr(dx), N * Cin, H, W, ks, up, stream())
     return dx
 
