@@ -724,66 +724,82 @@ __global__ void fold_ring_kernel(Ring RG, float* __restrict__ dx, int NC, int Hs
   }
 }
 
-// ring value at padded-grid (u, v) = sum_{co,kh,kw} W[co][ci][kh][kw] dY[n][co][u-kh][v-kw]:
-// one wave per ring position (dY reads wave-uniform: one line per load), lanes over ci,
-// taps outer and 8 output channels per batch of independent loads (latency hiding)
+// Ring of the padded-grid gradient as 4p lines (top rows, bottom rows, left and right columns of
+// the border), each a small GEMM  out[ci][i] = sum_{co, taps} W[co][ci][kh][kw] dY[co][u_i-kh][v_i-kw]
+// over the taps that can reach the line (rows: kh <= u resp. kh >= u-Hv+1; columns: kw likewise).
+// Block: 64 positions x 64 input channels, 16-deep k-chunks staged in LDS, 4x4 outputs per thread.
 __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
                                                          float* __restrict__ ring, int N, int Cout, int Cin, int KS,
                                                          int Hv, int Wv) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
   const int p = KS / 2, Wp = Wv + 2 * p;
-  const int segtb = p * Wp, seglr = Hv * p, R = 2 * segtb + 2 * seglr;
-  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (r >= R) return;
-  const int ci = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int n = blockIdx.z;
-  const long NC = (long)N * Cin;
-  int u, v;
-  long o;  // output offset of (n, ci, r) in the segment layout
-  const long nc = (long)n * Cin + (ci < Cin ? ci : 0);
-  if (r < segtb) {
-    u = r / Wp;
-    v = r - u * Wp;
-    o = nc * segtb + r;
-  } else if (r < 2 * segtb) {
-    const int q = r - segtb;
-    u = Hv + p + q / Wp;
-    v = q % Wp;
-    o = NC * segtb + nc * segtb + q;
-  } else if (r < 2 * segtb + seglr) {
-    const int q = r - 2 * segtb;
-    u = p + q / p;
-    v = q % p;
-    o = 2 * NC * segtb + nc * seglr + q;
-  } else {
-    const int q = r - 2 * segtb - seglr;
-    u = p + q / p;
-    v = Wv + p + q % p;
-    o = 2 * NC * segtb + NC * seglr + nc * seglr + q;
-  }
-  const int kh0 = max(0, u - Hv + 1), kh1 = min(KS - 1, u);
-  const int kw0 = max(0, v - Wv + 1), kw1 = min(KS - 1, v);
-  const int cic = ci < Cin ? ci : Cin - 1;
-  const long wstride = (long)Cin * KS * KS;  // between output channels
-  const long dstride = (long)Hv * Wv;
-  float acc = 0.f;
+  const int line = blockIdx.z % (4 * p), n = blockIdx.z / (4 * p);
+  const int seg = line / p, li = line % p;  // 0 top, 1 bottom, 2 left, 3 right
+  const int len = seg < 2 ? Wp : Hv;
+  const int i0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
+  if (i0 >= len) return;
+  // line geometry: position i -> (u, v)
+  const int u0 = seg == 0 ? li : (seg == 1 ? Hv + p + li : p);
+  const int v0 = seg == 2 ? li : (seg == 3 ? Wv + p + li : 0);
+  const int du = seg < 2 ? 0 : 1, dv = seg < 2 ? 1 : 0;
+  int kh0 = 0, kh1 = KS - 1, kw0 = 0, kw1 = KS - 1;
+  if (seg == 0) kh1 = u0;
+  if (seg == 1) kh0 = u0 - Hv + 1;
+  if (seg == 2) kw1 = v0;
+  if (seg == 3) kw0 = v0 - Wv + 1;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  const long dplane = (long)Hv * Wv;
+  const float* dyn = dy + (long)n * Cout * dplane;
+  // loader roles: A: co row = t>>4 (16), ci = (t&15)*4..+3 ; B: co row = t>>4, positions (t&15)*4..+3
+  const int lr = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;
   for (int kh = kh0; kh <= kh1; ++kh)
-    for (int kw = kw0; kw <= kw1; ++kw) {
-      const float* wp = w + (long)cic * KS * KS + kh * KS + kw;
-      const float* dp = dy + (long)n * Cout * dstride + (u - kh) * Wv + (v - kw);
-      int co = 0;
-      for (; co + 8 <= Cout; co += 8) {
-        float wv[8], dv[8];
+    for (int kw = kw0; kw <= kw1; ++kw)
+      for (int c0 = 0; c0 < Cout; c0 += 16) {
+        const int co = c0 + lr;
+        __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          wv[i] = wp[(co + i) * wstride];
-          dv[i] = dp[(co + i) * dstride];
+        for (int j = 0; j < 4; ++j) {
+          const int ci = ci0 + lc + j;
+          As[lr][lc + j] = (co < Cout && ci < Cin) ? w[(((long)co * Cin + ci) * KS + kh) * KS + kw] : 0.f;
+          const int i = i0 + lc + j;
+          const int uu = u0 + du * i - kh, vv = v0 + dv * i - kw;
+          const bool ok = co < Cout && i < len && uu >= 0 && uu < Hv && vv >= 0 && vv < Wv;
+          Bs[lr][lc + j] = ok ? dyn[co * dplane + (long)uu * Wv + vv] : 0.f;
         }
+        __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc += wv[i] * dv[i];
+        for (int k = 0; k < 16; ++k) {
+          const float4 a = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
+          const float4 bq = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
+          const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] += av[x] * bv[y];
+        }
       }
-      for (; co < Cout; ++co) acc += wp[co * wstride] * dp[co * dstride];
+  // segment layout: top/bottom [NC][p][Wp], left/right [NC][Hv][p]
+  const long NC = (long)N * Cin;
+  const long segtb = (long)p * Wp, seglr = (long)Hv * p;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int ci = ci0 + ty * 4 + x;
+    if (ci >= Cin) continue;
+    const long nc = (long)n * Cin + ci;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int i = i0 + tx * 4 + y;
+      if (i >= len) continue;
+      long o;
+      if (seg == 0) o = nc * segtb + (long)li * Wp + i;
+      else if (seg == 1) o = NC * segtb + nc * segtb + (long)li * Wp + i;
+      else if (seg == 2) o = 2 * NC * segtb + nc * seglr + (long)i * p + li;
+      else o = 2 * NC * segtb + NC * seglr + nc * seglr + (long)i * p + li;
+      ring[o] = acc[x][y];
     }
-  if (ci < Cin) ring[o] = acc;
+  }
 }
 
 }  // namespace
@@ -806,9 +822,9 @@ long vst_dgrad_ring_size(int Hv, int Wv, int KS) {
 int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream) {
   VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
-  VST_CHECK_ARG(N <= 65535);
-  const int R = (int)vst_dgrad_ring_size(Hv, Wv, KS);
-  dim3 g(ceil_div(R, 4), ceil_div(Cin, 64), N);
+  const int p = KS / 2;
+  VST_CHECK_ARG((long)N * 4 * p <= 65535);
+  dim3 g(ceil_div(max(Wv + 2 * p, Hv), 64), ceil_div(Cin, 64), N * 4 * p);
   dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, N, Cout, Cin, KS, Hv, Wv);
   return vst_launch_status();
 }
