@@ -74,10 +74,11 @@ int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws
  * four segments top/bottom/left/right), folded into dx's border band by vst_fold_ring
  * (accumulates). */
 int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream);
-long vst_dgrad_ring_size(int Hv, int Wv, int KS);
+int vst_dgrad_ring_splits(int Cout, int KS);
+long vst_dgrad_ring_size(int Hv, int Wv, int KS, int Cout);
 int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream);
-int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream);
+int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, int Cout, void* stream);
 
 /* adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hs*up+2p][Ws*up+2p] -> dx [NC][Hs][Ws] */
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,

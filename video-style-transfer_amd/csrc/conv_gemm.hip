@@ -663,23 +663,28 @@ __global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict
 // top [NC][p][Wv+2p], bottom [NC][p][Wv+2p], left [NC][Hv][p], right [NC][Hv][p].
 struct Ring {
   const float *top, *bot, *left, *right;
-  int Hv, Wv, p;
+  int Hv, Wv, p, S;
+  long slab;  // floats between split-K slabs
 };
 
 // value of padded-grid position (u, v) if it lies on the ring (returns false for core positions)
 __device__ __forceinline__ bool ring_at(const Ring& R, long nc, int u, int v, float& val) {
   const int p = R.p, Wp = R.Wv + 2 * p;
+  const float* q;
   if (u < p) {
-    val = R.top[(nc * p + u) * Wp + v];
+    q = R.top + (nc * p + u) * Wp + v;
   } else if (u >= R.Hv + p) {
-    val = R.bot[(nc * p + (u - R.Hv - p)) * Wp + v];
+    q = R.bot + (nc * p + (u - R.Hv - p)) * Wp + v;
   } else if (v < p) {
-    val = R.left[(nc * R.Hv + (u - p)) * p + v];
+    q = R.left + (nc * R.Hv + (u - p)) * p + v;
   } else if (v >= R.Wv + p) {
-    val = R.right[(nc * R.Hv + (u - p)) * p + (v - R.Wv - p)];
+    q = R.right + (nc * R.Hv + (u - p)) * p + (v - R.Wv - p);
   } else {
     return false;
   }
+  float a = 0.f;
+  for (int z = 0; z < R.S; ++z) a += q[z * R.slab];
+  val = a;
   return true;
 }
 
@@ -730,11 +735,11 @@ __global__ void fold_ring_kernel(Ring RG, float* __restrict__ dx, int NC, int Hs
 // Block: 64 positions x 64 input channels, 16-deep k-chunks staged in LDS, 4x4 outputs per thread.
 __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict__ dy, const float* __restrict__ w,
                                                          float* __restrict__ ring, int N, int Cout, int Cin, int KS,
-                                                         int Hv, int Wv) {
+                                                         int Hv, int Wv, int S) {
   __shared__ float As[16][64 + 4];
   __shared__ float Bs[16][64 + 4];
   const int p = KS / 2, Wp = Wv + 2 * p;
-  const int line = blockIdx.z % (4 * p), n = blockIdx.z / (4 * p);
+  const int line = blockIdx.z % (4 * p), sidx = (blockIdx.z / (4 * p)) % S, n = blockIdx.z / (4 * p * S);
   const int seg = line / p, li = line % p;  // 0 top, 1 bottom, 2 left, 3 right
   const int len = seg < 2 ? Wp : Hv;
   const int i0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
@@ -754,10 +759,14 @@ __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict
   const float* dyn = dy + (long)n * Cout * dplane;
   // loader roles: A: co row = t>>4 (16), ci = (t&15)*4..+3 ; B: co row = t>>4, positions (t&15)*4..+3
   const int lr = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;
-  for (int kh = kh0; kh <= kh1; ++kh)
-    for (int kw = kw0; kw <= kw1; ++kw)
-      for (int c0 = 0; c0 < Cout; c0 += 16) {
-        const int co = c0 + lr;
+  // flattened (kh, kw, co-chunk) iteration space, split S ways across blocks (slab sidx)
+  const int nch = (Cout + 15) / 16, nkw = kw1 - kw0 + 1;
+  const int T = (kh1 - kh0 + 1) * nkw * nch;
+  const int t0 = (int)((long)T * sidx / S), t1 = (int)((long)T * (sidx + 1) / S);
+  for (int it = t0; it < t1; ++it) {
+        const int cch = it % nch, tap = it / nch;
+        const int kh = kh0 + tap / nkw, kw = kw0 + tap % nkw;
+        const int co = cch * 16 + lr;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -780,9 +789,10 @@ __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict
             for (int y = 0; y < 4; ++y) acc[x][y] += av[x] * bv[y];
         }
       }
-  // segment layout: top/bottom [NC][p][Wp], left/right [NC][Hv][p]
+  // segment layout: top/bottom [NC][p][Wp], left/right [NC][Hv][p]; slab sidx after the others
   const long NC = (long)N * Cin;
   const long segtb = (long)p * Wp, seglr = (long)Hv * p;
+  ring += (long)sidx * NC * (2 * segtb + 2 * seglr);
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     const int ci = ci0 + ty * 4 + x;
@@ -813,23 +823,32 @@ int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int 
   return vst_launch_status();
 }
 
-long vst_dgrad_ring_size(int Hv, int Wv, int KS) {
+// split-K ways of the ring GEMMs: <= ~8 k-chunk iterations per block
+int vst_dgrad_ring_splits(int Cout, int KS) {
   const int p = KS / 2;
-  return 2L * p * (Wv + 2 * p) + 2L * Hv * p;
+  const long tmax = (long)(p + 1) * KS * ((Cout + 15) / 16);
+  long S = (tmax + 7) / 8;
+  return (int)(S < 1 ? 1 : (S > 8 ? 8 : S));
+}
+
+// floats per (n, ci) plane of the ring buffer, all split-K slabs included
+long vst_dgrad_ring_size(int Hv, int Wv, int KS, int Cout) {
+  const int p = KS / 2;
+  return (2L * p * (Wv + 2 * p) + 2L * Hv * p) * vst_dgrad_ring_splits(Cout, KS);
 }
 
 // ring = N*Cin*vst_dgrad_ring_size floats (segment layout of fold_ring_kernel)
 int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
                    void* stream) {
   VST_CHECK_ARG(dy && w && ring && N > 0 && Cout > 0 && Cin > 0 && (KS & 1) && KS > 1 && Hv > KS && Wv > KS);
-  const int p = KS / 2;
-  VST_CHECK_ARG((long)N * 4 * p <= 65535);
-  dim3 g(ceil_div(max(Wv + 2 * p, Hv), 64), ceil_div(Cin, 64), N * 4 * p);
-  dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, N, Cout, Cin, KS, Hv, Wv);
+  const int p = KS / 2, S = vst_dgrad_ring_splits(Cout, KS);
+  VST_CHECK_ARG((long)N * 4 * p * S <= 65535);
+  dim3 g(ceil_div(max(Wv + 2 * p, Hv), 64), ceil_div(Cin, 64), N * 4 * p * S);
+  dgrad_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(dy, w, ring, N, Cout, Cin, KS, Hv, Wv, S);
   return vst_launch_status();
 }
 
-int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, void* stream) {
+int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS, int up, int Cout, void* stream) {
   const int p = KS / 2;
   VST_CHECK_ARG(ring && dx && NC > 0 && (up == 1 || up == 2) && (KS & 1) && KS > 1);
   const int Hv = Hs * up, Wv = Ws * up;
@@ -846,6 +865,8 @@ int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS,
   RG.Hv = Hv;
   RG.Wv = Wv;
   RG.p = p;
+  RG.S = vst_dgrad_ring_splits(Cout, KS);
+  RG.slab = NC * (2L * p * Wp + 2L * Hv * p);
   const int nb = (bt + bb) * Ws + (Hs - bt - bb) * (ct + cb);
   dim3 g(ceil_div(nb, 256), (unsigned)(NC < 65535 ? NC : 65535));
   fold_ring_kernel<<<g, 256, 0, (hipStream_t)stream>>>(RG, dx, (int)NC, Hs, Ws, up, bt, bb, ct, cb);

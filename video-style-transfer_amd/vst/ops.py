@@ -132,9 +132,9 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
         lib.vst_pack_weight_upsum(ptr(w), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
         dx = conv_gemm(gz, wp, Cin, ks + 1, H, W, GM_ZERO, 2, ks - 1 - p, 1, algo_flops=flops)
     Hv, Wv = H * up, W * up
-    ring = _empty((N * Cin * lib.vst_dgrad_ring_size(Hv, Wv, ks),), gz)
+    ring = _empty((N * Cin * lib.vst_dgrad_ring_size(Hv, Wv, ks, Cout),), gz)
     lib.vst_dgrad_ring(ptr(gz), ptr(w), ptr(ring), N, Cout, Cin, ks, Hv, Wv, stream())
-    lib.vst_fold_ring(ptr(ring), ptr(dx), N * Cin, H, W, ks, up, stream())
+    lib.vst_fold_ring(ptr(ring), ptr(dx), N * Cin, H, W, ks, up, Cout, stream())
     return dx
 
 
