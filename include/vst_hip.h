@@ -115,7 +115,8 @@ int vst_channel_sum(const float* x, float* out, float* partial, int N, int C, in
 
 /* ---- VGG MaxPool2d(2, 2) (RC/network.py:12-24 via torchvision features) -------------------- */
 int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream);
-int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, void* stream);
+/* relu_mask: gx also masked by x > 0 (x = ReLU output consumed only by this pool) */
+int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, int relu_mask, void* stream);
 
 /* ---- flow warp (RC/utilities.py:39-57) / occlusion mask (RC/utilities.py:60-90) ------------
  * warp_bwd scatters with float atomics into gx (zero it first or accumulate). */

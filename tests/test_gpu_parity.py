@@ -136,6 +136,32 @@ def test_conv_relu_frozen_weights_dgrad_mask():
     assert rel_err(C(xg.grad), xr.grad) < 1e-4
 
 
+def test_vgg_slice_fused_relu_backward():
+    """run_vgg_slice: ReLU outputs consumed only by the next conv / pool get their backward mask
+    from the consumer (dgrad epilogue, pool backward); the slice output keeps its own pass."""
+    import torch.nn as nn
+
+    from vst.reconet.network import run_vgg_slice
+
+    g = torch.Generator().manual_seed(9)
+    seq = nn.Sequential(nn.Conv2d(16, 32, 3, padding=1), nn.ReLU(), nn.Conv2d(32, 32, 3, padding=1), nn.ReLU(),
+                        nn.MaxPool2d(2, 2), nn.Conv2d(32, 48, 3, padding=1), nn.ReLU(), nn.Conv2d(48, 48, 3, padding=1),
+                        nn.ReLU())
+    for prm in seq.parameters():
+        prm.requires_grad_(False)
+        prm.copy_(torch.randn(prm.shape, generator=g) * 0.15)
+    x = torch.randn(2, 16, 12, 18, generator=g)
+    xr = x.clone().requires_grad_(True)
+    ref = seq(xr)
+    gy = torch.randn(ref.shape, generator=g)
+    ref.backward(gy)
+    xg = G(x).requires_grad_(True)
+    out = run_vgg_slice(seq.to(DEV), xg)
+    out.backward(G(gy))
+    assert rel_err(C(out), ref.detach()) < 1e-4
+    assert rel_err(C(xg.grad), xr.grad) < 1e-4
+
+
 @pytest.mark.parametrize("relu,res,shape", [(True, False, (2, 48, 16, 20)), (False, True, (2, 192, 9, 15)),
                                             (True, False, (1, 96, 64, 128))])
 def test_instance_norm(relu, res, shape):

@@ -30,7 +30,7 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restric
 
 // gx over the full input (zeros where no window routes a gradient)
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ gx,
-                                   long NC, int H, int W) {
+                                   long NC, int H, int W, int relu_mask) {
   const int Ho = H / 2, Wo = W / 2;
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NC * H * W) return;
@@ -51,7 +51,8 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
         m = v[k];
         arg = k;
       }
-    if (arg == (iy & 1) * 2 + (ix & 1)) g = gy[nc * Ho * Wo + (long)oy * Wo + ox];
+    // relu_mask: x is a ReLU output whose only consumer is this pool -> fold the ReLU backward in
+    if (arg == (iy & 1) * 2 + (ix & 1) && (!relu_mask || m > 0.f)) g = gy[nc * Ho * Wo + (long)oy * Wo + ox];
   }
   gx[idx] = g;
 }
@@ -246,10 +247,10 @@ int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* st
   return vst_launch_status();
 }
 
-int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, void* stream) {
+int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, int relu_mask, void* stream) {
   VST_CHECK_ARG(x && gy && gx && NC > 0 && H >= 2 && W >= 2);
   long total = NC * H * W;
-  maxpool_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, gx, NC, H, W);
+  maxpool_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, gx, NC, H, W, relu_mask);
   return vst_launch_status();
 }
 

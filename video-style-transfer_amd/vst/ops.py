@@ -94,15 +94,19 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     return out
 
 
-def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None):
-    """Input gradient of (upsample x`up` -> pad -> conv(stride)) given the conv-output grad gz."""
+def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=None):
+    """Input gradient of (upsample x`up` -> pad -> conv(stride)) given the conv-output grad gz;
+    dmask: multiply the result by (dmask > 0) in the GEMM epilogue (zero-pad path only)."""
     N, Cin, H, W = x_shape
     Cout = w.shape[0]
     Ho, Wo = gz.shape[2:]
     flops = 2.0 * N * Cout * Ho * Wo * Cin * ks * ks
     if pad_mode == "zero" and up == 1:
         return conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1,
-                         gmask=gmask, algo_flops=flops)
+                         gmask=gmask, algo_flops=flops, epi=EPI_MASK if dmask is not None else 0,
+                         mask=dmask.contiguous() if dmask is not None else None)
+    if dmask is not None:
+        raise VstError("dgrad: fused ReLU mask only on the zero-pad (VGG) path")
     if pad_mode != "reflect":
         raise VstError("dgrad: zero padding with upsampling is not on the reference path")
     if stride == 2 and up == 1:
@@ -233,9 +237,13 @@ class Conv2dFn(Function):
     torchvision VGG Conv2d+ReLU pairs (RC/network.py:17-24, AA/vgg19.py:19-37)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act, bias_const=None):
+    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act, bias_const=None, mask_dx=False, premasked=False):
         """bias_const: a bias added in the epilogue whose gradient another Function produces
-        (conv -> InstanceNorm: the norm's backward already sums the conv-output gradient)."""
+        (conv -> InstanceNorm: the norm's backward already sums the conv-output gradient).
+        mask_dx: x is a ReLU output consumed only by this conv -> the data gradient is written
+        masked by x > 0 (the ReLU backward of the producer, fused into this dgrad's epilogue);
+        premasked: this conv's ReLU output is consumed only by such a masking consumer, so the
+        incoming gradient is already masked and the separate ReLU-backward pass is skipped."""
         x = _check(x, "conv input", 4)
         w = w.contiguous()
         N, Cin, H, W = x.shape
@@ -252,6 +260,7 @@ class Conv2dFn(Function):
             out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
                             stride, pad, up, epi=epi, bias=bias, aux=aux)
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
+        ctx.relu_flags = (bool(mask_dx), bool(premasked))
         ctx.has_bias = b is not None and bias_const is None
         ctx.params = (w, b)  # leaves: weight gradients go straight into their .grad when possible
         ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
@@ -266,14 +275,15 @@ class Conv2dFn(Function):
         if act == "tanh":
             gz = _empty(gy.shape, gy)
             lib.vst_tanh_out_bwd(ptr(gy), ptr(t), ptr(gz), gy.numel(), gy[0, 0].numel(), 0, stream())
-        elif act == "relu":
+        elif act == "relu" and not ctx.relu_flags[1]:
             # a separate masking pass (3 HBM streams) measured cheaper than gathering the mask
             # inside the dgrad GEMM (one extra load per gathered element, 9x per output)
             gz = _empty(gy.shape, gy)
             lib.vst_relu_bwd(ptr(gy), ptr(y), ptr(gz), gy.numel(), stream())
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask)
+            dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask,
+                            dmask=x if ctx.relu_flags[0] else None)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
             if rowsplit_ok(w.shape[0], ks, stride, pad_mode, up) and pad == ks // 2:
@@ -285,11 +295,11 @@ class Conv2dFn(Function):
             sink = grad_sink(ctx.params[1])
             db = channel_sum(gz, out=sink)
             db = None if sink is not None else db
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
-def conv2d(x, w, b=None, stride=1, pad=0, pad_mode="zero", up=1, act=None):
-    return Conv2dFn.apply(x, w, b, stride, pad, pad_mode, up, act)
+def conv2d(x, w, b=None, stride=1, pad=0, pad_mode="zero", up=1, act=None, mask_dx=False, premasked=False):
+    return Conv2dFn.apply(x, w, b, stride, pad, pad_mode, up, act, None, mask_dx, premasked)
 
 
 class InstanceNormFn(Function):
@@ -353,11 +363,12 @@ class MaxPool2x2Fn(Function):
     """nn.MaxPool2d(2, 2) of the VGG feature stacks."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, relu_mask=False):
         x = _check(x, "maxpool input", 4)
         N, C, H, W = x.shape
         y = _empty((N, C, H // 2, W // 2), x)
         lib.vst_maxpool2x2_fwd(ptr(x), ptr(y), N * C, H, W, stream())
+        ctx.relu_mask = relu_mask
         ctx.save_for_backward(x)
         return y
 
@@ -366,12 +377,14 @@ class MaxPool2x2Fn(Function):
         (x,) = ctx.saved_tensors
         N, C, H, W = x.shape
         gx = _empty(x.shape, x)
-        lib.vst_maxpool2x2_bwd(ptr(x), ptr(gy.contiguous()), ptr(gx), N * C, H, W, stream())
-        return gx
+        lib.vst_maxpool2x2_bwd(ptr(x), ptr(gy.contiguous()), ptr(gx), N * C, H, W, int(ctx.relu_mask), stream())
+        return gx, None
 
 
-def maxpool2x2(x):
-    return MaxPool2x2Fn.apply(x)
+def maxpool2x2(x, relu_mask=False):
+    """relu_mask: x is a ReLU output consumed only by this pool; the ReLU backward is folded into
+    the pool's backward (the producing conv is then built with premasked=True)."""
+    return MaxPool2x2Fn.apply(x, relu_mask)
 
 
 class WarpFn(Function):

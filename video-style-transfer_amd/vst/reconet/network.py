@@ -37,18 +37,26 @@ def vgg_features(cfg, n_layers):
 
 
 def run_vgg_slice(seq, x):
-    """Forward of one VGG slice on HIP kernels: Conv2d followed by ReLU -> fused conv+bias+relu."""
+    """Forward of one VGG slice on HIP kernels: Conv2d followed by ReLU -> fused conv+bias+relu.
+    A ReLU output consumed only by the next module of the slice (a conv or a max-pool) never sees
+    a separate ReLU-backward pass: the consumer's backward applies the mask (dgrad epilogue /
+    pool backward) and the producer is marked premasked.  Slice outputs (loss features) keep it."""
     mods = list(seq.children())
     i = 0
+    fuse_next = False  # the previous conv's ReLU output is consumed only by mods[i]
     while i < len(mods):
         m = mods[i]
         if isinstance(m, nn.Conv2d):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            nxt = mods[i + 2] if relu and i + 2 < len(mods) else None
+            internal = relu and isinstance(nxt, (nn.Conv2d, nn.MaxPool2d))
             x = ops.conv2d(x, m.weight, m.bias, stride=m.stride[0], pad=m.padding[0], pad_mode="zero",
-                           act="relu" if relu else None)
+                           act="relu" if relu else None, mask_dx=fuse_next, premasked=internal)
+            fuse_next = internal
             i += 2 if relu else 1
         elif isinstance(m, nn.MaxPool2d):
-            x = ops.maxpool2x2(x)
+            x = ops.maxpool2x2(x, relu_mask=fuse_next)
+            fuse_next = False
             i += 1
         elif isinstance(m, nn.ReLU):
             raise RuntimeError("standalone ReLU outside a conv+relu pair is not on the VGG path")
