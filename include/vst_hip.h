@@ -201,6 +201,24 @@ int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const f
                     const float* vns, const float* colc, const float* cols, const float* gout, float weight, float* dG,
                     float* dun, float* dvn, int N, int C, int HW, void* stream);
 
+/* Cosine attention without the S matrix (analytic row/column statistics, see adaattn.hip):
+ * vst_attn_gemm: per-image 1x1 GEMM with the affine epilogue out = (acc + ra_m) rb_m cg_p + rd_m
+ * (A = S c ks + e in the forward, dS = (dA - r) c ks in the backward); plane_dot: out[n][c] =
+ * sum_p x w; channel_dot: out[n][p] = sum_c x (v[n][c] | y[n][c][p]); attn_fwd_rows: c =
+ * 1/(rowsum qn), e = 1/rowsum from qkbar; attn_bwd_rows: dqn, -r, c r; scale_cols: y = x c[p];
+ * attn_dkn: dkn_j = -ks_j^2 sum_c K[c][j](Y[c][j] - qt[c]). */
+int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K, int P, int M, long a_batch_stride,
+                  const float* ra, const float* rb, const float* rd, const float* cg, void* stream);
+int vst_plane_dot(const float* x, const float* w, float* out, int N, int C, int P, void* stream);
+int vst_channel_dot(const float* x, const float* v, const float* y, float* out, int N, int C, int P, void* stream);
+int vst_attn_fwd_rows(const float* qkbar, const float* qn, float* c, float* e, long n, int Ns, void* stream);
+int vst_reciprocal(const float* x, float* y, long n, void* stream);
+int vst_attn_bwd_rows(const float* r, const float* DA, const float* qn, const float* c, const float* e, float* dqn,
+                      float* nr, float* cr, long n, int Ns, void* stream);
+int vst_scale_cols(const float* x, const float* c, float* y, int N, int R, int P, void* stream);
+int vst_attn_dkn(const float* K, const float* Y, const float* qt, const float* ks, float* dkn, int N, int d, int Ns,
+                 void* stream);
+
 /* dst[n][0:per] = src[n][0:per] with batch strides (channel concat / split, AA/network.py:87) */
 int vst_copy_planes(const float* src, long src_bs, float* dst, long dst_bs, int N, long per, void* stream);
 /* D = 1 - G / (un_i vn_j + 1e-6) (cosine_distance forward) */

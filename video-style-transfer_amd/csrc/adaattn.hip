@@ -522,3 +522,158 @@ extern "C" int vst_softmax_rows_bwd(const float* dA, const float* A, float* dS, 
   softmax_rows_bwd_kernel<<<rows, RT, 0, (hipStream_t)stream>>>(dA, A, dS, Ns);
   return vst_launch_status();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Analytic cosine-attention statistics (AA/network.py:115-125).  With s_ij = S_ij/(qn_i kn_j) + 1
+// and A = s / rowsum, every row/column reduction of the reference's N^2 matrices has a closed
+// form in O(d (Nc + Ns)):
+//   rowsum_i = (Q_i . kbar)/qn_i + Ns,          kbar = sum_j K_j / kn_j
+//   r_i  = sum_j dA_ij A_ij = sum_v dMV_vi MV_vi,   DA_i = sum_j dA_ij = sum_v dMV_vi vsum_v
+//   dqn_i = -(DA... ) see vst_attn_bwd_rows;  dkn_j via Y = Z^T [V;V^2], Z = (c . dMV) Q^T
+// so A (and dS) come straight out of the GEMM epilogues and S is never stored.
+namespace {
+
+// out[n][c] = sum_p x[n][c][p] * (w ? w[n][p] : 1)   (one block per (n, c) plane)
+__global__ void plane_dot_kernel(const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ out,
+                                 int C, int P) {
+  __shared__ double sh[RT / 64];
+  const long plane = blockIdx.x;
+  const int n = (int)(plane / C);
+  const float* xp = x + plane * P;
+  const float* wp = w ? w + (long)n * P : nullptr;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < P; i += RT) acc += (double)xp[i] * (wp ? wp[i] : 1.f);
+  const double t = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) out[plane] = (float)t;
+}
+
+// out[n][p] = sum_c x[n][c][p] * (v ? v[n][c] : y[n][c][p])   (64 pixels x 4 channel groups per block)
+__global__ void channel_dot_kernel(const float* __restrict__ x, const float* __restrict__ v,
+                                   const float* __restrict__ y, float* __restrict__ out, int N, int C, int P) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int tiles = (P + 63) / 64;
+  const int n = blockIdx.x / tiles;
+  const int p = (blockIdx.x % tiles) * 64 + lane;
+  double s = 0.0;
+  if (p < P) {
+    const float* xp = x + (long)n * C * P + p;
+    const float* yp = y ? y + (long)n * C * P + p : nullptr;
+    const float* vp = v ? v + (long)n * C : nullptr;
+    for (int c = grp; c < C; c += 4) s += (double)xp[(long)c * P] * (vp ? vp[c] : yp[(long)c * P]);
+  }
+  part[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && p < P) out[(long)n * P + p] = (float)(part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+}
+
+// forward row terms: rowsum = qkbar/qn + Ns; c = 1/(rowsum qn); e = 1/rowsum; (ks = 1/kn separately)
+__global__ void attn_fwd_rows_kernel(const float* __restrict__ qkbar, const float* __restrict__ qn, float* __restrict__ c,
+                                     float* __restrict__ e, long n, int Ns) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float rs = qkbar[i] / qn[i] + (float)Ns;
+  c[i] = 1.0f / (rs * qn[i]);
+  e[i] = 1.0f / rs;
+}
+
+__global__ void reciprocal_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = 1.0f / x[i];
+}
+
+// backward row terms from r = sum_v dMV MV and DA = sum_v dMV vsum:
+//   dqn = -(e/qn)(r Ns - DA);  nr = -r (epilogue offset);  cr = c r (for qtilde)
+__global__ void attn_bwd_rows_kernel(const float* __restrict__ r, const float* __restrict__ DA,
+                                     const float* __restrict__ qn, const float* __restrict__ c,
+                                     const float* __restrict__ e, float* __restrict__ dqn, float* __restrict__ nr,
+                                     float* __restrict__ cr, long n, int Ns) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dqn[i] = -(e[i] / qn[i]) * (r[i] * (float)Ns - DA[i]);
+  nr[i] = -r[i];
+  cr[i] = c[i] * r[i];
+}
+
+// X[n][v][i] = dMV[n][v][i] * c[n][i]
+__global__ void scale_cols_kernel(const float* __restrict__ x, const float* __restrict__ c, float* __restrict__ y,
+                                  int N, int R, int P) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * R * P) return;
+  const int p = (int)(idx % P);
+  const long n = idx / ((long)R * P);
+  y[idx] = x[idx] * c[n * P + p];
+}
+
+// dkn[n][j] = -ks_j^2 * sum_c K[c][j] (Y[c][j] - qt[c])
+__global__ void attn_dkn_kernel(const float* __restrict__ K, const float* __restrict__ Y, const float* __restrict__ qt,
+                                const float* __restrict__ ks, float* __restrict__ dkn, int N, int d, int Ns) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int tiles = (Ns + 63) / 64;
+  const int n = blockIdx.x / tiles;
+  const int j = (blockIdx.x % tiles) * 64 + lane;
+  double s = 0.0;
+  if (j < Ns) {
+    const float* kp = K + (long)n * d * Ns + j;
+    const float* yp = Y + (long)n * d * Ns + j;
+    const float* qp = qt + (long)n * d;
+    for (int c = grp; c < d; c += 4) s += (double)kp[(long)c * Ns] * ((double)yp[(long)c * Ns] - qp[c]);
+  }
+  part[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && j < Ns) {
+    const float k = ks[(long)n * Ns + j];
+    dkn[(long)n * Ns + j] = -(float)(part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) * k * k;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int vst_plane_dot(const float* x, const float* w, float* out, int N, int C, int P, void* stream) {
+  VST_CHECK_ARG(x && out && N > 0 && C > 0 && P > 0);
+  plane_dot_kernel<<<N * C, RT, 0, (hipStream_t)stream>>>(x, w, out, C, P);
+  return vst_launch_status();
+}
+
+int vst_channel_dot(const float* x, const float* v, const float* y, float* out, int N, int C, int P, void* stream) {
+  VST_CHECK_ARG(x && out && (v || y) && N > 0 && C > 0 && P > 0);
+  channel_dot_kernel<<<N * ceil_div(P, 64), 256, 0, (hipStream_t)stream>>>(x, v, y, out, N, C, P);
+  return vst_launch_status();
+}
+
+int vst_attn_fwd_rows(const float* qkbar, const float* qn, float* c, float* e, long n, int Ns, void* stream) {
+  VST_CHECK_ARG(qkbar && qn && c && e && n > 0 && Ns > 0);
+  attn_fwd_rows_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(qkbar, qn, c, e, n, Ns);
+  return vst_launch_status();
+}
+
+int vst_reciprocal(const float* x, float* y, long n, void* stream) {
+  VST_CHECK_ARG(x && y && n > 0);
+  reciprocal_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(x, y, n);
+  return vst_launch_status();
+}
+
+int vst_attn_bwd_rows(const float* r, const float* DA, const float* qn, const float* c, const float* e, float* dqn,
+                      float* nr, float* cr, long n, int Ns, void* stream) {
+  VST_CHECK_ARG(r && DA && qn && c && e && dqn && nr && cr && n > 0);
+  attn_bwd_rows_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(r, DA, qn, c, e, dqn, nr, cr, n, Ns);
+  return vst_launch_status();
+}
+
+int vst_scale_cols(const float* x, const float* c, float* y, int N, int R, int P, void* stream) {
+  VST_CHECK_ARG(x && c && y && N > 0 && R > 0 && P > 0);
+  scale_cols_kernel<<<ceil_div((long)N * R * P, 256), 256, 0, (hipStream_t)stream>>>(x, c, y, N, R, P);
+  return vst_launch_status();
+}
+
+int vst_attn_dkn(const float* K, const float* Y, const float* qt, const float* ks, float* dkn, int N, int d, int Ns,
+                 void* stream) {
+  VST_CHECK_ARG(K && Y && qt && ks && dkn && N > 0 && d > 0 && Ns > 0);
+  attn_dkn_kernel<<<N * ceil_div(Ns, 64), 256, 0, (hipStream_t)stream>>>(K, Y, qt, ks, dkn, N, d, Ns);
+  return vst_launch_status();
+}
+
+}  // extern "C"

@@ -45,11 +45,13 @@ struct ConvParams {
   int KH, KW, gmode, stride, pad, up;
   int pad_x;  // column padding (= pad except for the dgrad ring segments)
   int epi;
+  // EPI_AFFINE: v = (acc + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]  (ra, rd optional)
+  const float *ep_ra, *ep_rb, *ep_rd, *ep_cg;
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
-enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16 };
+enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32 };
 
 // source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
 // (select-only arithmetic: no divergent branches inside the k loop)
@@ -259,6 +261,11 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
         const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
         if (m >= P.M) continue;
         float v = acc[i][j][r];
+        if (P.epi & EPI_AFFINE) {
+          const long rm = (long)n * P.M + m;
+          v = (v + (P.ep_ra ? P.ep_ra[rm] : 0.f)) * P.ep_rb[rm] * P.ep_cg[(long)n * HWo + pp] +
+              (P.ep_rd ? P.ep_rd[rm] : 0.f);
+        }
         if (P.epi & EPI_BIAS) v += P.bias[m];
         if (P.epi & EPI_RELU) v = fmaxf(v, 0.f);
         const long o = (long)m * HWo + pp;
@@ -495,7 +502,9 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
                             int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
                             int stride, int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux,
-                            const float* gmask, void* stream) {
+                            const float* gmask, void* stream, const float* ep_ra = nullptr,
+                            const float* ep_rb = nullptr, const float* ep_rd = nullptr,
+                            const float* ep_cg = nullptr) {
   ConvParams P;
   P.src = src;
   P.wpack = wpack;
@@ -524,6 +533,10 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   P.pad_x = pad_x;
   P.up = up;
   P.epi = epi;
+  P.ep_ra = ep_ra;
+  P.ep_rb = ep_rb;
+  P.ep_rd = ep_rd;
+  P.ep_cg = ep_cg;
   P.fd_Wo = make_fastdiv(Wo);
   P.fd_Cs = make_fastdiv(Cs);
   P.fd_KW = make_fastdiv(KW);
@@ -549,6 +562,15 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
   if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad < Ws * up);
   return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad, up,
                           epi, a_batch_stride, aux, gmask, stream);
+}
+
+// out[n][m][p] = (sum_k A[n][k][m] B[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]
+// (A packed per image, a_batch_stride floats apart; B = src [N][K][P]; ra, rd may be NULL)
+int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K, int P, int M, long a_batch_stride,
+                  const float* ra, const float* rb, const float* rd, const float* cg, void* stream) {
+  VST_CHECK_ARG(src && apack && out && rb && cg && N > 0 && K > 0 && P > 0 && M > 0);
+  return conv_gemm_launch(src, apack, nullptr, nullptr, out, N, K, 1, P, M, K, 1, P, 1, 1, GM_ZERO, 1, 0, 0, 1,
+                          EPI_AFFINE, a_batch_stride, nullptr, nullptr, stream, ra, rb, rd, cg);
 }
 
 int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,

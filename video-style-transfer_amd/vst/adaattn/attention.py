@@ -12,6 +12,13 @@ backward:
   dVV2 = dMV A       conv_gemm, A = pack(dMV^T)
   dQ   = K dS^T      gemm_abt,  then + dqn/qn * Q   (cosine norms)
   dK   = Q dS        conv_gemm, A = pack(Q^T),    then + dkn/kn * K
+
+Cosine activation (the train_video path): S is never stored.  rowsum_i = (Q_i . kbar)/qn_i + Ns
+with kbar = sum_j K_j/kn_j, so A = S c_i ks_j + e_i (c = 1/(rowsum qn), e = 1/rowsum, ks = 1/kn)
+is the S GEMM's epilogue; in the backward r_i = sum_j dA_ij A_ij = sum_v dMV_vi MV_vi, so
+dS = (dA - r_i) c_i ks_j is the dA GEMM's epilogue, and the norm gradients have closed forms:
+dqn_i = -(e_i/qn_i)(r_i Ns - sum_v dMV_vi vsum_v),  dkn_j = -ks_j^2 sum_c K_cj (Y_cj - qt_c) with
+Y = Z^T [V;V^2], Z = (c . dMV) Q^T, qt = Q (c r).  Every N^2 pass is a GEMM; the rest is O(d N).
 """
 import torch
 from torch.autograd import Function
@@ -61,6 +68,37 @@ def gemm_abt(a, b, scale=1.0):
     return out
 
 
+def _vec(shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None):
+    """out[n][m][p] = (sum_k x[n][k][m] b[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]."""
+    N = b.shape[0]
+    ap, abs_ = packed_matrix(x, M, K, False)
+    out = _empty((N, M, P), b)
+    from .. import kprof
+
+    tok = kprof.begin(2.0 * N * M * P * K, 4.0 * (b.numel() + ap.numel() + out.numel()), ("attn", N, M, K, P))
+    lib.vst_attn_gemm(ptr(b), ptr(ap), ptr(out), N, K, P, M, abs_, ptr(ra), ptr(rb), ptr(rd), ptr(cg), stream())
+    kprof.end(tok)
+    return out
+
+
+def plane_dot(x, w=None):
+    N, C, P = x.shape
+    out = _vec((N, C), x)
+    lib.vst_plane_dot(ptr(x), ptr(w), ptr(out), N, C, P, stream())
+    return out
+
+
+def channel_dot(x, v=None, y=None):
+    N, C, P = x.shape
+    out = _vec((N, P), x)
+    lib.vst_channel_dot(ptr(x), ptr(v), ptr(y), ptr(out), N, C, P, stream())
+    return out
+
+
 def channel_norm(x):
     """||x[n][:][p]||_2 over channels -> [N][P] (LA.vector_norm, AA/network.py:121-122)."""
     N, C, P = x.shape
@@ -96,11 +134,19 @@ class AdaAttnFn(Function):
             raise VstError(f"adaattn: Q{tuple(Q.shape)} K{tuple(K.shape)} V{tuple(V.shape)} c{tuple(cn.shape)}")
         Q, K, V, cn = (ops._check(t, "adaattn operand", 4) for t in (Q, K, V, cn))
         Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
-        qn = kn = None
+        qn = kn = S = rowsum = None
         if activation == COSINE:
             qn, kn = channel_norm(Qm), channel_norm(Km)
-        S = bmm_at_b(Qm, Nc, d, False, Km, Ns)  # [N][Nc][Ns]
-        A, rowsum = attention_rows(S, activation, qn, kn)
+            ks = _vec((N, Ns), Q)
+            lib.vst_reciprocal(ptr(kn), ptr(ks), N * Ns, stream())
+            qkbar = channel_dot(Qm, v=plane_dot(Km, ks))
+            c, e = _vec((N, Nc), Q), _vec((N, Nc), Q)
+            lib.vst_attn_fwd_rows(ptr(qkbar), ptr(qn), ptr(c), ptr(e), N * Nc, Ns, stream())
+            A = attn_gemm(Qm, Nc, d, Km, Ns, rb=c, cg=ks, rd=e)  # [N][Nc][Ns], S never stored
+            rowsum = (ks, c, e)
+        else:
+            S = bmm_at_b(Qm, Nc, d, False, Km, Ns)  # [N][Nc][Ns]
+            A, _ = attention_rows(S, activation)
         VV2 = _empty((N, 2 * dv, Ns), V)
         lib.vst_square_concat(ptr(V), ptr(VV2), N, dv * Ns, stream())
         MV = gemm_abt(VV2, A)  # [N][2dv][Nc]
@@ -109,12 +155,13 @@ class AdaAttnFn(Function):
         ctx.activation = activation
         ctx.dims = (N, d, dv, Nc, Ns)
         if any(ctx.needs_input_grad[:3]):
-            ctx.save_for_backward(Q, K, V, cn, qn, kn, S, A, rowsum, VV2, MV)
+            extra = rowsum if rowsum is not None else (None, None, None)
+            ctx.save_for_backward(Q, K, V, cn, qn, kn, S, A, VV2, MV, *extra)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        Q, K, V, cn, qn, kn, S, A, rowsum, VV2, MV = ctx.saved_tensors
+        Q, K, V, cn, qn, kn, S, A, VV2, MV, ks, c, e = ctx.saved_tensors
         N, d, dv, Nc, Ns = ctx.dims
         dout = dout.contiguous()
         dMV = _empty(MV.shape, MV)
@@ -126,19 +173,17 @@ class AdaAttnFn(Function):
             lib.vst_square_concat_bwd(ptr(dVV2), ptr(V), ptr(dV), N, dv * Ns, stream())
             del dVV2
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            dA = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns)  # [N][Nc][Ns]
             Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
             if ctx.activation == COSINE:
-                dS = _empty(S.shape, S)
-                dqn = _empty((N, Nc), S)
-                dkn = _empty((N, Ns), S)
-                part = _empty((N * ((Nc + 63) // 64) * Ns,), S)
-                lib.vst_cos_attn_rows_bwd(ptr(dA), ptr(A), ptr(S), ptr(qn), ptr(kn), ptr(rowsum), ptr(dS), ptr(dqn),
-                                          ptr(dkn), ptr(part), N, Nc, Ns, stream())
-                del dA, part
+                r = channel_dot(dMV, y=MV)                 # sum_j dA_ij A_ij
+                DA = channel_dot(dMV, v=plane_dot(VV2))    # sum_j dA_ij
+                dqn, nr, cr = _vec((N, Nc), Q), _vec((N, Nc), Q), _vec((N, Nc), Q)
+                lib.vst_attn_bwd_rows(ptr(r), ptr(DA), ptr(qn), ptr(c), ptr(e), ptr(dqn), ptr(nr), ptr(cr), N * Nc, Ns,
+                                      stream())
+                dS = attn_gemm(dMV, Nc, 2 * dv, VV2, Ns, rb=c, cg=ks, ra=nr)  # (dA - r) c ks, dA never stored
             else:
-                dS = dA
-                lib.vst_softmax_rows_bwd(ptr(dA), ptr(A), ptr(dS), N * Nc, Ns, stream())
+                dS = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns)  # dA
+                lib.vst_softmax_rows_bwd(ptr(dS), ptr(A), ptr(dS), N * Nc, Ns, stream())
             if ctx.needs_input_grad[0]:
                 dQ = gemm_abt(Km, dS)  # [N][d][Nc]
                 if ctx.activation == COSINE:
@@ -147,6 +192,12 @@ class AdaAttnFn(Function):
             if ctx.needs_input_grad[1]:
                 dK = bmm_at_b(Qm, d, Nc, True, dS, Ns)  # [N][d][Ns]
                 if ctx.activation == COSINE:
+                    dMVc = _empty(dMV.shape, dMV)
+                    lib.vst_scale_cols(ptr(dMV), ptr(c), ptr(dMVc), N, 2 * dv, Nc, stream())
+                    Z = gemm_abt(dMVc, Qm)  # [N][2dv][d]
+                    Y = bmm_at_b(Z, d, 2 * dv, False, VV2, Ns)  # [N][d][Ns]
+                    dkn = _vec((N, Ns), K)
+                    lib.vst_attn_dkn(ptr(Km), ptr(Y), ptr(plane_dot(Qm, cr)), ptr(ks), ptr(dkn), N, d, Ns, stream())
                     lib.vst_norm_grad_add(ptr(dK), ptr(dkn), ptr(kn), ptr(Km), N, d, Ns, stream())
                 dK = dK.view(K.shape)
         if ctx.needs_input_grad[3]:
