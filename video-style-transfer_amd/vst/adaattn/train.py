@@ -8,7 +8,10 @@ Per step, exactly the reference loop body:
   loss_is = LAMBDA_IS * sum_{relu2_1..relu4_1} image_similarity_loss(fc1, fc2, fcs1, fcs2)
   backward, Adam(lr=1e-4).
 The loss weights are folded into the loss kernels' reductions.  The three data encodings run as
-one VGG19 pass of 3B when the inputs are handed over as one [3, B, 3, H, W] buffer.
+one VGG19 pass of 3B when the inputs are handed over as one [3, B, 3, H, W] buffer, and the two
+stylisations (and the VGG19 passes of their outputs) as one batch of 2B: every op on the path is
+per sample (InstanceNorm, attention per image), so this is the reference's two passes fused into
+larger GEMMs.
 
 Multi-GPU: one process per GPU, (content1, content2, style) triples sharded across ranks, one
 RCCL all-reduce of the flat gradient per step; Adam applies the 1/world average.  Every loss term
@@ -16,6 +19,7 @@ is a per-rank mean or per-rank sum exactly as the reference computes it on its o
 """
 import torch
 
+from .. import ops
 from ..reconet._flat import FlatParams
 from ..reconet.dist import allreduce_grads, world_info
 from .lossfn import global_stylized_loss, image_similarity_loss, local_feature_loss
@@ -24,6 +28,28 @@ from .utilities import feature_down_sample
 from .vgg19 import FEATURES
 
 LOSS_WEIGHTS = dict(LAMBDA_G=10.0, LAMBDA_L=3.0, LAMBDA_IS=100.0)
+
+
+def _batch_pair(a, b):
+    """{k: a[k] ++ b[k]} along the batch; a free view when b[k] directly follows a[k] in memory
+    (the 3B encoding buffer), a copy otherwise."""
+    out = {}
+    for k, x in a.items():
+        y = b[k]
+        if (x.is_contiguous() and y.is_contiguous() and y.data_ptr() == x.data_ptr() + x.numel() * x.element_size()
+                and x.untyped_storage().data_ptr() == y.untyped_storage().data_ptr()):
+            out[k] = torch.as_strided(x, (x.shape[0] + y.shape[0],) + tuple(x.shape[1:]), x.stride())
+        else:
+            out[k] = _cat2(x, y)
+    return out
+
+
+def _cat2(x, y):
+    """x ++ y along the batch with the library's plane-copy kernel."""
+    out = torch.empty((x.shape[0] + y.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=torch.float32)
+    ops.copy_into(x.contiguous(), out[:x.shape[0]])
+    ops.copy_into(y.contiguous(), out[x.shape[0]:])
+    return out
 
 
 class AdaAttNTrainer:
@@ -53,10 +79,12 @@ class AdaAttNTrainer:
     def losses(self, c1, c2=None, s=None):
         w = self.w
         fc1, fc2, fs = self.encode(c1, c2, s)
-        cs1 = self.model(fc1, fs)
-        cs2 = self.model(fc2, fs)
-        fcs1 = self.vgg(cs1)
-        fcs2 = self.vgg(cs2)
+        B = next(iter(fc1.values())).shape[0]
+        fc12 = _batch_pair(fc1, fc2)
+        fs2 = {k: _cat2(v, v) for k, v in fs.items()}
+        fcs = self.vgg(self.model(fc12, fs2))  # cs1 ++ cs2
+        fcs1 = {k: v[:B] for k, v in fcs.items()}
+        fcs2 = {k: v[B:] for k, v in fcs.items()}
         gs = None
         for k in FEATURES[1:]:
             t = global_stylized_loss(fcs1[k], fs[k], weight=w["LAMBDA_G"])
