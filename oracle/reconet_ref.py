@@ -252,15 +252,23 @@ def style_grams(VP, style):
     return [gram_matrix(f) for f in vgg_forward(VP, vgg_normalize_(style.clone()), VGG16_PLAN)]
 
 
-def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, temporal=True):
-    """Loss terms of one `train_candy` step (RC/train_single/train_candy.py:77-148).
-    Returns dict(loss, CL, SL, FTL, OTL, RL) as 0-d tensors (autograd-connected to P)."""
-    _, fmap1, s1 = reconet_forward(P, img1)
-    _, fmap2, s2 = reconet_forward(P, img2)
+def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, temporal=True, forward=None, teacher=None):
+    """Loss terms of one `train_candy` step (RC/train_single/train_candy.py:77-148), or of the
+    distillation trainers (RC/train_single/train_Flow_SD{1,2}.py:80-160) with
+    `forward` = the student's forward and `teacher` = (TP, teacher_forward, t_idx, s_idx): the
+    symmetric distillation term SDL = 0.01*BETA*(mse(t1, s1) + mse(t2, s2)) is computed and
+    reported but, as in the reference, not added to the total.
+    Returns dict(loss, CL, SL, FTL, OTL, RL[, SDL]) as 0-d tensors (autograd-connected to P)."""
+    forward = reconet_forward if forward is None else forward
+    o1 = forward(P, img1)
+    o2 = forward(P, img2)
+    fmap1, s1 = o1[-2], o1[-1]
+    fmap2, s2 = o2[-2], o2[-1]
     s1 = vgg_normalize_(s1)
     s2 = vgg_normalize_(s2)
-    i1 = vgg_normalize_(img1[:, [0, 1, 2]])
-    i2 = vgg_normalize_(img2[:, [0, 1, 2]])
+    idx = list(range(img1.shape[1] - 3, img1.shape[1]))  # the last frame's channels (`index`)
+    i1 = vgg_normalize_(img1[:, idx])
+    i2 = vgg_normalize_(img2[:, idx])
     sf1 = vgg_forward(VP, s1, VGG16_PLAN)
     sf2 = vgg_forward(VP, s2, VGG16_PLAN)
     cf1 = vgg_forward(VP, i1, VGG16_PLAN)
@@ -289,6 +297,11 @@ def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, tempora
            + (s2[:, :, :-1, 1:] - s2[:, :, :-1, :-1]) ** 2 + (s2[:, :, 1:, :-1] - s2[:, :, :-1, :-1]) ** 2)
     out["RL"] = w["GAMMA"] * torch.sum(reg)
     out["loss"] = sum(out[k] for k in ("FTL", "OTL", "CL", "SL", "RL") if k in out)
+    if teacher is not None:
+        TP, tfwd, ti, si = teacher
+        with torch.no_grad():
+            t1, t2 = tfwd(TP, img1)[ti], tfwd(TP, img2)[ti]
+        out["SDL"] = (F.mse_loss(t1, o1[si]) + F.mse_loss(t2, o2[si])) * (0.01 * w["BETA"])
     return out
 
 

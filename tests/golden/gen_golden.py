@@ -238,6 +238,89 @@ def gen_reconet():
 
 
 # --------------------------------------------------------------------------------------------
+# ReCoNet distillation trainers (RC/train_single/train_Flow_SD{1,2}.py)
+# --------------------------------------------------------------------------------------------
+def gen_sd():
+    _fresh_project(RC_DIR)
+    rc_util = _load("utilities", os.path.join(RC_DIR, "utilities.py"))
+    sys.modules["utilities"] = rc_util
+    rc_net = _load("network", os.path.join(RC_DIR, "network.py"))
+    sys.modules["network"] = rc_net
+    step, notes = {}, []
+    for tag, script, tcls, scls, (B, H, W, seeds) in (
+            ("sd2", "train_Flow_SD2.py", rc_net.ReCoNetSD1, rc_net.ReCoNetSD2, (2, 32, 64, (51, 52, 53, 54, 55))),
+            ("sd1", "train_Flow_SD1.py", rc_net.ReCoNet, rc_net.ReCoNetSD1, (2, 32, 64, (61, 62, 63, 64, 65)))):
+        # seeds: teacher, student, vgg, data, style
+        fake_ds = types.ModuleType("datasets")
+        fake_ds.FlyingThings3D_Monkaa = lambda *a, **k: None
+        style = style_image(seeds[4], H, W)
+        fake_ds.toTensor255 = lambda _img, _s=style: _s[0].clone()
+        sys.modules["datasets"] = fake_ds
+        tr = _load(f"rc_train_{tag}", os.path.join(RC_DIR, "train_single", script))
+        img1, img2, flow, mask = frame_pair_batch(seeds[3], B, H, W, mask_fn=rc_util.flow_warp_mask)
+        teacher_sd = {}
+        t0 = tcls()
+        seed_module(t0, seeds[0])
+        teacher_sd.update({k: v.clone() for k, v in t0.state_dict().items()})
+
+        def teacher_factory(n=1, _c=tcls):
+            return _c(n)
+
+        def student_factory(n=1, _c=scls, _s=seeds[1]):
+            net = _c(n)
+            seed_module(net, _s)
+            tr.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(net.named_parameters())))
+            return net
+
+        def vgg_factory(device="cpu", _s=seeds[2]):
+            v = rc_net.Vgg16(device)
+            seed_module(v, _s)
+            return v
+
+        class _Img:
+            BILINEAR = 2
+
+            @staticmethod
+            def open(_p):
+                class _O:
+                    def convert(self, *_):
+                        return self
+
+                    def resize(self, *_):
+                        return self
+
+                return _O()
+
+        tr.device, tr.batch_size, tr.IMG_SIZE, tr.epoch_start, tr.epoch_end = "cpu", B, (W, H), 1, 1
+        tr.DataLoader = lambda *a, **k: [(img1.clone(), img2.clone(), flow.clone(), mask.clone())]
+        setattr(tr, tcls.__name__, teacher_factory)
+        setattr(tr, scls.__name__, student_factory)
+        tr.Vgg16, tr.Image, tr.tqdm = vgg_factory, _Img, _TqdmRecorder
+        _TqdmRecorder.records = []
+        save, load = torch.save, torch.load
+        torch.save = lambda *a, **k: None
+        torch.load = lambda *a, **k: {k2: v.clone() for k2, v in teacher_sd.items()}
+        try:
+            tr.train()
+        except RuntimeError as e:  # the reference's own failure, recorded as a fact
+            notes.append(f"{script}: {str(e).splitlines()[0]}")
+            continue
+        finally:
+            torch.save, torch.load = save, load
+        rec = _TqdmRecorder.records[-1]
+        step[f"{tag}_img1"], step[f"{tag}_img2"] = _np(img1), _np(img2)
+        step[f"{tag}_flow"], step[f"{tag}_mask"], step[f"{tag}_style"] = _np(flow), _np(mask), _np(style)
+        step[f"{tag}_seeds"] = np.array(seeds)
+        for k in ("loss", "CL", "SL", "FTL", "OTL", "RL", "SDL"):
+            step[f"{tag}_{k}"] = np.array(rec[k], dtype=np.float64)
+        adam = tr.optim.Adam
+        _grad_summary(f"{tag}_", adam.grads, adam.after, step, seed=seeds[1] + 1000)
+    step["notes"] = np.array(notes)
+    np.savez_compressed(os.path.join(HERE, "sd_step.npz"), **step)
+    print("distillation fixtures written;", notes)
+
+
+# --------------------------------------------------------------------------------------------
 # AdaAttN (AA/)
 # --------------------------------------------------------------------------------------------
 def gen_adaattn():
@@ -332,8 +415,10 @@ def gen_adaattn():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["reconet", "adaattn"]
+    which = sys.argv[1:] or ["reconet", "adaattn", "sd"]
     if "reconet" in which:
         gen_reconet()
     if "adaattn" in which:
         gen_adaattn()
+    if "sd" in which:
+        gen_sd()

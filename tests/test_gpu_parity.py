@@ -320,3 +320,33 @@ def test_train_step_golden(golden, tag):
         sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
         got = C(named[n]).reshape(-1)[:64].numpy()
         assert np.abs(got - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
+
+
+def test_sd2_distillation_step_golden(golden):
+    """One train_Flow_SD2 step (student ReCoNetSD2, teacher ReCoNetSD1) vs the reference's own train()."""
+    from vst.reconet import network as N
+    from vst.reconet.train import SD_LOSS_WEIGHTS, ReCoNetTrainer
+
+    s = golden("sd_step")
+    seeds = s["sd2_seeds"]
+    teacher = _seeded(N.ReCoNetSD1(), shapes.reconet_sd1(), int(seeds[0]))
+    student = _seeded(N.ReCoNetSD2(), shapes.reconet_sd2(), int(seeds[1]))
+    student.load_state_dict(teacher.state_dict(), strict=False)  # train_Flow_SD2.py:45
+    teacher, student = teacher.to(DEV).eval(), student.to(DEV)
+    vgg = _seeded(N.Vgg16(), shapes.vgg16(), int(seeds[2])).to(DEV)
+    tr = ReCoNetTrainer(student, vgg, G(s["sd2_style"]), weights=SD_LOSS_WEIGHTS, teacher=teacher, sd_index=(0, 0))
+    frames = torch.stack([G(s["sd2_img1"]), G(s["sd2_img2"])])
+    tr.flat.zero_grad()
+    out = tr.losses(frames, G(s["sd2_flow"]), G(s["sd2_mask"]))
+    for k in ("loss", "CL", "SL", "FTL", "OTL", "RL", "SDL"):
+        assert rel_err(out[k].item(), s[f"sd2_{k}"]) < 1e-3, k
+    out["loss"].backward()
+    names = list(s["sd2_names"])
+    named = dict(student.named_parameters())
+    gmax = max(float(s[f"sd2_gnorm/{n}"]) for n in names)
+    for n in names:
+        gr = C(named[n].grad).reshape(-1)
+        gn = float(s[f"sd2_gnorm/{n}"])
+        assert abs(float(gr.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"sd2_gidx/{n}"]
+        assert np.abs(gr[idx].numpy() - s[f"sd2_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n

@@ -146,3 +146,41 @@ def test_adaattn_train_step(golden):
         assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
         idx = s[f"gidx/{n}"]
         assert np.abs(g.reshape(-1)[idx].numpy() - s[f"gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+
+
+# ----------------------------------------------------------------------------- distillation (SD2)
+SD_WEIGHTS = dict(ALPHA=1e5, BETA=1e10, GAMMA=1e-2, LAMBDA_F=1e11, LAMBDA_O=1e7)  # train_Flow_SD2.py:24-29
+
+
+def sd2_params(seeds, requires_grad=False):
+    """Teacher ReCoNetSD1 and student ReCoNetSD2 as train_Flow_SD2.py:42-45 builds them: the student's
+    res*_sd blocks come from the teacher checkpoint (load_state_dict(strict=False))."""
+    TP = oracle.seeded_params(shapes.reconet_sd1(), int(seeds[0]))
+    P = oracle.seeded_params(shapes.reconet_sd2(), int(seeds[1]))
+    for k in P:
+        if k in TP:
+            P[k] = TP[k].clone()
+    for v in P.values():
+        v.requires_grad_(requires_grad)
+    return TP, P
+
+
+def test_sd2_train_step(golden):
+    s = golden("sd_step")
+    assert any("train_Flow_SD1.py" in str(n) for n in s["notes"])  # the reference's SD1 trainer cannot load
+    seeds = s["sd2_seeds"]
+    TP, P = sd2_params(seeds, requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg16(), int(seeds[2]))
+    grams = R.style_grams(VP, T(s["sd2_style"]))
+    L = R.reconet_losses(P, VP, T(s["sd2_img1"]).clone(), T(s["sd2_img2"]).clone(), T(s["sd2_flow"]),
+                         T(s["sd2_mask"]), grams, w=SD_WEIGHTS, forward=R.reconet_sd2_forward,
+                         teacher=(TP, R.reconet_sd1_forward, 0, 0))
+    for k in ("loss", "CL", "SL", "FTL", "OTL", "RL", "SDL"):
+        assert rel_err(L[k].item(), s[f"sd2_{k}"]) < 1e-3, k
+    L["loss"].backward()
+    names = list(s["sd2_names"])
+    gmax = max(float(s[f"sd2_gnorm/{n}"]) for n in names)
+    for n in names:
+        g = P[n].grad
+        gn = float(s[f"sd2_gnorm/{n}"])
+        assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n

@@ -24,12 +24,20 @@ from ._flat import FlatParams
 from .dist import allreduce_grads, world_info
 
 LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
+# RC/train_single/train_Flow_SD{1,2}.py:24-29
+SD_LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=1e10, GAMMA=1e-2, LAMBDA_F=1e11, LAMBDA_O=1e7)
 
 
 class ReCoNetTrainer:
     def __init__(self, model, vgg, style, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weights=None, temporal=True,
-                 process_group=None):
+                 process_group=None, teacher=None, sd_index=(0, 0)):
+        """model: ReCoNet / ReCoNetSD1 / ReCoNetSD2 (feature map and styled image are its last two
+        outputs).  teacher + sd_index=(teacher output, student output): the distillation trainers
+        (train_Flow_SD{1,2}.py), whose symmetric distillation term SDL is reported but, as in the
+        reference, not part of the optimised loss."""
         self.model = model
+        self.teacher = teacher
+        self.sd_index = sd_index
         self.vgg = vgg
         self.w = dict(LOSS_WEIGHTS if weights is None else weights)
         self.temporal = temporal
@@ -55,7 +63,8 @@ class ReCoNetTrainer:
         w = self.w
         _, B, C, H, W = frames.shape
         x = frames.reshape(2 * B, C, H, W)
-        _, fmap, styled = self.model(x)
+        mout = self.model(x)
+        fmap, styled = mout[-2], mout[-1]
         s_n = ops.VggNormalizeFn.apply(styled)
         with torch.no_grad():
             i_n = ops.VggNormalizeFn.apply(x if C == 3 else x[:, C - 3:].contiguous())
@@ -85,6 +94,11 @@ class ReCoNetTrainer:
             if k in out:
                 total = out[k] if total is None else total + out[k]
         out["loss"] = total
+        if self.teacher is not None:
+            ti, si = self.sd_index
+            with torch.no_grad():
+                # mean over the 2B batch = (mse(t1, s1) + mse(t2, s2)) / 2
+                out["SDL"] = ops.mse(self.teacher(x)[ti], mout[si].detach(), 2.0 * 0.01 * w["BETA"])
         return out
 
     def step(self, frames, flow, mask):
