@@ -82,6 +82,15 @@ __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox
   return ok ? (y >> sh) * P.Ws + (x >> sh) : -1;
 }
 
+// float4 slot (row*4 + quad) of A-tile element idx: 8 consecutive lanes take 8 consecutive rows of
+// one quad, so each 8-lane ds_write_b128 group hits 8 distinct 4-bank slots (rows are 20 dwords
+// apart; bank = dword mod 32) -- the plain row-major order put rows r and r+1's quads 0 and 3 on
+// the same banks (2-way conflict on every A store).  The wave still covers whole 64-B rows.
+__device__ __forceinline__ int a_slot(int idx) {
+  const int row = (idx & 7) | ((idx >> 5) << 3), quad = (idx >> 3) & 3;
+  return row * 4 + quad;
+}
+
 template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW>
 __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   constexpr int BM = WM * TM * 32;
@@ -150,7 +159,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
-        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * 16 + 4 * idx);
+        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * 16 + 4 * a_slot(idx));
       }
     }
     if (CFAST) {
@@ -196,7 +205,8 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
-        *reinterpret_cast<f32x4*>(&As[buf][idx >> 2][(idx & 3) * 4]) = ra[i];
+        const int sl = a_slot(idx);
+        *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
       }
     }
     float bv[B_PER];

@@ -19,6 +19,7 @@ static inline int vst_launch_status() {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Unsigned division by a runtime constant (Granlund-Montgomery, 32-bit): n / d == umulhi(n, mul) >> shift
 // valid for n < 2^31.

@@ -152,10 +152,8 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
         if (A_F4 % NT == 0 || idx < A_F4) {
           const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> (s, hi) = (2q,0),(2q,1),(2q+1,0),(2q+1,1)
           float* row = &As[buf][m][0];
-          row[2 * q] = rav[i][0];
-          row[2 * q + 1] = rav[i][2];
-          row[8 + 2 * q] = rav[i][1];
-          row[8 + 2 * q + 1] = rav[i][3];
+          *reinterpret_cast<f32x2*>(&row[2 * q]) = f32x2{rav[i][0], rav[i][2]};
+          *reinterpret_cast<f32x2*>(&row[8 + 2 * q]) = f32x2{rav[i][1], rav[i][3]};
         }
       }
     } else {
@@ -272,7 +270,7 @@ static void launch_wg_t(int c, dim3 g, hipStream_t st, const WgParams& P) {
     case W32: wgrad_kernel<1, 1, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
     case W64: wgrad_kernel<1, 2, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
     case W96: wgrad_kernel<1, 3, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad_kernel<2, 2, 2, 2, AV, 4><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad_kernel<2, 2, 2, 2, AV, 3><<<g, NT, 0, st>>>(P); break;  // 4 per CU spills (128-VGPR cap)
     default: wgrad_kernel<2, 3, 2, 2, AV, 2><<<g, NT, 0, st>>>(P); break;
   }
 }
@@ -287,13 +285,33 @@ static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
     launch_wg_t<false>(c, g, st, P);
 }
 
-static int plan_splits(long tiles, int N, int HWo) {
-  // aim for ~1024 workgroups; at least 2 k-tiles per split
-  long want = 1024 / (tiles * N);
-  if (want < 1) want = 1;
-  long maxs = (HWo + 2 * BK - 1) / (2 * BK);
-  if (want > maxs) want = maxs;
-  return (int)(want < 1 ? 1 : want);
+static int wminw(int c) {  // resident blocks per CU of each configuration (its launch bound)
+  return c == W192 ? 2 : (c == W128 ? 3 : 4);
+}
+
+// Split-K count: minimise (waves of blocks) x (k-tiles per block + fixed cost) plus the slab
+// reduction traffic, i.e. fill the 256 CUs evenly without over-splitting.
+static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) {
+  const long slots = 256L * wminw(c);
+  const long ktiles = (HWo + BK - 1) / BK;
+  const double t_tile = wminw(c) * 2.0 * wbm(c) * WBN * BK / 0.44e12;  // s per k-tile per block
+  long maxs = (HWo + 2 * BK - 1) / (2 * BK);                        // >= 2 k-tiles per split
+  if (maxs > 64) maxs = 64;
+  if (maxs < 1) maxs = 1;
+  int best = 1;
+  double best_t = 1e30;
+  for (int S = 1; S <= maxs; ++S) {
+    const long blocks = tiles * N * S;
+    const long waves = (blocks + slots - 1) / slots;
+    const long kt = ((HWo + S - 1) / S + BK - 1) / BK;
+    const double t = waves * (kt + 4) * t_tile + (double)N * S * Mpad * Jpad * 8.0 / 4e12;
+    if (t < best_t * 0.995) {
+      best_t = t;
+      best = S;
+    }
+  }
+  (void)ktiles;
+  return best;
 }
 
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
@@ -335,7 +353,7 @@ static int splits_for(int N, int M, long J, int HWo) {
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
   long Jpad = (J + WBN - 1) / WBN * WBN;
-  return plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo);
+  return plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo, c, Mpad, Jpad);
 }
 
 }  // namespace
