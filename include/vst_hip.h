@@ -28,8 +28,17 @@ extern "C" {
 /* ---- library ------------------------------------------------------------------------------ */
 int vst_version(void);
 const char* vst_strerror(int code);
+/* GEMM arithmetic of every conv / Gram / attention product (library-global; packed weight
+ * operands are written in the layout of the mode current at pack time):
+ *   0  exact fp32 MFMA (v_mfma_f32_32x32x2_f32);
+ *   1  bf16x3 (default): fp32 operands split into hi + lo bf16, hi*hi + hi*lo + lo*hi on
+ *      v_mfma_f32_32x32x16_bf16 with fp32 accumulation (per-product error <= ~2^-16 relative);
+ *   2  bf16: hi*hi only (reduced precision, BASELINE config 5's half-precision MFMA path).
+ * The initial mode comes from the environment variable VST_GEMM_MODE (f32 | bf16x3 | bf16). */
+int vst_set_gemm_mode(int mode);
+int vst_get_gemm_mode(void);
 
-/* ---- convolution (implicit GEMM on v_mfma_f32_32x32x2_f32) --------------------------------
+/* ---- convolution (implicit GEMM on MFMA, arithmetic per vst_set_gemm_mode) ----------------
  * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv
  * (RC/network.py:114-120), torchvision VGG Conv2d(3x3, pad 1) + ReLU (RC/network.py:12-24),
  * and their autograd backward (dgrad / wgrad), the conv1 bias add and ConvTanh's

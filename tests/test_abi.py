@@ -14,7 +14,8 @@ def test_header_parses_and_lists_entry_points():
                  # AdaAttN path
                  "vst_gemm_abt", "vst_pack_matrix", "vst_channel_norm", "vst_cos_attn_rows", "vst_cos_attn_rows_bwd",
                  "vst_softmax_rows", "vst_softmax_rows_bwd", "vst_adaattn_out", "vst_adaattn_out_bwd",
-                 "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_copy_planes"):
+                 "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_copy_planes",
+                 "vst_set_gemm_mode", "vst_get_gemm_mode"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"
     assert len(protos["vst_conv_gemm"][1]) == 24
@@ -42,6 +43,12 @@ def test_host_side_argument_validation_without_gpu():
     assert lib.vst_conv_pack_dims(192, 1728, ctypes.byref(mp), ctypes.byref(kp)) == 0
     assert (mp.value, kp.value) == (192, 1728)
     assert lib.vst_wgrad_workspace(16, 192, 1728, 8192) > 0
+    # GEMM arithmetic mode: host-side state, validated, default bf16x3 unless VST_GEMM_MODE says otherwise
+    mode = lib.vst_get_gemm_mode()
+    assert mode in (0, 1, 2)
+    assert lib.vst_set_gemm_mode(7) == -1 and lib.vst_get_gemm_mode() == mode
+    assert lib.vst_set_gemm_mode(0) == 0 and lib.vst_get_gemm_mode() == 0
+    assert lib.vst_set_gemm_mode(mode) == 0
 
 
 def test_product_fails_loudly_without_hip_tensors():

@@ -25,7 +25,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
 
 // packed GEMM A operand from a row-major matrix per batch: X[k][m] (transpose=0) or X[m][k]
 __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restrict__ out, int B, int M, int K,
-                                   int transpose, int Mpad, int Kpad, long x_bs) {
+                                   int transpose, int Mpad, int Kpad, long x_bs, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long per = (long)Mpad * Kpad;
   if (idx >= B * per) return;
@@ -34,7 +34,7 @@ __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restric
   int m = (int)(t % Mpad), k = (int)(t / Mpad);
   float v = 0.f;
   if (m < M && k < K) v = transpose ? x[b * x_bs + (long)m * K + k] : x[b * x_bs + (long)k * M + m];
-  out[b * per + apack_index(k, m, Mpad)] = v;
+  apack_store(out + b * per, k, m, Mpad, v, bsplit);
 }
 
 // out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
@@ -332,8 +332,8 @@ int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int tran
                     void* stream) {
   VST_CHECK_ARG(x && packed && B > 0 && M > 0 && K > 0 && Mpad >= M && Kpad >= K);
   long total = (long)B * Mpad * Kpad;
-  pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, packed, B, M, K, transpose, Mpad, Kpad,
-                                                                            x_bs);
+  pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+      x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, vst_gemm_mode_internal() != VST_GEMM_F32);
   return vst_launch_status();
 }
 

@@ -14,6 +14,9 @@
 // Tile: 4 waves (256 threads); each wave owns TM x TN 32x32 accumulators (WM x WN waves).
 // LDS: A[BK][BM] and B[BK][BN], double buffered; global->register prefetch of tile t+1 overlaps
 // the MFMAs of tile t; one barrier per k-tile.
+#include <cstdlib>
+#include <cstring>
+
 #include "vst_common.h"
 #include "vst_hip.h"
 
@@ -91,7 +94,7 @@ __device__ __forceinline__ int a_slot(int idx) {
   return row * 4 + quad;
 }
 
-template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW>
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC>
 __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -100,6 +103,10 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   constexpr int ROWSTEP = NT / BN;           // B rows covered per pass
   constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
   constexpr int KSTEPS = BK / 2;
+  // k rows of this thread's B elements: fp32 MFMA (32x32x2: lane half h takes k = 2s + h) ->
+  // k = brow0 + ROWSTEP*i; bf16 MFMA (32x32x16: lane half h takes k = 8h..8h+7) -> contiguous
+  // k = brow0*B_PER + i, so each thread packs its own bf16 pairs
+  constexpr int KSTEP = PREC ? 1 : ROWSTEP;
   static_assert(NT % BN == 0 && BK % ROWSTEP == 0, "tile");
 
   static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
@@ -111,9 +118,14 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   const int lane = tid & 63, wave = tid >> 6;
   const int lo = lane & 31, hi = lane >> 5;
   const int wm = wave / WN, wn = wave % WN;
-  const int n = blockIdx.z;
-  const int m0 = blockIdx.y * BM;
-  const int p0 = blockIdx.x * BN;
+  // XCD-aware work order: M tile fastest, then pixel tile, then image, so the blocks that share a
+  // source panel (and its halo rows) run on one XCD's L2
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int rest = wk / gy;
+  const int n = rest / gx;
+  const int m0 = (wk - rest * gy) * BM;
+  const int p0 = (rest - n * gx) * BN;
   const int HWo = P.Ho * P.Wo;
   const long plane = (long)P.Hs * P.Ws;
   const float* src_n = P.src + (long)n * P.Cs * plane;
@@ -123,6 +135,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   // this thread's B column (fixed for the whole k loop)
   const int bcol = tid % BN;
   const int brow0 = tid / BN;
+  const int krow0 = PREC ? brow0 * B_PER : brow0;
   const int p = p0 + bcol;
   const bool pvalid = p < HWo;
   int oy = 0, ox = 0;
@@ -175,8 +188,8 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
         const int kh = tap / P.KW, kw = tap - (tap / P.KW) * P.KW;
         const int off0 = gather_offset(P, oy, ox, kh, kw);
         const bool ok = pvalid && kg < P.K && off0 >= 0;
-        const int vo = ok ? ((c0 + brow0) * plane_i + off0) * 4 : OOR;
-        const int vstep = ok ? ROWSTEP * plane_i * 4 : 0;
+        const int vo = ok ? ((c0 + (PREC ? brow0 * PER_G : brow0)) * plane_i + off0) * 4 : OOR;
+        const int vstep = ok ? KSTEP * plane_i * 4 : 0;
 #pragma unroll
         for (int i = 0; i < PER_G; ++i) {
           rb[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     } else {
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        const int k = k0 + brow0 + i * ROWSTEP;
+        const int k = k0 + krow0 + i * KSTEP;
         const int kc = k < P.K ? k : 0;
         const int tap = (int)fdiv((uint32_t)kc, P.fd_Cs);
         const int c = kc - tap * P.Cs;
@@ -212,7 +225,23 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     float bv[B_PER];
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) bv[i] = GM ? (rg[i] > 0.f ? rb[i] : 0.f) : rb[i];
-    if (ROWSTEP == 2) {  // rows k = brow0 + 2i: hi = brow0, s = i -> 8 contiguous floats
+    if constexpr (PREC != 0) {  // bf16 row: [hi k0..15][lo k0..15], this thread's k contiguous
+      uint32_t h[B_PER / 2], l[B_PER / 2];
+#pragma unroll
+      for (int q = 0; q < B_PER / 2; ++q) split_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
+      if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
+        *reinterpret_cast<u32x4*>(d + 4 * brow0) = u32x4{h[0], h[1], h[2], h[3]};
+        if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8 + 4 * brow0) = u32x4{l[0], l[1], l[2], l[3]};
+      } else {                       // k = 0..15
+        *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<u32x4*>(d + 4) = u32x4{h[4], h[5], h[6], h[7]};
+        if (PREC == 1) {
+          *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
+          *reinterpret_cast<u32x4*>(d + 12) = u32x4{l[4], l[5], l[6], l[7]};
+        }
+      }
+    } else if constexpr (ROWSTEP == 2) {  // rows k = brow0 + 2i: hi = brow0, s = i -> 8 contiguous floats
       float* d = &Bs[buf][bcol][brow0 * 8];
       *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[1], bv[2], bv[3]);
       *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[4], bv[5], bv[6], bv[7]);
@@ -232,27 +261,32 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
-    // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
-    f32x4 a[TM][2], b[TN][2];
+    if constexpr (PREC != 0) {
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else {
+      // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
+      f32x4 a[TM][2], b[TN][2];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
-      a[i][0] = *reinterpret_cast<const f32x4*>(r);
-      a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      for (int i = 0; i < TM; ++i) {
+        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        a[i][0] = *reinterpret_cast<const f32x4*>(r);
+        a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        b[j][0] = *reinterpret_cast<const f32x4*>(r);
+        b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
-      b[j][0] = *reinterpret_cast<const f32x4*>(r);
-      b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
-    }
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     if (t + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
   }
@@ -326,25 +360,34 @@ static int widen_cfg(int c, long HWo) {
 #define VST_MINW_SMALL 4
 #endif
 
-template <bool CF, bool GMK>
+template <bool CF, bool GMK, int PR>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
   switch (cfg) {
-    case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3><<<grid, NT, 0, st>>>(P); break;
-    case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
-    case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL><<<grid, NT, 0, st>>>(P); break;
-    case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3><<<grid, NT, 0, st>>>(P); break;
-    case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2><<<grid, NT, 0, st>>>(P); break;
-    case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, VST_MINW_T128><<<grid, NT, 0, st>>>(P); break;
-    default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192><<<grid, NT, 0, st>>>(P); break;
+    case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
+    case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
+    case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
+    case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
+    case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2, PR><<<grid, NT, 0, st>>>(P); break;
+    case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P); break;
+    default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR><<<grid, NT, 0, st>>>(P); break;
   }
+}
+
+template <int PR>
+static void launch_prec(bool cfast, bool gm, int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (cfast)
+    gm ? launch_cfg<true, true, PR>(cfg, grid, st, P) : launch_cfg<true, false, PR>(cfg, grid, st, P);
+  else
+    gm ? launch_cfg<false, true, PR>(cfg, grid, st, P) : launch_cfg<false, false, PR>(cfg, grid, st, P);
 }
 
 // ---------------------------------------------------------------------------------------------
 // fwd:        A[k = (kh*KW+kw)*Cin + ci][m = co]
 // transposed: A[k = (kh*KW+kw)*Cout + co][m = ci]        (data gradient)
 // split_kh:   A[k = kw*Cin + ci][m = co*KH + kh]          (row-split GEMM for tiny Cout, see vst_hip.h)
+// bsplit: write the bf16 hi/lo layout of the bf16 GEMM modes (vst_common.h apack_store)
 __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KH,
-                                   int KW, int transposed, int split_kh, int Mpad, int Kpad) {
+                                   int KW, int transposed, int split_kh, int Mpad, int Kpad, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)Mpad * Kpad;
   if (idx >= total) return;
@@ -366,7 +409,7 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
       v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
     }
   }
-  out[apack_index(k, m, Mpad)] = v;
+  apack_store(out, k, m, Mpad, v, bsplit);
 }
 
 // adjoint of (nearest x`up` upsample -> ReflectionPad2d(pad)): dpad [NC][Hv+2p][Wv+2p] -> dx [NC][Hs][Ws]
@@ -420,7 +463,7 @@ __global__ void fold_reflect_kernel(const float* __restrict__ dpad, float* __res
 // padded-input pixels (2yy+py, 2xx+px), and they read dY[yy - i][xx - j].  Packed as a
 // transposed A: k = (i*nkw + j)*Cout + co, m = ci.
 __global__ void pack_parity_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
-                                   int py, int px, int Mpad, int Kpad) {
+                                   int py, int px, int Mpad, int Kpad, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)Mpad * Kpad) return;
   int m = (int)(idx % Mpad);
@@ -432,7 +475,7 @@ __global__ void pack_parity_kernel(const float* __restrict__ w, float* __restric
     int i = tap / nkw, j = tap % nkw;
     v = w[(((long)co * Cin + m) * KS + py + 2 * i) * KS + px + 2 * j];
   }
-  out[apack_index(k, m, Mpad)] = v;
+  apack_store(out, k, m, Mpad, v, bsplit);
 }
 
 // fold_reflect over the 4 parity-class planes [class (a,b)][NC][Hc_a][Wc_b] of the padded grid
@@ -481,7 +524,17 @@ __global__ void fold_reflect_parity_kernel(const float* __restrict__ cls, float*
 
 extern "C" {
 
-int vst_version(void) { return 100; }
+int vst_version(void) { return 101; }
+
+static int g_gemm_mode = -1;
+
+int vst_set_gemm_mode(int mode) {
+  VST_CHECK_ARG(mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16);
+  g_gemm_mode = mode;
+  return VST_OK;
+}
+
+int vst_get_gemm_mode(void) { return vst_gemm_mode_internal(); }
 
 const char* vst_strerror(int code) {
   if (code == VST_OK) return "success";
@@ -502,12 +555,24 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
                     int Mpad, int Kpad, void* stream) {
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && !(transposed && split_kh));
   long total = (long)Mpad * Kpad;
-  pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad,
-                                                                            Kpad);
+  pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+      w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad, Kpad, vst_gemm_mode_internal() != VST_GEMM_F32);
   return vst_launch_status();
 }
 
 }  // extern "C"
+
+// initial mode from the environment: VST_GEMM_MODE = f32 | bf16x3 (default) | bf16
+int vst_gemm_mode_internal() {
+  if (g_gemm_mode < 0) {
+    const char* e = getenv("VST_GEMM_MODE");
+    int m = VST_GEMM_BF16X3;
+    if (e && !strcmp(e, "f32")) m = VST_GEMM_F32;
+    if (e && !strcmp(e, "bf16")) m = VST_GEMM_BF16;
+    g_gemm_mode = m;
+  }
+  return g_gemm_mode;
+}
 
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
                             int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
@@ -551,12 +616,13 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   P.fd_Cs = make_fastdiv(Cs);
   P.fd_KW = make_fastdiv(KW);
   dim3 grid(ceil_div((long)Ho * Wo, bn), P.Mpad / bm, N);
-  bool cfast = (Cs % 16) == 0;
+  const bool cfast = (Cs % 16) == 0, gm = gmask != nullptr;
   hipStream_t st = (hipStream_t)stream;
-  if (cfast)
-    gmask ? launch_cfg<true, true>(cfg, grid, st, P) : launch_cfg<true, false>(cfg, grid, st, P);
-  else
-    gmask ? launch_cfg<false, true>(cfg, grid, st, P) : launch_cfg<false, false>(cfg, grid, st, P);
+  switch (vst_gemm_mode_internal()) {
+    case VST_GEMM_F32: launch_prec<0>(cfast, gm, cfg, grid, st, P); break;
+    case VST_GEMM_BF16: launch_prec<2>(cfast, gm, cfg, grid, st, P); break;
+    default: launch_prec<1>(cfast, gm, cfg, grid, st, P); break;
+  }
   return vst_launch_status();
 }
 
@@ -587,8 +653,8 @@ int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int
                            void* stream) {
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && (py == 0 || py == 1) && (px == 0 || px == 1));
   long total = (long)Mpad * Kpad;
-  pack_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, py, px, Mpad,
-                                                                            Kpad);
+  pack_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+      w, packed, Cout, Cin, KS, py, px, Mpad, Kpad, vst_gemm_mode_internal() != VST_GEMM_F32);
   return vst_launch_status();
 }
 
@@ -667,7 +733,7 @@ namespace {
 // Summed-tap packed weight for the up=2 core: W'[jh][jw] = sum W[kh][kw] over
 // kh in {KS-1-jh, KS-jh}, kw in {KS-1-jw, KS-jw} (valid ones); transposed A: m = ci, k = (jh*(KS+1)+jw)*Cout + co
 __global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
-                                  int Mpad, int Kpad) {
+                                  int Mpad, int Kpad, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)Mpad * Kpad) return;
   const int m = (int)(idx % Mpad);
@@ -688,7 +754,7 @@ __global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict
       }
     }
   }
-  out[apack_index(k, m, Mpad)] = v;
+  apack_store(out, k, m, Mpad, v, bsplit);
 }
 
 // The ring of the padded-grid gradient, stored as four segments (each written by one GEMM):
@@ -851,7 +917,8 @@ extern "C" {
 int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream) {
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= Cin && Kpad >= (KS + 1) * (KS + 1) * Cout);
   long total = (long)Mpad * Kpad;
-  pack_upsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, Mpad, Kpad);
+  pack_upsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, Mpad, Kpad,
+                                                                           vst_gemm_mode_internal() != VST_GEMM_F32);
   return vst_launch_status();
 }
 

@@ -195,7 +195,7 @@ __global__ void tv_bwd_kernel(const float* __restrict__ s, long NC, int H, int W
 // S[n](k, m) = scale * (g[n][k][m] + g[n][m][k]) for k, m < C, zero padded, in the packed A layout
 // (bmm backward of F F^T: dF = (gG + gG^T) F / (C H W); S is symmetric so [k][m] is the packed A)
 __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict__ S, int N, int C, int Kpad, int Mpad,
-                                  float scale) {
+                                  float scale, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)N * Kpad * Mpad) return;
   int m = (int)(idx % Mpad);
@@ -207,7 +207,7 @@ __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict
     const float* gn = g + n * C * C;
     v = (gn[k * C + m] + gn[m * C + k]) * scale;
   }
-  S[n * (long)Kpad * Mpad + apack_index(k, m, Mpad)] = v;
+  apack_store(S + n * (long)Kpad * Mpad, k, m, Mpad, v, bsplit);
 }
 
 // ReLU backward: gx = gy * (y > 0)
@@ -358,7 +358,8 @@ int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const f
 int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, void* stream) {
   VST_CHECK_ARG(g && S && N > 0 && C > 0 && Kpad >= C && Mpad >= C);
   long total = (long)N * Kpad * Mpad;
-  symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale);
+  symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale,
+                                                                           vst_gemm_mode_internal() != VST_GEMM_F32);
   return vst_launch_status();
 }
 

@@ -57,6 +57,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// GEMM arithmetic mode (library-global, see vst_set_gemm_mode in vst_hip.h)
+enum { VST_GEMM_F32 = 0, VST_GEMM_BF16X3 = 1, VST_GEMM_BF16 = 2 };
+int vst_gemm_mode_internal();
+
 // Packed GEMM A operand ("weights"), k-tiles of 16: element (k, m) lives at
 //   ((k/16) * Mpad + m) * 16 + (k%2) * 8 + (k%16)/2
 // so one MFMA lane's 8 values of a k-tile (k = 2s + hi, s = 0..7, for v_mfma_f32_32x32x2_f32)
@@ -64,4 +68,90 @@ static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 // contiguous BM*16-float block in global memory.
 __host__ __device__ inline long apack_index(int k, int m, int Mpad) {
   return ((long)(k >> 4) * Mpad + m) * 16 + (k & 1) * 8 + ((k & 15) >> 1);
+}
+
+// ---- bf16 MFMA arithmetic ------------------------------------------------------------------
+// VST_GEMM_F32:    exact fp32 MFMA (v_mfma_f32_32x32x2_f32, 64 cycles per 32x32x2).
+// VST_GEMM_BF16X3: fp32 operands split x = hi + lo into two round-to-nearest bf16 values and
+//   multiplied as lo*hi + hi*lo + hi*hi on v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  The
+//   dropped lo*lo term and the rounding of lo bound the per-product error by ~2^-16 relative
+//   (fp32 MFMA: 2^-24), at 3 x 32 cycles per 32x32x16 instead of 8 x 64: 5.3x the MFMA rate.
+// VST_GEMM_BF16:   hi*hi only (one bf16 MFMA, ~2^-8 relative per product): the reduced-precision
+//   MFMA path of BASELINE config 5 (bf16 keeps fp32's exponent range: no loss scaling).
+// Every packed A operand is written in the layout of the mode current at pack time, so packs
+// must not be reused across a mode change.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair (round to nearest even), element 0 in the low half
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+// split (a, b) into packed hi and lo bf16 pairs: a = hi_a + lo_a (+ ~2^-17 relative)
+__device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pack_bf16x2(a, b);
+  const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xffff0000u);
+  lo = pack_bf16x2(a - ha, b - hb);
+}
+
+// Split packed A layout: the 16 k of one (k-tile, row m) block (64 bytes, the same footprint as
+// the fp32 block) hold 16 hi bf16 in natural k order, then the 16 lo bf16: an MFMA lane (k =
+// 8h + j) reads its hi and lo fragments with one ds_read_b128 each.
+__device__ __forceinline__ void apack_store(float* out, int k, int m, int Mpad, float v, int split) {
+  if (!split) {
+    out[apack_index(k, m, Mpad)] = v;
+    return;
+  }
+  unsigned short* u = reinterpret_cast<unsigned short*>(out + ((long)(k >> 4) * Mpad + m) * 16);
+  const uint32_t h = pack_bf16x2(v, 0.f) & 0xffffu;
+  const float l = v - __uint_as_float(h << 16);
+  u[k & 15] = (unsigned short)h;
+  u[16 + (k & 15)] = (unsigned short)(pack_bf16x2(l, 0.f) & 0xffffu);
+}
+
+// One 16-deep k-tile of a wave's TM x TN block of 32x32 accumulators from bf16 LDS rows
+// ([hi k0..15][lo k0..15][pad], 20 dwords): rows a0 + 32i + lane&31 of A, b0 + 32j + lane&31 of B.
+template <int TM, int TN, int PREC, int LS>
+__device__ __forceinline__ void mfma_bf16_ktile(f32x16 (&acc)[TM][TN], float (*A)[LS], float (*B)[LS], int a0,
+                                                int b0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8_t ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const float* p = &A[a0 + i * 32 + r][4 * h];
+    ah[i] = *reinterpret_cast<const bf16x8_t*>(p);
+    if (PREC == 1) al[i] = *reinterpret_cast<const bf16x8_t*>(p + 8);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float* p = &B[b0 + j * 32 + r][4 * h];
+    bh[j] = *reinterpret_cast<const bf16x8_t*>(p);
+    if (PREC == 1) bl[j] = *reinterpret_cast<const bf16x8_t*>(p + 8);
+  }
+  if (PREC == 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+}
+
+// Dispatch hands workgroups to the 8 XCDs round-robin (bid % 8, a speed assumption only):
+// remap so each XCD gets one contiguous range of the work order, which keeps blocks that share
+// operands (neighbouring pixel tiles, all tiles of one split-K chunk) on one L2.
+__device__ __forceinline__ int xcd_remap(int bid, int G) {
+  const int q = G >> 3, r = G & 7, xcd = bid & 7, loc = bid >> 3;
+  return xcd < r ? xcd * (q + 1) + loc : r * (q + 1) + (xcd - r) * q + loc;
 }

@@ -1,4 +1,5 @@
-// Split-K "activation-gradient x im2col(input)^T" GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// Split-K "activation-gradient x im2col(input)^T" GEMM on MFMA (fp32 32x32x2, or bf16x3 / bf16 32x32x16
+// per vst_set_gemm_mode).
 //
 //   slab[z][m][j] = sum_{r in chunk z}  A[n][m][r] * gather(src[n], j, r)
 //
@@ -27,16 +28,21 @@ struct WgParams {
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
-template <int WM, int TM, int WN, int TN, bool AV, int MINW>
+template <int WM, int TM, int WN, int TN, bool AV, int MINW, int PREC>
 __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int LS = 20;                       // LDS row: [hi][s] (k = 2s + hi) + 4 pad floats
+  constexpr int LS = 20;                       // LDS row: fp32 [hi][s] (k = 2s + hi) / bf16 [hi k][lo k]; + 4 pad
   constexpr int A_F4 = BM * BK / 4;            // vector path: float4 per A tile
   constexpr int A_PV = (A_F4 + NT - 1) / NT;
-  constexpr int A_PS = BM * BK / NT;           // scalar path: floats per thread
-  constexpr int B_PER = BN * BK / NT;
+  // scalar element map: PAIR consecutive pixels per thread (the bf16 paths pack a thread's two
+  // pixels into one dword), CPT rows (A) / columns (B) per pass
+  constexpr int PAIR = PREC ? 2 : 1;
+  constexpr int CPT = NT * PAIR / BK;          // 16 (fp32) or 32 (bf16)
+  constexpr int NCOL = BN / CPT;               // B columns per thread
+  constexpr int NAR = BM / CPT;                // A rows per thread (scalar path)
   static_assert(BK == 16, "LDS layout assumes 16-pixel k-tiles");
+  static_assert(BN % CPT == 0 && BM % CPT == 0, "tile");
 
   __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
@@ -45,10 +51,15 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   const int lane = tid & 63, wave = tid >> 6;
   const int lo = lane & 31, hi = lane >> 5;
   const int wm = wave / WN, wn = wave % WN;
-  const int j0 = blockIdx.x * BN;
-  const int m0 = blockIdx.y * BM;
-  const int n = blockIdx.z / P.S;
-  const int sidx = blockIdx.z - n * P.S;
+  // XCD-aware work order (column tile fastest, then row tile, then (image, split)): the tiles of
+  // one split-K chunk share its A rows and source pixels, so they run on one XCD's L2
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int rest = wk / gx, bz = rest / gy;
+  const int j0 = (wk - rest * gx) * BN;
+  const int m0 = (rest - bz * gy) * BM;
+  const int n = bz / P.S;
+  const int sidx = bz - n * P.S;
   const int HWo = P.Ho * P.Wo;
   const int r_begin = sidx * P.chunk;
   const int r_end = min(HWo, r_begin + P.chunk);
@@ -61,14 +72,14 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   const __amdgpu_buffer_rsrc_t bsrd =
       __builtin_amdgcn_make_buffer_rsrc((void*)src_n, (short)0, (int)((long)P.Cs * plane * 4), 0x00020000);
 
-  const int rr = tid % BK;  // B: this thread's pixel within a k-tile
-  const int cc = tid / BK;  // B: base column
+  const int rr = PREC ? (tid % (BK / 2)) * 2 : tid % BK;  // this thread's (first) pixel within a k-tile
+  const int cc = PREC ? tid / (BK / 2) : tid / BK;        // base row / column
 
   // decode this thread's B columns once: (ci, kh, kw) packed, -1 if j >= J
-  int jdesc[B_PER];
+  int jdesc[NCOL];
 #pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    int j = j0 + cc + i * (NT / BK);
+  for (int i = 0; i < NCOL; ++i) {
+    int j = j0 + cc + i * CPT;
     int d = -1;
     if (j < P.J) {
       int tap = (int)fdiv((uint32_t)j, P.fd_Cs);
@@ -89,8 +100,8 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   f32x4 rav[AV ? A_PV : 1];
-  float ras[AV ? 1 : A_PS];
-  float rb[B_PER];
+  float ras[AV ? 1 : NAR * PAIR];
+  float rb[NCOL * PAIR];
   const int ntiles = r_end > r_begin ? (r_end - r_begin + BK - 1) / BK : 0;
   const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
   const int sh = P.up - 1;
@@ -106,7 +117,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
 
   auto load_tile = [&](int t) {
     const int rt = r_begin + t * BK;
-    if (AV) {
+    if constexpr (AV) {
 #pragma unroll
       for (int i = 0; i < A_PV; ++i) {
         const int idx = tid + i * NT;
@@ -117,51 +128,91 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < A_PS; ++i) {
-        const int off = a_offset(m0 + cc + i * (NT / BK), rt + rr);
-        ras[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(asrd, off == OOR ? OOR : off * 4, 0, 0));
-      }
-    }
-    const int r = rt + rr;
-    const bool rv = r < r_end;
-    const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
-    const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
+      for (int i = 0; i < NAR; ++i)
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int d = jdesc[i];
-      const int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
-      int y = by + kh, x = bx + kw;
-      bool ok = rv && d >= 0;
-      if (P.gmode == 0) {
-        y = abs(y);
-        y = min(y, 2 * Hv - 2 - y);
-        x = abs(x);
-        x = min(x, 2 * Wv - 2 - x);
-      } else {
-        ok = ok && y >= 0 && y < Hv && x >= 0 && x < Wv;
+        for (int q = 0; q < PAIR; ++q) {
+          const int off = a_offset(m0 + cc + i * CPT, rt + rr + q);
+          ras[i * PAIR + q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(asrd, off == OOR ? OOR : off * 4, 0, 0));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PAIR; ++q) {
+      const int r = rt + rr + q;
+      const bool rv = r < r_end;
+      const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
+      const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
+#pragma unroll
+      for (int i = 0; i < NCOL; ++i) {
+        const int d = jdesc[i];
+        const int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
+        int y = by + kh, x = bx + kw;
+        bool ok = rv && d >= 0;
+        if (P.gmode == 0) {
+          y = abs(y);
+          y = min(y, 2 * Hv - 2 - y);
+          x = abs(x);
+          x = min(x, 2 * Wv - 2 - x);
+        } else {
+          ok = ok && y >= 0 && y < Hv && x >= 0 && x < Wv;
+        }
+        const int vo = ok ? (ci * plane + (y >> sh) * P.Ws + (x >> sh)) * 4 : OOR;
+        rb[i * PAIR + q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
       }
-      const int vo = ok ? (ci * plane + (y >> sh) * P.Ws + (x >> sh)) * 4 : OOR;
-      rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
     }
   };
   auto store_tile = [&](int buf) {
-    if (AV) {
+    if constexpr (PREC == 0) {
+      if constexpr (AV) {
 #pragma unroll
-      for (int i = 0; i < A_PV; ++i) {
-        const int idx = tid + i * NT;
-        if (A_F4 % NT == 0 || idx < A_F4) {
-          const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> (s, hi) = (2q,0),(2q,1),(2q+1,0),(2q+1,1)
-          float* row = &As[buf][m][0];
-          *reinterpret_cast<f32x2*>(&row[2 * q]) = f32x2{rav[i][0], rav[i][2]};
-          *reinterpret_cast<f32x2*>(&row[8 + 2 * q]) = f32x2{rav[i][1], rav[i][3]};
+        for (int i = 0; i < A_PV; ++i) {
+          const int idx = tid + i * NT;
+          if (A_F4 % NT == 0 || idx < A_F4) {
+            const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> (s, hi) = (2q,0),(2q,1),(2q+1,0),(2q+1,1)
+            float* row = &As[buf][m][0];
+            *reinterpret_cast<f32x2*>(&row[2 * q]) = f32x2{rav[i][0], rav[i][2]};
+            *reinterpret_cast<f32x2*>(&row[8 + 2 * q]) = f32x2{rav[i][1], rav[i][3]};
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NAR; ++i) As[buf][cc + i * CPT][(rr & 1) * 8 + (rr >> 1)] = ras[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NCOL; ++i) Bs[buf][cc + i * CPT][(rr & 1) * 8 + (rr >> 1)] = rb[i];
+    } else {  // bf16 rows [hi px 0..15][lo px 0..15]
+      if constexpr (AV) {
+#pragma unroll
+        for (int i = 0; i < A_PV; ++i) {
+          const int idx = tid + i * NT;
+          if (A_F4 % NT == 0 || idx < A_F4) {
+            const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> bf16 slots 4q..4q+3 = dwords 2q, 2q+1
+            uint32_t h0, l0, h1, l1;
+            split_bf16x2(rav[i][0], rav[i][1], h0, l0);
+            split_bf16x2(rav[i][2], rav[i][3], h1, l1);
+            uint32_t* row = reinterpret_cast<uint32_t*>(&As[buf][m][0]);
+            *reinterpret_cast<u32x2*>(row + 2 * q) = u32x2{h0, h1};
+            if (PREC == 1) *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{l0, l1};
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NAR; ++i) {
+          uint32_t h, l;
+          split_bf16x2(ras[2 * i], ras[2 * i + 1], h, l);
+          uint32_t* row = reinterpret_cast<uint32_t*>(&As[buf][cc + i * CPT][0]);
+          row[rr >> 1] = h;
+          if (PREC == 1) row[8 + (rr >> 1)] = l;
         }
       }
-    } else {
 #pragma unroll
-      for (int i = 0; i < A_PS; ++i) As[buf][cc + i * (NT / BK)][(rr & 1) * 8 + (rr >> 1)] = ras[i];
+      for (int i = 0; i < NCOL; ++i) {
+        uint32_t h, l;
+        split_bf16x2(rb[2 * i], rb[2 * i + 1], h, l);
+        uint32_t* row = reinterpret_cast<uint32_t*>(&Bs[buf][cc + i * CPT][0]);
+        row[rr >> 1] = h;
+        if (PREC == 1) row[8 + (rr >> 1)] = l;
+      }
     }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) Bs[buf][cc + i * (NT / BK)][(rr & 1) * 8 + (rr >> 1)] = rb[i];
   };
 
   if (ntiles > 0) {
@@ -172,31 +223,36 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
-    f32x4 a[TM][2], b[TN][2];
+    if constexpr (PREC != 0) {
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else {
+      f32x4 a[TM][2], b[TN][2];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
-      a[i][0] = *reinterpret_cast<const f32x4*>(r);
-      a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      for (int i = 0; i < TM; ++i) {
+        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        a[i][0] = *reinterpret_cast<const f32x4*>(r);
+        a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        b[j][0] = *reinterpret_cast<const f32x4*>(r);
+        b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < BK / 2; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
-      b[j][0] = *reinterpret_cast<const f32x4*>(r);
-      b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     if (t + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
   }
 
-  float* slab = P.slab + (long)blockIdx.z * P.Mpad * P.Jpad;
+  float* slab = P.slab + (long)bz * P.Mpad * P.Jpad;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int jj = j0 + (wn * TN + j) * 32 + lo;
@@ -264,25 +320,34 @@ __global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __rest
   out[idx] = s * scale;
 }
 
-template <bool AV>
+template <bool AV, int PR>
 static void launch_wg_t(int c, dim3 g, hipStream_t st, const WgParams& P) {
   switch (c) {
-    case W32: wgrad_kernel<1, 1, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad_kernel<1, 2, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad_kernel<1, 3, 4, 1, AV, 4><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad_kernel<2, 2, 2, 2, AV, 3><<<g, NT, 0, st>>>(P); break;  // 4 per CU spills (128-VGPR cap)
-    default: wgrad_kernel<2, 3, 2, 2, AV, 2><<<g, NT, 0, st>>>(P); break;
+    case W32: wgrad_kernel<1, 1, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad_kernel<1, 2, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad_kernel<1, 3, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad_kernel<2, 2, 2, 2, AV, 3, PR><<<g, NT, 0, st>>>(P); break;  // 4 per CU spills (128-VGPR cap)
+    default: wgrad_kernel<2, 3, 2, 2, AV, 2, PR><<<g, NT, 0, st>>>(P); break;
   }
+}
+
+template <int PR>
+static void launch_wg_p(bool av, int c, dim3 g, hipStream_t st, const WgParams& P) {
+  if (av)
+    launch_wg_t<true, PR>(c, g, st, P);
+  else
+    launch_wg_t<false, PR>(c, g, st, P);
 }
 
 static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
   // float4 A loads need 4 consecutive pixels in one row segment (and, for the row-split gather,
   // in one output row)
   const bool av = (P.Ho * P.Wo) % 4 == 0 && (!P.asplit || P.Wo % 4 == 0);
-  if (av)
-    launch_wg_t<true>(c, g, st, P);
-  else
-    launch_wg_t<false>(c, g, st, P);
+  switch (vst_gemm_mode_internal()) {
+    case VST_GEMM_F32: launch_wg_p<0>(av, c, g, st, P); break;
+    case VST_GEMM_BF16: launch_wg_p<2>(av, c, g, st, P); break;
+    default: launch_wg_p<1>(av, c, g, st, P); break;
+  }
 }
 
 static int wminw(int c) {  // resident blocks per CU of each configuration (its launch bound)

@@ -33,8 +33,9 @@ def _empty(shape, like):
     return torch.empty(shape, device=like.device, dtype=torch.float32)
 
 
-def packed_matrix(x, M, K, transpose):
+def packed_matrix(x, M, K, transpose, role="attn"):
     """Per-image packed GEMM A operand from x[n] = X[K][M] (transpose=False) or X[M][K]."""
+    ops.gemm_role(role)
     N = x.shape[0]
     Mpad, Kpad = ops.pack_dims(M, K)
     ap = _empty((N * Kpad * Mpad,), x)
@@ -42,18 +43,19 @@ def packed_matrix(x, M, K, transpose):
     return ap, Kpad * Mpad
 
 
-def bmm_at_b(x, M, K, transpose, b, P, out=None):
+def bmm_at_b(x, M, K, transpose, b, P, out=None, role="attn"):
     """out[n] = Aop[n]^T-as-packed @ b[n]:  out[n][m][p] = sum_k Aop[n][k][m] b[n][k][p], where
     Aop[n][k][m] = x[n][k][m] (transpose=False) or x[n][m][k] (transpose=True)."""
     N = b.shape[0]
-    ap, abs_ = packed_matrix(x, M, K, transpose)
+    ap, abs_ = packed_matrix(x, M, K, transpose, role)
     o = ops.conv_gemm(b.view(N, K, 1, P), ap, M, 1, 1, P, ops.GM_ZERO, 1, 0, 1, a_batch_stride=abs_,
                       out=None if out is None else out.view(N, M, 1, P))
     return o.view(N, M, P)
 
 
-def gemm_abt(a, b, scale=1.0):
+def gemm_abt(a, b, scale=1.0, role="attn"):
     """out[n][m][j] = scale * sum_r a[n][m][r] b[n][j][r]."""
+    ops.gemm_role(role)
     N, M, R = a.shape
     J = b.shape[1]
     if b.shape[0] != N or b.shape[2] != R:
@@ -62,7 +64,7 @@ def gemm_abt(a, b, scale=1.0):
     ws = _empty((lib.vst_wgrad_workspace(N, M, J, R),), a)
     from .. import kprof
 
-    tok = kprof.begin(2.0 * N * M * J * R, 4.0 * (a.numel() + b.numel() + out.numel()), ("abt", N, M, J, R))
+    tok = kprof.begin(2.0 * N * M * J * R, 4.0 * (a.numel() + b.numel() + out.numel()), ("abt", N, M, J, R), ops.gemm_mode())
     lib.vst_gemm_abt(ptr(a), ptr(b), ptr(out), ptr(ws), N, M, J, R, float(scale), stream())
     kprof.end(tok, family="gemm_abt")
     return out
@@ -72,14 +74,14 @@ def _vec(shape, like):
     return torch.empty(shape, device=like.device, dtype=torch.float32)
 
 
-def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None):
+def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None, role="attn"):
     """out[n][m][p] = (sum_k x[n][k][m] b[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]."""
     N = b.shape[0]
-    ap, abs_ = packed_matrix(x, M, K, False)
+    ap, abs_ = packed_matrix(x, M, K, False, role)
     out = _empty((N, M, P), b)
     from .. import kprof
 
-    tok = kprof.begin(2.0 * N * M * P * K, 4.0 * (b.numel() + ap.numel() + out.numel()), ("attn", N, M, K, P))
+    tok = kprof.begin(2.0 * N * M * P * K, 4.0 * (b.numel() + ap.numel() + out.numel()), ("attn", N, M, K, P), ops.gemm_mode())
     lib.vst_attn_gemm(ptr(b), ptr(ap), ptr(out), N, K, P, M, abs_, ptr(ra), ptr(rb), ptr(rd), ptr(cg), stream())
     kprof.end(tok)
     return out
@@ -134,6 +136,7 @@ class AdaAttnFn(Function):
             raise VstError(f"adaattn: Q{tuple(Q.shape)} K{tuple(K.shape)} V{tuple(V.shape)} c{tuple(cn.shape)}")
         Q, K, V, cn = (ops._check(t, "adaattn operand", 4) for t in (Q, K, V, cn))
         Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
+        role = "attn_" + activation
         qn = kn = S = rowsum = None
         if activation == COSINE:
             qn, kn = channel_norm(Qm), channel_norm(Km)
@@ -142,14 +145,14 @@ class AdaAttnFn(Function):
             qkbar = channel_dot(Qm, v=plane_dot(Km, ks))
             c, e = _vec((N, Nc), Q), _vec((N, Nc), Q)
             lib.vst_attn_fwd_rows(ptr(qkbar), ptr(qn), ptr(c), ptr(e), N * Nc, Ns, stream())
-            A = attn_gemm(Qm, Nc, d, Km, Ns, rb=c, cg=ks, rd=e)  # [N][Nc][Ns], S never stored
+            A = attn_gemm(Qm, Nc, d, Km, Ns, rb=c, cg=ks, rd=e, role=role)  # [N][Nc][Ns], S never stored
             rowsum = (ks, c, e)
         else:
-            S = bmm_at_b(Qm, Nc, d, False, Km, Ns)  # [N][Nc][Ns]
+            S = bmm_at_b(Qm, Nc, d, False, Km, Ns, role=role)  # [N][Nc][Ns]
             A, _ = attention_rows(S, activation)
         VV2 = _empty((N, 2 * dv, Ns), V)
         lib.vst_square_concat(ptr(V), ptr(VV2), N, dv * Ns, stream())
-        MV = gemm_abt(VV2, A)  # [N][2dv][Nc]
+        MV = gemm_abt(VV2, A, role=role)  # [N][2dv][Nc]
         out = _empty((N, dv, h, w), V)
         lib.vst_adaattn_out(ptr(MV), ptr(cn), ptr(out), N, dv * Nc, stream())
         ctx.activation = activation
@@ -163,12 +166,13 @@ class AdaAttnFn(Function):
     def backward(ctx, dout):
         Q, K, V, cn, qn, kn, S, A, VV2, MV, ks, c, e = ctx.saved_tensors
         N, d, dv, Nc, Ns = ctx.dims
+        role = "attn_" + ctx.activation
         dout = dout.contiguous()
         dMV = _empty(MV.shape, MV)
         lib.vst_adaattn_out_bwd(ptr(dout), ptr(MV), ptr(cn), ptr(dMV), N, dv * Nc, stream())
         dQ = dK = dV = None
         if ctx.needs_input_grad[2]:
-            dVV2 = bmm_at_b(dMV, 2 * dv, Nc, True, A, Ns)  # [N][2dv][Ns]
+            dVV2 = bmm_at_b(dMV, 2 * dv, Nc, True, A, Ns, role=role)  # [N][2dv][Ns]
             dV = _empty(V.shape, V)
             lib.vst_square_concat_bwd(ptr(dVV2), ptr(V), ptr(dV), N, dv * Ns, stream())
             del dVV2
@@ -180,22 +184,22 @@ class AdaAttnFn(Function):
                 dqn, nr, cr = _vec((N, Nc), Q), _vec((N, Nc), Q), _vec((N, Nc), Q)
                 lib.vst_attn_bwd_rows(ptr(r), ptr(DA), ptr(qn), ptr(c), ptr(e), ptr(dqn), ptr(nr), ptr(cr), N * Nc, Ns,
                                       stream())
-                dS = attn_gemm(dMV, Nc, 2 * dv, VV2, Ns, rb=c, cg=ks, ra=nr)  # (dA - r) c ks, dA never stored
+                dS = attn_gemm(dMV, Nc, 2 * dv, VV2, Ns, rb=c, cg=ks, ra=nr, role=role)  # (dA - r) c ks
             else:
-                dS = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns)  # dA
+                dS = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns, role=role)  # dA
                 lib.vst_softmax_rows_bwd(ptr(dS), ptr(A), ptr(dS), N * Nc, Ns, stream())
             if ctx.needs_input_grad[0]:
-                dQ = gemm_abt(Km, dS)  # [N][d][Nc]
+                dQ = gemm_abt(Km, dS, role=role)  # [N][d][Nc]
                 if ctx.activation == COSINE:
                     lib.vst_norm_grad_add(ptr(dQ), ptr(dqn), ptr(qn), ptr(Qm), N, d, Nc, stream())
                 dQ = dQ.view(Q.shape)
             if ctx.needs_input_grad[1]:
-                dK = bmm_at_b(Qm, d, Nc, True, dS, Ns)  # [N][d][Ns]
+                dK = bmm_at_b(Qm, d, Nc, True, dS, Ns, role=role)  # [N][d][Ns]
                 if ctx.activation == COSINE:
                     dMVc = _empty(dMV.shape, dMV)
                     lib.vst_scale_cols(ptr(dMV), ptr(c), ptr(dMVc), N, 2 * dv, Nc, stream())
-                    Z = gemm_abt(dMVc, Qm)  # [N][2dv][d]
-                    Y = bmm_at_b(Z, d, 2 * dv, False, VV2, Ns)  # [N][d][Ns]
+                    Z = gemm_abt(dMVc, Qm, role=role)  # [N][2dv][d]
+                    Y = bmm_at_b(Z, d, 2 * dv, False, VV2, Ns, role=role)  # [N][d][Ns]
                     dkn = _vec((N, Ns), K)
                     lib.vst_attn_dkn(ptr(Km), ptr(Y), ptr(plane_dot(Qm, cr)), ptr(ks), ptr(dkn), N, d, Ns, stream())
                     lib.vst_norm_grad_add(ptr(dK), ptr(dkn), ptr(kn), ptr(Km), N, d, Ns, stream())

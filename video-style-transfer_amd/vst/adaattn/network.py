@@ -93,6 +93,10 @@ class Decoder(nn.Module):
         self.conv8 = Conv(64, 3, kernel_size=3, stride=1)
 
     def forward(self, x5, x4, x3):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(x5, x4, x3)
+
+    def _forward(self, x5, x4, x3):
         x = ops.upsample2x(x5, addend=x4)
         x = self.conv1(x)
         x = ops.upsample_cat(self.conv2(x), x3)
@@ -156,6 +160,10 @@ class AdaAttN(nn.Module):
         self.activation = _activation(activation)
 
     def forward(self, c_x, s_x, c_1x, s_1x):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(c_x, s_x, c_1x, s_1x)
+
+    def _forward(self, c_x, s_x, c_1x, s_1x):
         Q = ops.conv2d(instance_norm_plain(c_1x), self.f.weight, self.f.bias)
         K = ops.conv2d(instance_norm_plain(s_1x), self.g.weight, self.g.bias)
         V = ops.conv2d(s_x, self.h.weight, self.h.bias)
@@ -175,6 +183,10 @@ class StylizingNetwork(nn.Module):
         self.decoder = Decoder()
 
     def forward(self, fc, fs):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(fc, fs)
+
+    def _forward(self, fc, fs):
         fc = list(fc.values())
         fs = list(fs.values())
         outs = []

@@ -235,6 +235,10 @@ class ReCoNet(nn.Module):
         self.deconv3 = ConvTanh(48, 3, kernel_size=9, stride=1)
 
     def forward(self, x):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(x)
+
+    def _forward(self, x):
         x = self.conv1(x)
         x = self.conv2(x)
         x = self.conv3(x)
@@ -269,6 +273,10 @@ class ReCoNetSD1(nn.Module):
         self.deconv3 = ConvTanh(32, 3, kernel_size=9, stride=1)
 
     def forward(self, x):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(x)
+
+    def _forward(self, x):
         x = self.conv1(x)
         x = self.conv2(x)
         x = self.conv3_sd(x)
@@ -304,6 +312,10 @@ class ReCoNetSD2(nn.Module):
         self.deconv3_sd2 = ConvTanh(16, 3, kernel_size=9, stride=1)
 
     def forward(self, x):
+        with ops.gemm_scope("stylizer"):
+            return self._forward(x)
+
+    def _forward(self, x):
         x = self.conv1_sd2(x)
         x = self.conv2_sd2(x)
         x = self.conv3_sd2(x)
