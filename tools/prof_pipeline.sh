@@ -7,7 +7,7 @@ what=${2:-all}
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-args="--model $model --steps 3 --warmup 1 --no-cpu-baseline --no-vgg19"
+args="--model $model --steps 3 --warmup 1 --no-cpu-baseline --no-vgg19 --gemm ${GEMM:-parity}"
 if [ "$what" == "stats" ] || [ "$what" == "all" ]; then
   timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$model -o run -- \
     python3 bench.py $args > gpurun_out/prof_$model.log 2>&1 || { echo "stats pass failed rc=$?"; exit 3; }

@@ -1,0 +1,379 @@
+// Implicit-GEMM convolution kernel template (shared by the per-precision translation units
+// conv_gemm_p{0,1,2}.hip, which each instantiate one GEMM arithmetic mode, and conv_gemm.hip,
+// which holds the host launcher and the C ABI).  See conv_gemm.hip for the algorithm.
+#pragma once
+#include "vst_common.h"
+
+namespace vstk {
+
+__device__ __forceinline__ f32x4 mk4(float a, float b, float c, float d) {
+  f32x4 v = {a, b, c, d};
+  return v;
+}
+
+#ifndef VST_CONV_BK
+#define VST_CONV_BK 16
+#endif
+constexpr int BK = VST_CONV_BK;  // k-tile depth (multiple of 16)
+constexpr int NT = 256;
+
+struct ConvParams {
+  const float* src;
+  const float* wpack;
+  const float* bias;
+  const float* mask;
+  const float* gmask;
+  float* out;
+  float* aux;
+  long a_batch_stride;
+  int Cs, Hs, Ws;
+  int M, Mpad, K, Kpad;
+  int Ho, Wo;
+  int KH, KW, gmode, stride, pad, up;
+  int pad_x;  // column padding (= pad except for the dgrad ring segments)
+  int epi;
+  // EPI_AFFINE: v = (acc + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]  (ra, rd optional)
+  const float *ep_ra, *ep_rb, *ep_rd, *ep_cg;
+  FastDiv fd_Wo, fd_Cs, fd_KW;
+};
+
+enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
+enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32 };
+
+// source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
+// (select-only arithmetic: no divergent branches inside the k loop)
+__device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox, int kh, int kw) {
+  if (P.gmode == GM_TRANSPOSED) {
+    int ty = oy + P.pad - kh, tx = ox + P.pad_x - kw;
+    bool ok = ty >= 0 && tx >= 0;
+    if (P.stride == 2) {
+      ok = ok && !((ty | tx) & 1);
+      ty >>= 1;
+      tx >>= 1;
+    }
+    ok = ok && ty < P.Hs && tx < P.Ws;
+    return ok ? ty * P.Ws + tx : -1;
+  }
+  const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
+  int y = oy * P.stride + kh - P.pad, x = ox * P.stride + kw - P.pad_x;
+  bool ok = true;
+  if (P.gmode == GM_REFLECT) {
+    y = abs(y);
+    y = y >= Hv ? 2 * Hv - 2 - y : y;
+    x = abs(x);
+    x = x >= Wv ? 2 * Wv - 2 - x : x;
+  } else {
+    ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
+  }
+  const int sh = P.up - 1;
+  return ok ? (y >> sh) * P.Ws + (x >> sh) : -1;
+}
+
+// float4 slot (row*4 + quad) of A-tile element idx: 8 consecutive lanes take 8 consecutive rows of
+// one quad, so each 8-lane ds_write_b128 group hits 8 distinct 4-bank slots (rows are 20 dwords
+// apart; bank = dword mod 32) -- the plain row-major order put rows r and r+1's quads 0 and 3 on
+// the same banks (2-way conflict on every A store).  The wave still covers whole 64-B rows.
+__device__ __forceinline__ int a_slot(int idx) {
+  const int row = (idx & 7) | ((idx >> 5) << 3), quad = (idx >> 3) & 3;
+  return row * 4 + quad;
+}
+
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC>
+__global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int A_F4 = BK * BM / 4;          // float4 per A tile
+  constexpr int A_PER = (A_F4 + NT - 1) / NT;
+  constexpr int ROWSTEP = NT / BN;           // B rows covered per pass
+  constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
+  constexpr int KSTEPS = BK / 2;
+  // k rows of this thread's B elements: fp32 MFMA (32x32x2: lane half h takes k = 2s + h) ->
+  // k = brow0 + ROWSTEP*i; bf16 MFMA (32x32x16: lane half h takes k = 8h..8h+7) -> contiguous
+  // k = brow0*B_PER + i, so each thread packs its own bf16 pairs
+  constexpr int KSTEP = PREC ? 1 : ROWSTEP;
+  static_assert(NT % BN == 0 && BK % ROWSTEP == 0, "tile");
+
+  static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
+  constexpr int LS = 20;  // LDS row: [hi][s] 16 floats + 4 pad (conflict-free ds_read_b128 / ds_write_b128)
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int lo = lane & 31, hi = lane >> 5;
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware work order: M tile fastest, then pixel tile, then image, so the blocks that share a
+  // source panel (and its halo rows) run on one XCD's L2
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  // (integer division is VALU work: readfirstlane keeps the results scalar, so the buffer
+  // descriptors built from them stay in SGPRs -- no waterfall loops around the loads)
+  const int rest = __builtin_amdgcn_readfirstlane(wk / gy);
+  const int n = __builtin_amdgcn_readfirstlane(rest / gx);
+  const int m0 = __builtin_amdgcn_readfirstlane((wk - rest * gy) * BM);
+  const int p0 = __builtin_amdgcn_readfirstlane((rest - n * gx) * BN);
+  const int HWo = P.Ho * P.Wo;
+  const long plane = (long)P.Hs * P.Ws;
+  const float* src_n = P.src + (long)n * P.Cs * plane;
+  const float* gm_n = GM ? P.gmask + (long)n * P.Cs * plane : nullptr;
+  const float* A = P.wpack + (long)n * P.a_batch_stride;
+
+  // this thread's B column (fixed for the whole k loop)
+  const int bcol = tid % BN;
+  const int brow0 = tid / BN;
+  const int krow0 = PREC ? brow0 * B_PER : brow0;
+  const int p = p0 + bcol;
+  const bool pvalid = p < HWo;
+  int oy = 0, ox = 0;
+  if (pvalid) {
+    oy = (int)fdiv((uint32_t)p, P.fd_Wo);
+    ox = p - oy * P.Wo;
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  f32x4 ra[A_PER];
+  float rb[B_PER];
+  float rg[GM ? B_PER : 1];
+  // buffer descriptors over this image's source planes (wave-uniform inputs only)
+  const int plane_i = P.Hs * P.Ws;
+  const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane_i * 4u;
+  constexpr int OOR = 0x7ffffff0;  // any offset >= num_records reads 0
+  const __amdgpu_buffer_rsrc_t srd = uniform_rsrc(src_n, src_bytes);
+  const __amdgpu_buffer_rsrc_t gsrd = uniform_rsrc(GM ? gm_n : src_n, src_bytes);
+  const int ntiles = P.Kpad / BK;
+
+  // Issue every global load of tile t without branches (out-of-range taps read a clamped, valid
+  // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
+  auto load_tile = [&](int t) {
+    const int k0 = t * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int idx = tid + i * NT;
+      if (A_F4 % NT == 0 || idx < A_F4) {
+        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * 16 + 4 * a_slot(idx));
+      }
+    }
+    if (CFAST) {
+      // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
+      // offset per thread per group; out-of-range taps use an offset past the buffer end, which
+      // the buffer-load range check turns into 0 (no branch, no select)
+      constexpr int NG = BK / 16, PER_G = B_PER / NG;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int kg = k0 + 16 * g;
+        // wave-uniform tap decode by multiply-shift (SALU), not by integer division
+        const int tap = (int)fdiv((uint32_t)kg, P.fd_Cs);
+        const int c0 = kg - tap * P.Cs;
+        const int kh = (int)fdiv((uint32_t)tap, P.fd_KW), kw = tap - kh * P.KW;
+        const int off0 = gather_offset(P, oy, ox, kh, kw);
+        const bool ok = pvalid && kg < P.K && off0 >= 0;
+        const int vo = ok ? ((c0 + (PREC ? brow0 * PER_G : brow0)) * plane_i + off0) * 4 : OOR;
+        const int vstep = ok ? KSTEP * plane_i * 4 : 0;
+#pragma unroll
+        for (int i = 0; i < PER_G; ++i) {
+          rb[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
+          if (GM) rg[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo + i * vstep, 0, 0));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int k = k0 + krow0 + i * KSTEP;
+        const int kc = k < P.K ? k : 0;
+        const int tap = (int)fdiv((uint32_t)kc, P.fd_Cs);
+        const int c = kc - tap * P.Cs;
+        const int kh = (int)fdiv((uint32_t)tap, P.fd_KW);
+        const int kw = tap - kh * P.KW;
+        const int off0 = gather_offset(P, oy, ox, kh, kw);
+        const bool ok = pvalid && k < P.K && off0 >= 0;
+        const int vo = ok ? (c * plane_i + off0) * 4 : OOR;
+        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, 0, 0));
+        if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, 0, 0));
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int idx = tid + i * NT;
+      if (A_F4 % NT == 0 || idx < A_F4) {
+        const int sl = a_slot(idx);
+        *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
+      }
+    }
+    float bv[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) bv[i] = GM ? (rg[i] > 0.f ? rb[i] : 0.f) : rb[i];
+    if constexpr (PREC != 0) {  // bf16 row: [hi k0..15][lo k0..15], this thread's k contiguous
+      uint32_t h[B_PER / 2], l[B_PER / 2];
+#pragma unroll
+      for (int q = 0; q < B_PER / 2; ++q) split_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
+      if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
+        *reinterpret_cast<u32x4*>(d + 4 * brow0) = u32x4{h[0], h[1], h[2], h[3]};
+        if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8 + 4 * brow0) = u32x4{l[0], l[1], l[2], l[3]};
+      } else {                       // k = 0..15
+        *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<u32x4*>(d + 4) = u32x4{h[4], h[5], h[6], h[7]};
+        if (PREC == 1) {
+          *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
+          *reinterpret_cast<u32x4*>(d + 12) = u32x4{l[4], l[5], l[6], l[7]};
+        }
+      }
+    } else if constexpr (ROWSTEP == 2) {  // rows k = brow0 + 2i: hi = brow0, s = i -> 8 contiguous floats
+      float* d = &Bs[buf][bcol][brow0 * 8];
+      *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[1], bv[2], bv[3]);
+      *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[4], bv[5], bv[6], bv[7]);
+    } else {             // ROWSTEP == 1: rows k = i
+      float* d = &Bs[buf][bcol][0];
+      *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[2], bv[4], bv[6]);
+      *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[8], bv[10], bv[12], bv[14]);
+      *reinterpret_cast<f32x4*>(d + 8) = mk4(bv[1], bv[3], bv[5], bv[7]);
+      *reinterpret_cast<f32x4*>(d + 12) = mk4(bv[9], bv[11], bv[13], bv[15]);
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1);
+    if constexpr (PREC != 0) {
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else {
+      // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
+      f32x4 a[TM][2], b[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        a[i][0] = *reinterpret_cast<const f32x4*>(r);
+        a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        b[j][0] = *reinterpret_cast<const f32x4*>(r);
+        b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  float* out_n = P.out + (long)n * P.M * HWo;
+  const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int pp = p0 + (wn * TN + j) * 32 + lo;
+    if (pp >= HWo) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (m >= P.M) continue;
+        float v = acc[i][j][r];
+        if (P.epi & EPI_AFFINE) {
+          const long rm = (long)n * P.M + m;
+          v = (v + (P.ep_ra ? P.ep_ra[rm] : 0.f)) * P.ep_rb[rm] * P.ep_cg[(long)n * HWo + pp] +
+              (P.ep_rd ? P.ep_rd[rm] : 0.f);
+        }
+        if (P.epi & EPI_BIAS) v += P.bias[m];
+        if (P.epi & EPI_RELU) v = fmaxf(v, 0.f);
+        const long o = (long)m * HWo + pp;
+        if (P.epi & EPI_TANH) {
+          const float t = tanhf(v / 255.0f);
+          if (P.aux) P.aux[(long)n * P.M * HWo + o] = t;
+          v = t * 150.0f + 127.5f;
+        }
+        if (P.epi & EPI_MASK) v = mask_n[o] > 0.f ? v : 0.f;
+        if (P.epi & EPI_ACCUM) v += out_n[o];
+        out_n[o] = v;
+      }
+    }
+  }
+}
+
+// tile configurations (BM x BN)
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W };
+
+inline int select_cfg(int M) {
+  if (M <= 32) return T32;
+  if (M <= 64) return T64;
+  if (M <= 96) return T96;
+  if (M % 192 == 0 && M % 128 != 0) return T192;
+  return T128;
+}
+inline int cfg_bm(int c) {
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96};
+  return bm[c];
+}
+inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
+#ifndef VST_WIDE
+#define VST_WIDE 1
+#endif
+// 64/96-row tiles on large pixel grids: 256-column tiles (twice the MFMAs per A fragment)
+inline int widen_cfg(int c, long HWo) {
+  if (!VST_WIDE || HWo < 8192) return c;
+  return c == T64 ? T64W : (c == T96 ? T96W : c);
+}
+
+#ifndef VST_MINW_T128
+#define VST_MINW_T128 4
+#endif
+#ifndef VST_MINW_T192
+#define VST_MINW_T192 2
+#endif
+#ifndef VST_MINW_SMALL
+#define VST_MINW_SMALL 4
+#endif
+// bf16 paths: the hi/lo conversion temporaries push the 2x2-accumulator tile past 128 VGPRs
+#ifndef VST_MINW_T128_BF
+#define VST_MINW_T128_BF 3
+#endif
+
+template <bool CF, bool GMK, int PR>
+static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
+  switch (cfg) {
+    case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
+    case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
+    case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
+    case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
+    case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2, PR><<<grid, NT, 0, st>>>(P); break;
+    case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P); break;
+    default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR><<<grid, NT, 0, st>>>(P); break;
+  }
+}
+
+template <int PR>
+void launch_prec(bool cfast, bool gm, int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (cfast)
+    gm ? launch_cfg<true, true, PR>(cfg, grid, st, P) : launch_cfg<true, false, PR>(cfg, grid, st, P);
+  else
+    gm ? launch_cfg<false, true, PR>(cfg, grid, st, P) : launch_cfg<false, false, PR>(cfg, grid, st, P);
+}
+
+
+extern template void launch_prec<0>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_prec<1>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_prec<2>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
+
+}  // namespace vstk

@@ -132,6 +132,9 @@ __device__ __forceinline__ void mfma_bf16_ktile(f32x16 (&acc)[TM][TN], float (*A
     bh[j] = *reinterpret_cast<const bf16x8_t*>(p);
     if (PREC == 1) bl[j] = *reinterpret_cast<const bf16x8_t*>(p + 8);
   }
+  // every fragment read is issued before the first MFMA: the chain then waits on counted
+  // lgkmcnt instead of re-reading into one register between MFMAs
+  __builtin_amdgcn_sched_barrier(0);
   if (PREC == 1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -146,6 +149,20 @@ __device__ __forceinline__ void mfma_bf16_ktile(f32x16 (&acc)[TM][TN], float (*A
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+}
+
+// A wave-uniform pointer forced into SGPRs: a buffer descriptor built from a pointer the compiler
+// keeps in VGPRs (e.g. after a 64-bit VALU multiply) makes every buffer load a waterfall loop.
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (void*)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), (short)0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
 }
 
 // Dispatch hands workgroups to the 8 XCDs round-robin (bid % 8, a speed assumption only):

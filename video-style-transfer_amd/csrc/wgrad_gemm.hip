@@ -28,7 +28,10 @@ struct WgParams {
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
-template <int WM, int TM, int WN, int TN, bool AV, int MINW, int PREC>
+// TAP: the block's columns are input channels of ONE tap (kh, kw) (grid.x = taps x channel
+// tiles), so the im2col offset of a pixel is computed once per pixel instead of once per
+// (pixel, column) -- the per-element index math otherwise dominates the bf16 MFMA loop.
+template <int WM, int TM, int WN, int TN, bool AV, int MINW, int PREC, bool TAP>
 __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -55,10 +58,17 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   // one split-K chunk share its A rows and source pixels, so they run on one XCD's L2
   const int gx = gridDim.x, gy = gridDim.y;
   const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
-  const int rest = wk / gx, bz = rest / gy;
-  const int j0 = (wk - rest * gx) * BN;
-  const int m0 = (rest - bz * gy) * BM;
-  const int n = bz / P.S;
+  // (readfirstlane: keep the block coordinates, and the buffer descriptors built from them, scalar)
+  const int rest = __builtin_amdgcn_readfirstlane(wk / gx), bz = __builtin_amdgcn_readfirstlane(rest / gy);
+  const int bx = wk - rest * gx;
+  const int j0 = __builtin_amdgcn_readfirstlane(bx * BN);
+  // TAP: bx = tap * nct + channel tile
+  const int nct = (P.Cs + BN - 1) / BN;
+  const int tap = TAP ? __builtin_amdgcn_readfirstlane(bx / nct) : 0;
+  const int ci0 = TAP ? __builtin_amdgcn_readfirstlane((bx - tap * nct) * BN) : 0;
+  const int tkh = TAP ? tap / P.KW : 0, tkw = TAP ? tap - (tap / P.KW) * P.KW : 0;
+  const int m0 = __builtin_amdgcn_readfirstlane((rest - bz * gy) * BM);
+  const int n = __builtin_amdgcn_readfirstlane(bz / P.S);
   const int sidx = bz - n * P.S;
   const int HWo = P.Ho * P.Wo;
   const int r_begin = sidx * P.chunk;
@@ -68,17 +78,22 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   const float* a_n = P.a + (long)n * a_img;
   const float* src_n = P.src + (long)n * P.Cs * plane;
   constexpr int OOR = 0x7ffffff0;
-  const __amdgpu_buffer_rsrc_t asrd = __builtin_amdgcn_make_buffer_rsrc((void*)a_n, (short)0, (int)(a_img * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t bsrd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)src_n, (short)0, (int)((long)P.Cs * plane * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)(a_img * 4));
+  const __amdgpu_buffer_rsrc_t bsrd = uniform_rsrc(src_n, (uint32_t)((long)P.Cs * plane * 4));
 
   const int rr = PREC ? (tid % (BK / 2)) * 2 : tid % BK;  // this thread's (first) pixel within a k-tile
   const int cc = PREC ? tid / (BK / 2) : tid / BK;        // base row / column
 
   // decode this thread's B columns once: (ci, kh, kw) packed, -1 if j >= J
+  // (TAP: the channel's plane offset in elements, -1 if ci >= Cs)
   int jdesc[NCOL];
 #pragma unroll
   for (int i = 0; i < NCOL; ++i) {
+    if (TAP) {
+      const int ci = ci0 + cc + i * CPT;
+      jdesc[i] = ci < P.Cs ? ci * plane : -1;
+      continue;
+    }
     int j = j0 + cc + i * CPT;
     int d = -1;
     if (j < P.J) {
@@ -141,6 +156,25 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       const bool rv = r < r_end;
       const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
       const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
+      if (TAP) {  // one source offset per pixel, shared by all of this thread's channels
+        int y = by + tkh, x = bx + tkw;
+        bool ok = rv;
+        if (P.gmode == 0) {
+          y = abs(y);
+          y = min(y, 2 * Hv - 2 - y);
+          x = abs(x);
+          x = min(x, 2 * Wv - 2 - x);
+        } else {
+          ok = ok && y >= 0 && y < Hv && x >= 0 && x < Wv;
+        }
+        const int off = (y >> sh) * P.Ws + (x >> sh);
+#pragma unroll
+        for (int i = 0; i < NCOL; ++i) {
+          const int vo = ok && jdesc[i] >= 0 ? (jdesc[i] + off) * 4 : OOR;
+          rb[i * PAIR + q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
+        }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < NCOL; ++i) {
         const int d = jdesc[i];
@@ -255,7 +289,12 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   float* slab = P.slab + (long)bz * P.Mpad * P.Jpad;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int jj = j0 + (wn * TN + j) * 32 + lo;
+    int jj = j0 + (wn * TN + j) * 32 + lo;
+    if (TAP) {
+      const int ci = ci0 + (wn * TN + j) * 32 + lo;
+      if (ci >= P.Cs) continue;
+      jj = tap * P.Cs + ci;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -320,33 +359,33 @@ __global__ void gram_reduce_kernel(const float* __restrict__ slab, float* __rest
   out[idx] = s * scale;
 }
 
-template <bool AV, int PR>
+template <bool AV, int PR, bool TAP>
 static void launch_wg_t(int c, dim3 g, hipStream_t st, const WgParams& P) {
   switch (c) {
-    case W32: wgrad_kernel<1, 1, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad_kernel<1, 2, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad_kernel<1, 3, 4, 1, AV, 4, PR><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad_kernel<2, 2, 2, 2, AV, 3, PR><<<g, NT, 0, st>>>(P); break;  // 4 per CU spills (128-VGPR cap)
-    default: wgrad_kernel<2, 3, 2, 2, AV, 2, PR><<<g, NT, 0, st>>>(P); break;
+    case W32: wgrad_kernel<1, 1, 4, 1, AV, 4, PR, TAP><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad_kernel<1, 2, 4, 1, AV, 4, PR, TAP><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad_kernel<1, 3, 4, 1, AV, 4, PR, TAP><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad_kernel<2, 2, 2, 2, AV, 3, PR, TAP><<<g, NT, 0, st>>>(P); break;  // 4 per CU spills (128-VGPR cap)
+    default: wgrad_kernel<2, 3, 2, 2, AV, 2, PR, TAP><<<g, NT, 0, st>>>(P); break;
   }
 }
 
 template <int PR>
-static void launch_wg_p(bool av, int c, dim3 g, hipStream_t st, const WgParams& P) {
-  if (av)
-    launch_wg_t<true, PR>(c, g, st, P);
+static void launch_wg_p(bool av, bool tap, int c, dim3 g, hipStream_t st, const WgParams& P) {
+  if (tap)
+    av ? launch_wg_t<true, PR, true>(c, g, st, P) : launch_wg_t<false, PR, true>(c, g, st, P);
   else
-    launch_wg_t<false, PR>(c, g, st, P);
+    av ? launch_wg_t<true, PR, false>(c, g, st, P) : launch_wg_t<false, PR, false>(c, g, st, P);
 }
 
-static void launch_wg(int c, dim3 g, hipStream_t st, const WgParams& P) {
+static void launch_wg(int c, bool tap, dim3 g, hipStream_t st, const WgParams& P) {
   // float4 A loads need 4 consecutive pixels in one row segment (and, for the row-split gather,
   // in one output row)
   const bool av = (P.Ho * P.Wo) % 4 == 0 && (!P.asplit || P.Wo % 4 == 0);
   switch (vst_gemm_mode_internal()) {
-    case VST_GEMM_F32: launch_wg_p<0>(av, c, g, st, P); break;
-    case VST_GEMM_BF16: launch_wg_p<2>(av, c, g, st, P); break;
-    default: launch_wg_p<1>(av, c, g, st, P); break;
+    case VST_GEMM_F32: launch_wg_p<0>(av, tap, c, g, st, P); break;
+    case VST_GEMM_BF16: launch_wg_p<2>(av, tap, c, g, st, P); break;
+    default: launch_wg_p<1>(av, tap, c, g, st, P); break;
   }
 }
 
@@ -409,8 +448,12 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
   P.fd_Wo = make_fastdiv(Wo);
   P.fd_Cs = make_fastdiv(Cs);
   P.fd_KW = make_fastdiv(KW);
-  dim3 g(P.Jpad / WBN, P.Mpad / wbm(c), N * S);
-  launch_wg(c, g, st, P);
+  // tap-uniform column tiles when the channels fill whole 128-column tiles (VGG / AdaAttN decoder
+  // widths; measured slower for the ReCoNet widths 48/96/192, whose padded tiles waste MFMAs)
+  const bool tap = !asplit && KH * KW > 1 && Cs % WBN == 0;
+  const int gxn = tap ? KH * KW * ((Cs + WBN - 1) / WBN) : P.Jpad / WBN;
+  dim3 g(gxn, P.Mpad / wbm(c), N * S);
+  launch_wg(c, tap, g, st, P);
   return vst_launch_status();
 }
 
