@@ -6,6 +6,8 @@ Tolerances (north_star: "within 1e-3 relative fp32"):
   * model forward vs golden: 1e-3 relative to the tensor's max magnitude;
   * loss terms: 1e-3 relative; gradients: per-tensor norm within 1e-3 (+1e-4 of the largest norm).
 """
+import zlib
+
 import numpy as np
 import pytest
 import torch
@@ -107,11 +109,18 @@ def gemm_mode(request):
 CONV_TOL = {"f32": 1e-4, "bf16x3": 1e-4, "bf16": 5e-2}
 
 
-def _mode_err(mode, a, b):
-    if mode != "bf16":
-        return rel_err(a, b)
+def _norm_err(a, b):
     a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _mode_err(mode, a, b, relu_grad=False):
+    """max-abs error for exact-ish arithmetic; a ReLU's backward under bf16 products can flip
+    the mask of a pre-activation within rounding of 0 (one element of the incoming gradient
+    changes), so those gradients -- and everything in bf16 -- are held to ||err|| / ||ref||."""
+    if mode == "bf16" or (relu_grad and mode != "f32"):
+        return _norm_err(a, b)
+    return rel_err(a, b)
 
 
 @pytest.mark.parametrize("case", CONV_CASES, ids=[f"{c[1]}-{c[4]}-k{c[5]}s{c[6]}{c[7][0]}u{c[8]}{c[9] or ''}" for c in CONV_CASES])
@@ -120,7 +129,7 @@ def test_conv_fwd_bwd(case, gemm_mode):
 
     tol = CONV_TOL[gemm_mode]
     N, Cin, H, W, Cout, k, stride, pad_mode, up, act = case
-    g = torch.Generator().manual_seed(hash(case) % 1000)
+    g = torch.Generator().manual_seed(zlib.crc32(repr(case).encode()) % 1000)  # stable across processes
     x = torch.randn(N, Cin, H, W, generator=g) * (40.0 if act == "tanh" else 1.0)
     w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
     b = torch.randn(Cout, generator=g) * 0.1
@@ -135,9 +144,11 @@ def test_conv_fwd_bwd(case, gemm_mode):
     assert y.shape == yr.shape
     assert _mode_err(gemm_mode, C(y), yr.detach()) < tol
     y.backward(G(gy))
-    assert _mode_err(gemm_mode, C(xg.grad), xr.grad) < tol
-    assert _mode_err(gemm_mode, C(wg.grad), wr.grad) < tol
-    assert _mode_err(gemm_mode, C(bg.grad), br.grad) < tol
+    rg = act == "relu"
+    gtol = 1e-3 if rg and gemm_mode == "bf16x3" else tol
+    assert _mode_err(gemm_mode, C(xg.grad), xr.grad, rg) < gtol
+    assert _mode_err(gemm_mode, C(wg.grad), wr.grad, rg) < gtol
+    assert _mode_err(gemm_mode, C(bg.grad), br.grad, rg) < gtol
 
 
 def test_conv_relu_frozen_weights_dgrad_mask():
