@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--gemm", default=os.environ.get("VST_GEMM_POLICY", "parity"),
-                    choices=("parity", "bf16x3", "f32", "bf16"),
+                    choices=("parity", "bf16x6", "bf16x3", "f32", "bf16"),
                     help="GEMM arithmetic policy (vst.ops.POLICIES): parity = bf16x3 split MFMA except the "
                          "stylizer forwards (fp32 MFMA); bf16x3 / f32 everywhere; bf16 = reduced precision")
     return ap.parse_args()
@@ -296,7 +296,7 @@ def main():
                          "achieved": achieved, "peak": ks["peak_tflops"], "unit": "TFLOP/s",
                          "frac": achieved / ks["peak_tflops"], "traffic": traffic,
                          "peak_note": "algorithmic fp32-operand TFLOP/s; peak = the launches' mix of MFMA peaks "
-                                      "(f32 157.3, bf16x3 2500/3, bf16 2500), flops / sum(flops_i / peak_i)",
+                                      "(f32 157.3, bf16x6 2500/6, bf16x3 2500/3, bf16 2500), flops / sum(flops_i / peak_i)",
                          "frac_of_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "by_mode": {ops.gemm_mode_name(m): v for m, v in ks["by_mode"].items()},
                          "traffic_source": traffic_src,

@@ -33,8 +33,11 @@ const char* vst_strerror(int code);
  *   0  exact fp32 MFMA (v_mfma_f32_32x32x2_f32);
  *   1  bf16x3 (default): fp32 operands split into hi + lo bf16, hi*hi + hi*lo + lo*hi on
  *      v_mfma_f32_32x32x16_bf16 with fp32 accumulation (per-product error <= ~2^-16 relative);
- *   2  bf16: hi*hi only (reduced precision, BASELINE config 5's half-precision MFMA path).
- * The initial mode comes from the environment variable VST_GEMM_MODE (f32 | bf16x3 | bf16). */
+ *   2  bf16: hi*hi only (reduced precision, BASELINE config 5's half-precision MFMA path);
+ *   3  bf16x6: three-way hi + mid + lo split, six products (fp32-level error, <= ~2^-24); its
+ *      packed operands are 1.5x the fp32 size (Kpad*Mpad*3/2 floats); the weight-gradient /
+ *      Gram / A*B^T kernels (no packed operand) run bf16x3 under it.
+ * The initial mode comes from the environment variable VST_GEMM_MODE (f32 | bf16x3 | bf16 | bf16x6). */
 int vst_set_gemm_mode(int mode);
 int vst_get_gemm_mode(void);
 

@@ -15,7 +15,7 @@ ref = F.conv2d(x.double(), w.double(), padding=1)
 a = torch.randn(2, 40, 300, generator=g)
 b = torch.randn(2, 56, 300, generator=g)
 refg = torch.bmm(a.double(), b.double().transpose(1, 2))
-for mode in ("f32", "bf16x3", "bf16"):
+for mode in ("f32", "bf16x6", "bf16x3", "bf16"):
     ops.set_gemm_mode(mode)
     y = ops.conv2d(x.cuda(), w.cuda(), None, pad=1).cpu().double()
     e = ((y - ref).abs().max() / ref.abs().max()).item()

@@ -57,13 +57,12 @@ def margin(tag):
 POLICIES = {
     "f32": ("f32", {}),
     "bf16x3": ("bf16x3", {}),
-    "bf16x3/fwd-f32": ("bf16x3", {"fwd": "f32"}),
-    "bf16x3/stylizer-f32": ("bf16x3", {"stylizer.fwd": "f32"}),
-    "bf16x3/img-f32": ("bf16x3", {"fwd_img": "f32"}),
-    "bf16x3/stylimg-f32": ("bf16x3", {"stylizer.fwd_img": "f32"}),
+    "bf16x6": ("bf16x6", {}),
+    "bf16x3/stylizer-f32": ("bf16x3", {"stylizer.fwd": "f32", "stylizer.fwd_img": "f32"}),
+    "bf16x3/stylizer-bf16x6": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6"}),
 }
 for name, (base, pol) in POLICIES.items():
     ops.set_gemm_mode(base, pol)
     for tag in ("b2", "b1r"):
         lm, gm, worst = margin(tag)
-        print(f"{name:20s} {tag:4s} loss margin {lm:.3f}  grad margin {gm:.3f} ({worst})", flush=True)
+        print(f"{name:24s} {tag:4s} loss margin {lm:.3f}  grad margin {gm:.3f} ({worst})", flush=True)

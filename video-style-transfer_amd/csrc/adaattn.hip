@@ -34,7 +34,7 @@ __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restric
   int m = (int)(t % Mpad), k = (int)(t / Mpad);
   float v = 0.f;
   if (m < M && k < K) v = transpose ? x[b * x_bs + (long)m * K + k] : x[b * x_bs + (long)k * M + m];
-  apack_store(out + b * per, k, m, Mpad, v, bsplit);
+  apack_store(out + b * per * (bsplit == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
 }
 
 // out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
@@ -333,7 +333,7 @@ int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int tran
   VST_CHECK_ARG(x && packed && B > 0 && M > 0 && K > 0 && Mpad >= M && Kpad >= K);
   long total = (long)B * Mpad * Kpad;
   pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, vst_gemm_mode_internal() != VST_GEMM_F32);
+      x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 

@@ -173,7 +173,7 @@ int vst_version(void) { return 101; }
 static int g_gemm_mode = -1;
 
 int vst_set_gemm_mode(int mode) {
-  VST_CHECK_ARG(mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16);
+  VST_CHECK_ARG(mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16 || mode == VST_GEMM_BF16X6);
   g_gemm_mode = mode;
   return VST_OK;
 }
@@ -200,19 +200,20 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && !(transposed && split_kh));
   long total = (long)Mpad * Kpad;
   pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad, Kpad, vst_gemm_mode_internal() != VST_GEMM_F32);
+      w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 
 }  // extern "C"
 
-// initial mode from the environment: VST_GEMM_MODE = f32 | bf16x3 (default) | bf16
+// initial mode from the environment: VST_GEMM_MODE = f32 | bf16x3 (default) | bf16 | bf16x6
 int vst_gemm_mode_internal() {
   if (g_gemm_mode < 0) {
     const char* e = getenv("VST_GEMM_MODE");
     int m = VST_GEMM_BF16X3;
     if (e && !strcmp(e, "f32")) m = VST_GEMM_F32;
     if (e && !strcmp(e, "bf16")) m = VST_GEMM_BF16;
+    if (e && !strcmp(e, "bf16x6")) m = VST_GEMM_BF16X6;
     g_gemm_mode = m;
   }
   return g_gemm_mode;
@@ -265,6 +266,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   switch (vst_gemm_mode_internal()) {
     case VST_GEMM_F32: launch_prec<0>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16: launch_prec<2>(cfast, gm, cfg, grid, st, P); break;
+    case VST_GEMM_BF16X6: launch_prec<3>(cfast, gm, cfg, grid, st, P); break;
     default: launch_prec<1>(cfast, gm, cfg, grid, st, P); break;
   }
   return vst_launch_status();
@@ -298,7 +300,7 @@ int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && (py == 0 || py == 1) && (px == 0 || px == 1));
   long total = (long)Mpad * Kpad;
   pack_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      w, packed, Cout, Cin, KS, py, px, Mpad, Kpad, vst_gemm_mode_internal() != VST_GEMM_F32);
+      w, packed, Cout, Cin, KS, py, px, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 
@@ -562,7 +564,7 @@ int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int 
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= Cin && Kpad >= (KS + 1) * (KS + 1) * Cout);
   long total = (long)Mpad * Kpad;
   pack_upsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, Mpad, Kpad,
-                                                                           vst_gemm_mode_internal() != VST_GEMM_F32);
+                                                                           apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 

@@ -82,7 +82,9 @@ template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PRE
 __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int A_F4 = BK * BM / 4;          // float4 per A tile
+  // A block per (k-tile, row): 16 fp32 / 16 hi + 16 lo bf16 (64 B); bf16x6: + 16 mid bf16 (96 B)
+  constexpr int AW = PREC == 3 ? 24 : 16;    // dwords per (k-tile, row)
+  constexpr int A_F4 = BM * AW / 4;          // float4 per A tile
   constexpr int A_PER = (A_F4 + NT - 1) / NT;
   constexpr int ROWSTEP = NT / BN;           // B rows covered per pass
   constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
@@ -94,7 +96,8 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(NT % BN == 0 && BK % ROWSTEP == 0, "tile");
 
   static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
-  constexpr int LS = 20;  // LDS row: [hi][s] 16 floats + 4 pad (conflict-free ds_read_b128 / ds_write_b128)
+  // LDS row: the A block + 4 pad dwords (20 or 28 dwords: conflict-free ds_read_b128 / ds_write_b128)
+  constexpr int LS = AW + 4;
   __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
 
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
-        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * 16 + 4 * a_slot(idx));
+        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * AW + 4 * (AW == 16 ? a_slot(idx) : idx));
       }
     }
     if (CFAST) {
@@ -204,14 +207,37 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     for (int i = 0; i < A_PER; ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
-        const int sl = a_slot(idx);
-        *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
+        if (AW == 16) {
+          const int sl = a_slot(idx);
+          *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
+        } else {
+          *reinterpret_cast<f32x4*>(&As[buf][idx / 6][(idx % 6) * 4]) = ra[i];
+        }
       }
     }
     float bv[B_PER];
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) bv[i] = GM ? (rg[i] > 0.f ? rb[i] : 0.f) : rb[i];
-    if constexpr (PREC != 0) {  // bf16 row: [hi k0..15][lo k0..15], this thread's k contiguous
+    if constexpr (PREC == 3) {  // bf16x6 row: [hi k0..15][mid k0..15][lo k0..15]
+      uint32_t h[B_PER / 2], m[B_PER / 2], l[B_PER / 2];
+#pragma unroll
+      for (int q = 0; q < B_PER / 2; ++q) split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
+      if constexpr (ROWSTEP == 2) {
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+          const uint32_t* v = part == 0 ? h : (part == 1 ? m : l);
+          *reinterpret_cast<u32x4*>(d + 8 * part + 4 * brow0) = u32x4{v[0], v[1], v[2], v[3]};
+        }
+      } else {
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+          const uint32_t* v = part == 0 ? h : (part == 1 ? m : l);
+          *reinterpret_cast<u32x4*>(d + 8 * part) = u32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<u32x4*>(d + 8 * part + 4) = u32x4{v[4], v[5], v[6], v[7]};
+        }
+      }
+    } else if constexpr (PREC != 0) {  // bf16 row: [hi k0..15][lo k0..15], this thread's k contiguous
       uint32_t h[B_PER / 2], l[B_PER / 2];
 #pragma unroll
       for (int q = 0; q < B_PER / 2; ++q) split_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
@@ -247,7 +273,9 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
-    if constexpr (PREC != 0) {
+    if constexpr (PREC == 3) {
+      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else if constexpr (PREC != 0) {
       mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
     } else {
       // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
@@ -375,5 +403,6 @@ void launch_prec(bool cfast, bool gm, int cfg, dim3 grid, hipStream_t st, const 
 extern template void launch_prec<0>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 extern template void launch_prec<1>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 extern template void launch_prec<2>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_prec<3>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 
 }  // namespace vstk

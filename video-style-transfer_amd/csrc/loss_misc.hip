@@ -207,7 +207,7 @@ __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict
     const float* gn = g + n * C * C;
     v = (gn[k * C + m] + gn[m * C + k]) * scale;
   }
-  apack_store(S + n * (long)Kpad * Mpad, k, m, Mpad, v, bsplit);
+  apack_store(S + n * (long)Kpad * Mpad * (bsplit == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
 }
 
 // ReLU backward: gx = gy * (y > 0)
@@ -359,7 +359,7 @@ int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, f
   VST_CHECK_ARG(g && S && N > 0 && C > 0 && Kpad >= C && Mpad >= C);
   long total = (long)N * Kpad * Mpad;
   symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale,
-                                                                           vst_gemm_mode_internal() != VST_GEMM_F32);
+                                                                           apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 

@@ -58,8 +58,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // GEMM arithmetic mode (library-global, see vst_set_gemm_mode in vst_hip.h)
-enum { VST_GEMM_F32 = 0, VST_GEMM_BF16X3 = 1, VST_GEMM_BF16 = 2 };
+enum { VST_GEMM_F32 = 0, VST_GEMM_BF16X3 = 1, VST_GEMM_BF16 = 2, VST_GEMM_BF16X6 = 3 };
 int vst_gemm_mode_internal();
+// packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6)
+static inline int apack_split(int mode) { return mode == VST_GEMM_F32 ? 0 : (mode == VST_GEMM_BF16X6 ? 2 : 1); }
 
 // Packed GEMM A operand ("weights"), k-tiles of 16: element (k, m) lives at
 //   ((k/16) * Mpad + m) * 16 + (k%2) * 8 + (k%16)/2
@@ -98,19 +100,35 @@ __device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uin
   lo = pack_bf16x2(a - ha, b - hb);
 }
 
+// three-way split: a = hi + mid + lo, residual ~2^-25 relative (bf16x6 mode)
+__device__ __forceinline__ void split3_bf16x2(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = pack_bf16x2(a, b);
+  const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
+  mid = pack_bf16x2(ra, rb);
+  lo = pack_bf16x2(ra - __uint_as_float(mid << 16), rb - __uint_as_float(mid & 0xffff0000u));
+}
+
 // Split packed A layout: the 16 k of one (k-tile, row m) block (64 bytes, the same footprint as
 // the fp32 block) hold 16 hi bf16 in natural k order, then the 16 lo bf16: an MFMA lane (k =
-// 8h + j) reads its hi and lo fragments with one ds_read_b128 each.
+// 8h + j) reads its hi and lo fragments with one ds_read_b128 each.  split == 2 (bf16x6): 96-byte
+// blocks [hi][mid][lo] (the pack buffer is 1.5x the fp32 one).
 __device__ __forceinline__ void apack_store(float* out, int k, int m, int Mpad, float v, int split) {
   if (!split) {
     out[apack_index(k, m, Mpad)] = v;
     return;
   }
-  unsigned short* u = reinterpret_cast<unsigned short*>(out + ((long)(k >> 4) * Mpad + m) * 16);
+  const int aw = split == 2 ? 24 : 16;
+  unsigned short* u = reinterpret_cast<unsigned short*>(out + ((long)(k >> 4) * Mpad + m) * aw);
   const uint32_t h = pack_bf16x2(v, 0.f) & 0xffffu;
-  const float l = v - __uint_as_float(h << 16);
+  const float r = v - __uint_as_float(h << 16);
+  const uint32_t md = pack_bf16x2(r, 0.f) & 0xffffu;
   u[k & 15] = (unsigned short)h;
-  u[16 + (k & 15)] = (unsigned short)(pack_bf16x2(l, 0.f) & 0xffffu);
+  if (split == 2) {
+    u[16 + (k & 15)] = (unsigned short)md;
+    u[32 + (k & 15)] = (unsigned short)(pack_bf16x2(r - __uint_as_float(md << 16), 0.f) & 0xffffu);
+  } else {
+    u[16 + (k & 15)] = (unsigned short)md;
+  }
 }
 
 // One 16-deep k-tile of a wave's TM x TN block of 32x32 accumulators from bf16 LDS rows
@@ -149,6 +167,42 @@ __device__ __forceinline__ void mfma_bf16_ktile(f32x16 (&acc)[TM][TN], float (*A
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+}
+
+// bf16x6: six products lo*hi + mid*mid + hi*lo + mid*hi + hi*mid + hi*hi (smallest first) of
+// three-way splits; the dropped terms are below 2^-24 of |a b| (fp32-like error)
+template <int TM, int TN, int LS>
+__device__ __forceinline__ void mfma_bf16x6_ktile(f32x16 (&acc)[TM][TN], float (*A)[LS], float (*B)[LS], int a0,
+                                                  int b0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8_t ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const float* p = &A[a0 + i * 32 + r][4 * h];
+    ah[i] = *reinterpret_cast<const bf16x8_t*>(p);
+    am[i] = *reinterpret_cast<const bf16x8_t*>(p + 8);
+    al[i] = *reinterpret_cast<const bf16x8_t*>(p + 16);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float* p = &B[b0 + j * 32 + r][4 * h];
+    bh[j] = *reinterpret_cast<const bf16x8_t*>(p);
+    bm[j] = *reinterpret_cast<const bf16x8_t*>(p + 8);
+    bl[j] = *reinterpret_cast<const bf16x8_t*>(p + 16);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f32x16 c = acc[i][j];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+    }
 }
 
 // A wave-uniform pointer forced into SGPRs: a buffer descriptor built from a pointer the compiler

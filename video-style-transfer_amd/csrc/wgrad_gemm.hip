@@ -385,7 +385,7 @@ static void launch_wg(int c, bool tap, dim3 g, hipStream_t st, const WgParams& P
   switch (vst_gemm_mode_internal()) {
     case VST_GEMM_F32: launch_wg_p<0>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg_p<2>(av, tap, c, g, st, P); break;
-    default: launch_wg_p<1>(av, tap, c, g, st, P); break;
+    default: launch_wg_p<1>(av, tap, c, g, st, P); break;  // bf16x3 (also under bf16x6: no packed operand here)
   }
 }
 

@@ -38,9 +38,10 @@ def packed_matrix(x, M, K, transpose, role="attn"):
     ops.gemm_role(role)
     N = x.shape[0]
     Mpad, Kpad = ops.pack_dims(M, K)
-    ap = _empty((N * Kpad * Mpad,), x)
+    per = ops.pack_floats(Mpad, Kpad)
+    ap = _empty((N * per,), x)
     lib.vst_pack_matrix(ptr(x), ptr(ap), N, M, K, int(transpose), Mpad, Kpad, M * K, stream())
-    return ap, Kpad * Mpad
+    return ap, per
 
 
 def bmm_at_b(x, M, K, transpose, b, P, out=None, role="attn"):

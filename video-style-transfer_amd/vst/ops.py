@@ -34,7 +34,7 @@ def _check(t, name, ndim=None):
     return t.contiguous()
 
 
-GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2}
+GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
 _BASE_MODE = [None]  # the mode chosen by the user (set_gemm_mode / VST_GEMM_MODE)
 _LIB_MODE = [None]   # the mode currently set in the library
 # per-role overrides of the base mode; roles: "fwd" (forward products), "dgrad" (data gradients,
@@ -46,15 +46,17 @@ def _mode_id(mode):
     return int(GEMM_MODES.get(mode, mode))
 
 
-# Named policies (base mode, per-role overrides).  "parity" (default): every GEMM on bf16x3
-# except the ones whose fp32 rounding the step's tests pin to the reference -- the stylizer
-# forwards (their outputs feed InstanceNorm, whose mean subtraction and ReLU decisions amplify
-# a 5e-6 relative product error into 0.1-1e-2 of a gradient element) and the softmax attention
-# (exp of raw dot products).  "bf16x3": every GEMM split (loss terms within 2e-6 of the
-# reference; gradients within ~1e-3 of their tensor norm).  "f32": exact fp32 MFMA everywhere.
-# "bf16": single bf16 products (the reduced-precision path of BASELINE config 5).
+# Named policies (base mode, per-role overrides).  "parity" (default): bf16x3 split MFMA for
+# every GEMM except the stylizer forwards, which run bf16x6 (three-way split, fp32-level error):
+# their outputs feed InstanceNorm, whose mean subtraction and ReLU decisions amplify a 5e-6
+# relative product error into 1e-3 of a gradient element's tensor norm; and the softmax
+# attention (exp of raw dot products) stays exact fp32.  "bf16x6": fp32-level products
+# everywhere (wgrad-kernel GEMMs bf16x3).  "bf16x3": every GEMM split in two (loss terms within
+# 2e-6 of the reference; gradient elements within ~1e-3 of their tensor norm).  "f32": exact
+# fp32 MFMA everywhere.  "bf16": single bf16 products (reduced-precision path of config 5).
 POLICIES = {
-    "parity": ("bf16x3", {"stylizer.fwd": "f32", "stylizer.fwd_img": "f32", "attn_softmax": "f32"}),
+    "parity": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6", "attn_softmax": "f32"}),
+    "bf16x6": ("bf16x6", {"attn_softmax": "f32"}),
     "bf16x3": ("bf16x3", {}),
     "f32": ("f32", {}),
     "bf16": ("bf16", {}),
@@ -133,6 +135,11 @@ def gemm_role(role):
     return m
 
 
+def pack_floats(Mpad, Kpad):
+    """Floats of one packed A operand in the current mode (bf16x6 blocks are 96 B, others 64 B)."""
+    return Kpad * Mpad * 3 // 2 if gemm_mode() == 3 else Kpad * Mpad
+
+
 def pack_dims(M, K):
     mp, kp = ctypes.c_int(), ctypes.c_int()
     lib.vst_conv_pack_dims(M, K, ctypes.byref(mp), ctypes.byref(kp))
@@ -165,7 +172,7 @@ def packed_weight(w, transposed, split_kh=False):
     else:
         M, K = (Cin, KH * KW * Cout) if transposed else (Cout, KH * KW * Cin)
     Mpad, Kpad = pack_dims(M, K)
-    out = _empty((Kpad * Mpad,), w)
+    out = _empty((pack_floats(Mpad, Kpad),), w)
     lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, stream())
     if not w.requires_grad:
         entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
@@ -234,7 +241,7 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
         dx = conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, 1, p, 1, algo_flops=flops)
     else:
         Mpad, Kpad = pack_dims(Cin, (ks + 1) * (ks + 1) * Cout)
-        wp = _empty((Kpad * Mpad,), w)
+        wp = _empty((pack_floats(Mpad, Kpad),), w)
         lib.vst_pack_weight_upsum(ptr(w), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
         dx = conv_gemm(gz, wp, Cin, ks + 1, H, W, GM_ZERO, 2, ks - 1 - p, 1, algo_flops=flops)
     Hv, Wv = H * up, W * up
@@ -262,7 +269,7 @@ def conv_dgrad_parity(gz, w, x_shape, ks, pad, gmask=None):
             view.zero_()
             continue
         Mpad, Kpad = pack_dims(Cin, nkh * nkw * Cout)
-        wp = _empty((Kpad * Mpad,), w)
+        wp = _empty((pack_floats(Mpad, Kpad),), w)
         lib.vst_pack_weight_parity(ptr(w), ptr(wp), Cout, Cin, ks, a, b, Mpad, Kpad, stream())
         conv_gemm(gz, wp, Cin, nkw, Hc[a], Wc[b], GM_TRANSPOSED, 1, 0, 1, out=view, gmask=gmask, kh=nkh)
     dx = _empty(x_shape, gz)
@@ -543,10 +550,10 @@ class GramFn(Function):
         (y,) = ctx.saved_tensors
         N, C, H, W = y.shape
         Mpad, Kpad = pack_dims(C, C)
-        S = _empty((N * Kpad * Mpad,), y)
+        S = _empty((N * pack_floats(Mpad, Kpad),), y)
         gemm_role("dgrad")
         lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, 1.0 / (C * H * W), stream())
-        dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=Kpad * Mpad)
+        dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=pack_floats(Mpad, Kpad))
         return dy.view(N, C, H, W)
 
 
