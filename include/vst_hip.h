@@ -69,15 +69,17 @@ int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const
  * (RC/network.py:169 deconv3 = ConvTanh(48, 3, 9): 27 GEMM rows instead of 3 padded to 32) */
 int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* aux, int N, int Cout, int KH, int H,
                         int W, int epi, void* stream);
-/* stride-2 data gradient by parity class (py, px) of the padded input grid: transposed pack of
- * the taps kh = py+2i, kw = px+2j (k = (i*nkw+j)*Cout + co, m = cin); each class is then a
- * stride-1 transposed vst_conv_gemm(pad=0, KH=nkh, KW=nkw) on the class grid, 4x fewer MACs than
- * zero-stuffing (RC/network.py:158-159 conv2/conv3 backward) */
-int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,
-                           void* stream);
-/* adjoint of ReflectionPad2d(pad) from the 4 class planes [(0,0),(0,1),(1,0),(1,1)][NC][Hc][Wc] */
-int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws, int pad, int accumulate,
-                            void* stream);
+/* stride-2 reflect-pad data gradient (RC/network.py:158-159 conv2/conv3 backward) as ONE
+ * transposed GEMM over all four parity phases of the padded input grid: GEMM row m = ci*4 + 2a + b
+ * computes padded pixel (2I+a, 2J+b) from the ceil(KS/2)^2 window dY[I-t][J-s] (A packed by
+ * vst_pack_weight_phase2: Mpad/Kpad from vst_conv_pack_dims(4*Cin, ceil(KS/2)^2*Cout)).  The
+ * epilogue writes interior pixels straight into dx [N][Cin][H][W] and the reflect-pad border into
+ * border [N][Cin][H+2p][W+2p] (only its border is written/read); vst_fold_border then adds the
+ * border's reflections into dx.  gmask (optional, dY-shaped) gates dY by (gmask > 0). */
+int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream);
+int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
+                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
+int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream);
 /* Reflect-pad dgrad without the padded grid (ConvLayer / UpsampleConvLayer backward,
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of

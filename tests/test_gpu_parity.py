@@ -66,6 +66,9 @@ CONV_CASES = [
     (2, 3, 20, 28, 48, 9, 1, "reflect", 1, None),     # ReCoNet conv1 (Cin=3 slow gather path)
     (2, 48, 16, 24, 96, 3, 2, "reflect", 1, None),    # conv2 (stride 2)
     (2, 96, 10, 12, 192, 3, 2, "reflect", 1, None),   # conv3
+    (1, 32, 15, 21, 64, 3, 2, "reflect", 1, None),    # stride 2, odd sizes (uneven parity phases)
+    (2, 16, 3, 5, 32, 3, 2, "reflect", 1, None),      # stride 2, 3-row input (border band = all rows)
+    (1, 16, 11, 13, 32, 5, 2, "reflect", 1, None),    # stride 2, k5 pad 2 (3x3 phase window)
     (2, 192, 9, 15, 192, 3, 1, "reflect", 1, None),   # residual conv, ragged
     (2, 192, 5, 8, 96, 3, 1, "reflect", 2, None),     # deconv1 (nearest x2 upsample)
     (1, 96, 9, 6, 48, 3, 1, "reflect", 2, None),      # deconv2

@@ -103,65 +103,61 @@ __global__ void fold_reflect_kernel(const float* __restrict__ dpad, float* __res
   }
 }
 
-// Stride-2 data gradient, parity class (py, px): only taps kh = py + 2i, kw = px + 2j reach
-// padded-input pixels (2yy+py, 2xx+px), and they read dY[yy - i][xx - j].  Packed as a
-// transposed A: k = (i*nkw + j)*Cout + co, m = ci.
-__global__ void pack_parity_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
-                                   int py, int px, int Mpad, int Kpad, int bsplit) {
+// Stride-2 data gradient, all four parity phases stacked in one transposed GEMM (EPI_PHASE2):
+// padded-input pixel (2I+a, 2J+b) receives taps kh = a + 2t, kw = b + 2s from dY[I-t][J-s], so with
+// the window t, s < ceil(KS/2) over dY the A operand is k = (t*KW2 + s)*Cout + co, m = ci*4 + 2a + b,
+// zero where a + 2t or b + 2s falls outside the kernel.
+__global__ void pack_phase2_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KS,
+                                   int Mpad, int Kpad, int bsplit) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)Mpad * Kpad) return;
   int m = (int)(idx % Mpad);
   int k = (int)(idx / Mpad);
-  const int nkh = (KS - py + 1) / 2, nkw = (KS - px + 1) / 2;
+  const int K2 = (KS + 1) / 2;
   float v = 0.f;
-  if (m < Cin && k < nkh * nkw * Cout) {
-    int tap = k / Cout, co = k % Cout;
-    int i = tap / nkw, j = tap % nkw;
-    v = w[(((long)co * Cin + m) * KS + py + 2 * i) * KS + px + 2 * j];
+  if (m < 4 * Cin && k < K2 * K2 * Cout) {
+    const int tap = k / Cout, co = k % Cout, t = tap / K2, sx = tap % K2;
+    const int ci = m >> 2, kh = ((m >> 1) & 1) + 2 * t, kw = (m & 1) + 2 * sx;
+    if (kh < KS && kw < KS) v = w[(((long)co * Cin + ci) * KS + kh) * KS + kw];
   }
   apack_store(out, k, m, Mpad, v, bsplit);
 }
 
-// fold_reflect over the 4 parity-class planes [class (a,b)][NC][Hc_a][Wc_b] of the padded grid
-struct Cls4 {
-  const float *c00, *c01, *c10, *c11;
-  int w0, w1;
-};
-__device__ __forceinline__ float parity_at(const Cls4& c, int yp, int xp) {
-  const bool ya = yp & 1, xb = xp & 1;
-  const float* base = ya ? (xb ? c.c11 : c.c10) : (xb ? c.c01 : c.c00);
-  return base[(yp >> 1) * (xb ? c.w1 : c.w0) + (xp >> 1)];
-}
-
-// grid: x over the pixels of one plane, y over planes (grid-stride)
-__global__ void fold_reflect_parity_kernel(const float* __restrict__ cls, float* __restrict__ dx, int NC, int Hs,
-                                           int Ws, int pad, int accumulate) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= Hs * Ws) return;
-  const int xs = p % Ws, ys = p / Ws;
+// dx (+)= the reflect-pad border of the padded-grid gradient (the interior went straight to dx):
+// one thread per element of dx's border band (rows/cols within pad+1 of an edge)
+__global__ void fold_border_kernel(const float* __restrict__ border, float* __restrict__ dx, int NC, int Hs, int Ws,
+                                   int pad) {
+  const int nb = pad < Hs / 2 ? pad + 1 : Hs;  // band rows at each edge (rows 0..pad and Hs-1-pad..Hs-1)
+  const int band_rows = nb >= Hs ? Hs : 2 * nb;
+  const int nbc = pad < Ws / 2 ? pad + 1 : Ws;
+  const int band_cols = nbc >= Ws ? Ws : 2 * nbc;
+  const long per_plane = (long)band_rows * Ws + (long)(Hs - band_rows) * band_cols;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= per_plane * NC) return;
+  const int nc = (int)(idx / per_plane);
+  int q = (int)(idx - (long)nc * per_plane), y, x;
+  if (q < band_rows * Ws) {
+    const int r = q / Ws;
+    x = q - r * Ws;
+    y = (band_rows == Hs || r < nb) ? r : Hs - band_rows + r;
+  } else {
+    q -= band_rows * Ws;
+    const int r = q / band_cols, c = q - r * band_cols;
+    y = nb + r;
+    x = (band_cols == Ws || c < nbc) ? c : Ws - band_cols + c;
+  }
   const int Hp = Hs + 2 * pad, Wp = Ws + 2 * pad;
-  const int Hc0 = (Hp + 1) / 2, Hc1 = Hp / 2;
-  const int Wc0 = (Wp + 1) / 2, Wc1 = Wp / 2;
-  const long s01 = (long)NC * Hc0 * Wc0, s10 = s01 + (long)NC * Hc0 * Wc1, s11 = s10 + (long)NC * Hc1 * Wc0;
-  const Src3 ry = reflect_sources(ys, Hs, pad), cx = reflect_sources(xs, Ws, pad);
-  for (int nc = blockIdx.y; nc < NC; nc += gridDim.y) {
-    const Cls4 c = {cls + (long)nc * Hc0 * Wc0, cls + s01 + (long)nc * Hc0 * Wc1, cls + s10 + (long)nc * Hc1 * Wc0,
-                    cls + s11 + (long)nc * Hc1 * Wc1, Wc0, Wc1};
-    float s = 0.f;
-#define VST_ROW(yp)                                         \
-  {                                                         \
-    s += parity_at(c, yp, cx.a);                        \
-    if (cx.b >= 0) s += parity_at(c, yp, cx.b);         \
-    if (cx.c >= 0) s += parity_at(c, yp, cx.c);         \
-  }
-    VST_ROW(ry.a);
-    if (ry.b >= 0) VST_ROW(ry.b);
-    if (ry.c >= 0) VST_ROW(ry.c);
-#undef VST_ROW
-    float* o = dx + (long)nc * Hs * Ws + p;
-    if (accumulate) s += *o;
-    *o = s;
-  }
+  const float* b = border + (long)nc * Hp * Wp;
+  const Src3 ry = reflect_sources(y, Hs, pad), cx = reflect_sources(x, Ws, pad);
+  // every (row source, column source) pair except (direct, direct) is a border position
+  float s = 0.f;
+  const int us[3] = {ry.a, ry.b, ry.c}, vs[3] = {cx.a, cx.b, cx.c};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if ((i | j) && us[i] >= 0 && vs[j] >= 0) s += b[(long)us[i] * Wp + vs[j]];
+  dx[((long)nc * Hs + y) * Ws + x] += s;
 }
 
 }  // namespace
@@ -224,8 +220,13 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
                             int stride, int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux,
                             const float* gmask, void* stream, const float* ep_ra = nullptr,
                             const float* ep_rb = nullptr, const float* ep_rd = nullptr,
-                            const float* ep_cg = nullptr) {
+                            const float* ep_cg = nullptr, float* ph_border = nullptr, int ph_H = 0, int ph_W = 0,
+                            int ph_pad = 0) {
   ConvParams P;
+  P.ph_border = ph_border;
+  P.ph_H = ph_H;
+  P.ph_W = ph_W;
+  P.ph_pad = ph_pad;
   P.src = src;
   P.wpack = wpack;
   P.bias = bias;
@@ -295,20 +296,34 @@ int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K
                           EPI_AFFINE, a_batch_stride, nullptr, nullptr, stream, ra, rb, rd, cg);
 }
 
-int vst_pack_weight_parity(const float* w, float* packed, int Cout, int Cin, int KS, int py, int px, int Mpad, int Kpad,
+int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad,
                            void* stream) {
-  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && (py == 0 || py == 1) && (px == 0 || px == 1));
+  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= 4 * Cin);
+  VST_CHECK_ARG(Kpad >= (KS + 1) / 2 * ((KS + 1) / 2) * Cout);
   long total = (long)Mpad * Kpad;
-  pack_parity_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      w, packed, Cout, Cin, KS, py, px, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
+  pack_phase2_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+      w, packed, Cout, Cin, KS, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
   return vst_launch_status();
 }
 
-int vst_fold_reflect_parity(const float* cls, float* dx, long NC, int Hs, int Ws, int pad, int accumulate,
-                            void* stream) {
-  VST_CHECK_ARG(cls && dx && NC > 0 && Hs > 0 && Ws > 0 && pad >= 0 && pad < Hs && pad < Ws);
-  dim3 g(ceil_div((long)Hs * Ws, 256), (unsigned)(NC < 65535 ? NC : 65535));
-  fold_reflect_parity_kernel<<<g, 256, 0, (hipStream_t)stream>>>(cls, dx, (int)NC, Hs, Ws, pad, accumulate);
+int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
+                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream) {
+  VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Ho > 0 && Wo > 0 && Cin > 0 && KS > 0);
+  VST_CHECK_ARG(pad >= 0 && pad < H && pad < W && Ho == (H + 2 * pad - KS) / 2 + 1 && Wo == (W + 2 * pad - KS) / 2 + 1);
+  const int K2 = (KS + 1) / 2;
+  const int Hc = (H + 2 * pad + 1) / 2, Wc = (W + 2 * pad + 1) / 2;
+  return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, 4 * Cin, K2 * K2 * Cout, Hc, Wc, K2, K2,
+                          GM_TRANSPOSED, 1, 0, 0, 1, EPI_PHASE2, 0, nullptr, gmask, stream, nullptr, nullptr, nullptr,
+                          nullptr, border, H, W, pad);
+}
+
+int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream) {
+  VST_CHECK_ARG(border && dx && NC > 0 && H > 0 && W > 0 && pad >= 0 && pad < H && pad < W);
+  if (pad == 0) return VST_OK;
+  const int nb = pad < H / 2 ? pad + 1 : H, nbc = pad < W / 2 ? pad + 1 : W;
+  const int br = nb >= H ? H : 2 * nb, bc = nbc >= W ? W : 2 * nbc;
+  const long total = ((long)br * W + (long)(H - br) * bc) * NC;
+  fold_border_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(border, dx, (int)NC, H, W, pad);
   return vst_launch_status();
 }
 

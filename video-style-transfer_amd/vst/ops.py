@@ -219,7 +219,7 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
     if pad_mode != "reflect":
         raise VstError("dgrad: zero padding with upsampling is not on the reference path")
     if stride == 2 and up == 1:
-        return conv_dgrad_parity(gz, w, x_shape, ks, pad, gmask)
+        return conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask, flops)
     if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
         return conv_dgrad_ring(gz, w, x_shape, ks, up, flops)
     Hp, Wp = H * up + 2 * pad, W * up + 2 * pad
@@ -251,29 +251,25 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
     return dx
 
 
-def conv_dgrad_parity(gz, w, x_shape, ks, pad, gmask=None):
-    """Stride-2 reflect-pad conv input gradient as 4 parity-class stride-1 GEMMs (no zero taps)."""
+def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
+    """Stride-2 reflect-pad conv input gradient: one transposed GEMM over the 4 parity phases of
+    the padded grid (rows ci*4 + phase), interior written straight into dx, border folded after."""
     N, Cin, H, W = x_shape
-    Cout = w.shape[0]
-    Hp, Wp = H + 2 * pad, W + 2 * pad
-    Hc, Wc = ((Hp + 1) // 2, Hp // 2), ((Wp + 1) // 2, Wp // 2)
-    classes = [(a, b) for a in (0, 1) for b in (0, 1)]
-    sizes = [N * Cin * Hc[a] * Wc[b] for a, b in classes]
-    cls = _empty((sum(sizes),), gz)
-    off = 0
-    for (a, b), sz in zip(classes, sizes):
-        nkh, nkw = (ks - a + 1) // 2, (ks - b + 1) // 2
-        view = cls[off:off + sz].view(N, Cin, Hc[a], Wc[b])
-        off += sz
-        if nkh * nkw == 0:
-            view.zero_()
-            continue
-        Mpad, Kpad = pack_dims(Cin, nkh * nkw * Cout)
-        wp = _empty((pack_floats(Mpad, Kpad),), w)
-        lib.vst_pack_weight_parity(ptr(w), ptr(wp), Cout, Cin, ks, a, b, Mpad, Kpad, stream())
-        conv_gemm(gz, wp, Cin, nkw, Hc[a], Wc[b], GM_TRANSPOSED, 1, 0, 1, out=view, gmask=gmask, kh=nkh)
+    Cout, Ho, Wo = w.shape[0], gz.shape[2], gz.shape[3]
+    k2 = (ks + 1) // 2
+    Mpad, Kpad = pack_dims(4 * Cin, k2 * k2 * Cout)
+    wp = _empty((pack_floats(Mpad, Kpad),), w)
+    lib.vst_pack_weight_phase2(ptr(w.contiguous()), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
     dx = _empty(x_shape, gz)
-    lib.vst_fold_reflect_parity(ptr(cls), ptr(dx), N * Cin, H, W, pad, 0, stream())
+    border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
+    Hc, Wc = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
+    tok = kprof.begin(flops if flops is not None else 2.0 * N * Cout * Ho * Wo * Cin * ks * ks,
+                      4.0 * (gz.numel() + wp.numel() + dx.numel()),
+                      (N, Cout, Ho, Wo, 4 * Cin, Hc, Wc, k2, k2, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
+    lib.vst_conv_dgrad_s2(ptr(gz), ptr(wp), ptr(gmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
+                          stream())
+    kprof.end(tok)
+    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
 
 
