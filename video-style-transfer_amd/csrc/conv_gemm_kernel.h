@@ -157,6 +157,12 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   const __amdgpu_buffer_rsrc_t gsrd = uniform_rsrc(GM ? gm_n : src_n, src_bytes);
   const int ntiles = P.Kpad / BK;
 
+  // CFAST tap walk: tiles are loaded in k order, so the (tap, channel) position advances by 16
+  // channels per tile and the gather offset is decoded once per tap (wave-uniform branch), not once
+  // per k-tile
+  int st_tap = 0, st_c0 = 0, st_vbase = 0;
+  bool st_ok = false;
+
   // Issue every global load of tile t without branches (out-of-range taps read a clamped, valid
   // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
   auto load_tile = [&](int t) {
@@ -172,23 +178,26 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
       // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
       // offset per thread per group; out-of-range taps use an offset past the buffer end, which
       // the buffer-load range check turns into 0 (no branch, no select)
-      constexpr int NG = BK / 16, PER_G = B_PER / NG;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const int kg = k0 + 16 * g;
-        // wave-uniform tap decode by multiply-shift (SALU), not by integer division
-        const int tap = (int)fdiv((uint32_t)kg, P.fd_Cs);
-        const int c0 = kg - tap * P.Cs;
-        const int kh = (int)fdiv((uint32_t)tap, P.fd_KW), kw = tap - kh * P.KW;
+      // (Cs % 16 == 0, so K = taps * Cs is a whole number of tiles and every tile is in range)
+      static_assert(BK == 16, "one tap per k-tile");
+      (void)k0;
+      if (st_c0 == 0) {
+        const int kh = (int)fdiv((uint32_t)st_tap, P.fd_KW), kw = st_tap - kh * P.KW;
         const int off0 = gather_offset(P, oy, ox, kh, kw);
-        const bool ok = pvalid && kg < P.K && off0 >= 0;
-        const int vo = ok ? ((c0 + (PREC ? brow0 * PER_G : brow0)) * plane_i + off0) * 4 : OOR;
-        const int vstep = ok ? KSTEP * plane_i * 4 : 0;
+        st_ok = pvalid && off0 >= 0;
+        st_vbase = ((PREC ? brow0 * B_PER : brow0) * plane_i + off0) * 4;
+      }
+      const int vo = st_ok ? st_vbase + st_c0 * plane_i * 4 : OOR;
+      const int vstep = st_ok ? KSTEP * plane_i * 4 : 0;
 #pragma unroll
-        for (int i = 0; i < PER_G; ++i) {
-          rb[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
-          if (GM) rg[g * PER_G + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo + i * vstep, 0, 0));
-        }
+      for (int i = 0; i < B_PER; ++i) {
+        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
+        if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo + i * vstep, 0, 0));
+      }
+      st_c0 += 16;
+      if (st_c0 == P.Cs) {
+        st_c0 = 0;
+        ++st_tap;
       }
     } else {
 #pragma unroll
