@@ -15,7 +15,7 @@ fi
 if [ "$what" == "pmc" ] || [ "$what" == "all" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 500 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_${model}_$c -o run -- \
-      python3 bench.py --model $model --steps 1 --warmup 1 --no-cpu-baseline --no-vgg19 > gpurun_out/pmc_${model}_$c.log 2>&1 \
+      python3 bench.py --model $model --steps 1 --warmup 1 --no-cpu-baseline --no-vgg19 --gemm ${GEMM:-parity} > gpurun_out/pmc_${model}_$c.log 2>&1 \
       || { echo "pmc $c pass failed rc=$?"; exit 4; }
   done
 fi

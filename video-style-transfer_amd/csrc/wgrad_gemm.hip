@@ -84,6 +84,12 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   const int rr = PREC ? (tid % (BK / 2)) * 2 : tid % BK;  // this thread's (first) pixel within a k-tile
   const int cc = PREC ? tid / (BK / 2) : tid / BK;        // base row / column
 
+  // CONS (Cs % NCOL == 0, wave-uniform): this thread's NCOL columns are consecutive channels of
+  // one tap (LDS rows cc*NCOL + i), so each pixel's reflect/zero index math is done once for all
+  // of them; otherwise the columns are cc + i*CPT, each decoded on its own.
+  const bool cons = !TAP && P.Cs % NCOL == 0;
+  const int crow0 = cons ? cc * NCOL : cc, cstep = cons ? 1 : CPT;
+
   // decode this thread's B columns once: (ci, kh, kw) packed, -1 if j >= J
   // (TAP: the channel's plane offset in elements, -1 if ci >= Cs)
   int jdesc[NCOL];
@@ -94,7 +100,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       jdesc[i] = ci < P.Cs ? ci * plane : -1;
       continue;
     }
-    int j = j0 + cc + i * CPT;
+    int j = j0 + crow0 + i * cstep;
     int d = -1;
     if (j < P.J) {
       int tap = (int)fdiv((uint32_t)j, P.fd_Cs);
@@ -175,6 +181,26 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
         }
         continue;
       }
+      if (cons) {  // one tap for all of this thread's columns (J % NCOL == 0: all valid or none)
+        const int d = jdesc[0];
+        const int ci = d & 0xffff, kh = (d >> 16) & 0xff, kw = d >> 24;
+        int y = by + kh, x = bx + kw;
+        bool ok = rv && d >= 0;
+        if (P.gmode == 0) {
+          y = abs(y);
+          y = min(y, 2 * Hv - 2 - y);
+          x = abs(x);
+          x = min(x, 2 * Wv - 2 - x);
+        } else {
+          ok = ok && y >= 0 && y < Hv && x >= 0 && x < Wv;
+        }
+        const int vo = ok ? (ci * plane + (y >> sh) * P.Ws + (x >> sh)) * 4 : OOR;
+        const int vstep = ok ? plane * 4 : 0;
+#pragma unroll
+        for (int i = 0; i < NCOL; ++i)
+          rb[i * PAIR + q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + i * vstep, 0, 0));
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < NCOL; ++i) {
         const int d = jdesc[i];
@@ -212,7 +238,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
         for (int i = 0; i < NAR; ++i) As[buf][cc + i * CPT][(rr & 1) * 8 + (rr >> 1)] = ras[i];
       }
 #pragma unroll
-      for (int i = 0; i < NCOL; ++i) Bs[buf][cc + i * CPT][(rr & 1) * 8 + (rr >> 1)] = rb[i];
+      for (int i = 0; i < NCOL; ++i) Bs[buf][crow0 + i * cstep][(rr & 1) * 8 + (rr >> 1)] = rb[i];
     } else {  // bf16 rows [hi px 0..15][lo px 0..15]
       if constexpr (AV) {
 #pragma unroll
@@ -242,7 +268,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       for (int i = 0; i < NCOL; ++i) {
         uint32_t h, l;
         split_bf16x2(rb[2 * i], rb[2 * i + 1], h, l);
-        uint32_t* row = reinterpret_cast<uint32_t*>(&Bs[buf][cc + i * CPT][0]);
+        uint32_t* row = reinterpret_cast<uint32_t*>(&Bs[buf][crow0 + i * cstep][0]);
         row[rr >> 1] = h;
         if (PREC == 1) row[8 + (rr >> 1)] = l;
       }
