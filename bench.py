@@ -269,8 +269,9 @@ def main():
                         f"3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}")
             data = "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights"
         else:
-            metric = "training frame-pairs/sec at 256\u00d7512, AdaAttN train_video step (VGG19 encoder/loss)"
-            workload = (f"config4 shape: AdaAttN train_video step (cosine attention, gs+lf+is losses), "
+            metric = f"training frame-pairs/sec at {H}\u00d7{W}, AdaAttN train_video step (VGG19 encoder/loss)"
+            shape = "config5 shape" if (H, W, B) == (512, 1024, 8) else "config4 shape"
+            workload = (f"{shape}: AdaAttN train_video step (cosine attention, gs+lf+is losses), "
                         f"B={B} (content1, content2, style) triples/GPU, 3x{H}x{W}")
             data = "synthetic (numpy PCG64 images U[0,255)); random-init weights"
         result = {

@@ -8,6 +8,8 @@
 // pixels r of ONE image per block (grid.z = N * S splits); partial slabs are summed by
 // `wgrad_reduce` (into PyTorch's [co][ci][kh][kw] order) or `gram_reduce` (per image, scaled),
 // which keeps the result deterministic (no float atomics).
+#include <cstdlib>
+
 #include "vst_common.h"
 #include "vst_hip.h"
 
@@ -487,7 +489,10 @@ static int splits_for(int N, int M, long J, int HWo) {
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
   long Jpad = (J + WBN - 1) / WBN * WBN;
-  return plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo, c, Mpad, Jpad);
+  static const int smul = getenv("VST_WGRAD_SMUL") ? atoi(getenv("VST_WGRAD_SMUL")) : 1;  // tuning experiments
+  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo, c, Mpad, Jpad) * (smul > 0 ? smul : 1);
+  const int maxs = (HWo + 2 * BK - 1) / (2 * BK);
+  return S < maxs ? S : (maxs > 0 ? maxs : 1);
 }
 
 }  // namespace
