@@ -80,6 +80,12 @@ int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int
 int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
                       int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
 int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream);
+/* stride-1 reflect-pad data gradient (ResidualBlock / ConvTanh backward, RC/network.py:72-75,
+ * 145-150, 83-85): the transposed GEMM (A = vst_pack_weight(transposed=1)) runs over the padded
+ * grid (H+2p) x (W+2p); interior pixels go straight into dx, the p-wide border into border
+ * [N][Cin][H+2p][W+2p]; then vst_fold_border. */
+int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,
+                          int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
 /* Reflect-pad dgrad without the padded grid (ConvLayer / UpsampleConvLayer backward,
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of

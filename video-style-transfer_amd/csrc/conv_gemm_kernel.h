@@ -36,14 +36,16 @@ struct ConvParams {
   const float *ep_ra, *ep_rb, *ep_rd, *ep_cg;
   // EPI_PHASE2 (stride-2 data gradient, all four parity phases in one GEMM): row m = ci*4 + 2a + b,
   // pixel (I, J) of the phase grid -> padded-grid position (2I + a, 2J + b); interior positions go
-  // straight to dx [N][M/4][ph_H][ph_W], the reflect-pad border to ph_border [N][M/4][Hp][Wp]
+  // straight to dx [N][M/4][ph_H][ph_W], the reflect-pad border to ph_border [N][M/4][Hp][Wp].
+  // EPI_PADOUT (stride-1 data gradient over the padded grid): row m = ci, pixel (u, v) of the
+  // padded grid, same interior / border split.
   float* ph_border;
   int ph_H, ph_W, ph_pad;
   FastDiv fd_Wo, fd_Cs, fd_KW;
 };
 
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
-enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32, EPI_PHASE2 = 64 };
+enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32, EPI_PHASE2 = 64, EPI_PADOUT = 128 };
 
 // source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
 // (select-only arithmetic: no divergent branches inside the k loop)
@@ -322,9 +324,10 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* out_n = P.out + (long)n * P.M * HWo;
   const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
-  if (P.epi & EPI_PHASE2) {
-    // the 4 consecutive rows of a C-register group are the 4 phases of one channel
-    const int Cx = P.M >> 2, Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
+  if (P.epi & (EPI_PHASE2 | EPI_PADOUT)) {
+    // PHASE2: the 4 consecutive rows of a C-register group are the 4 phases of one channel
+    const bool ph2 = P.epi & EPI_PHASE2;
+    const int Cx = ph2 ? P.M >> 2 : P.M, Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
     float* dx_n = P.out + (long)n * Cx * P.ph_H * P.ph_W;
     float* bd_n = P.ph_border + (long)n * Cx * Hp * Wp;
 #pragma unroll
@@ -332,15 +335,30 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
       const int pp = p0 + (wn * TN + j) * 32 + lo;
       if (pp >= HWo) continue;
       const int I = (int)fdiv((uint32_t)pp, P.fd_Wo), J = pp - I * P.Wo;
+      if (!ph2) {  // one padded-grid pixel per column: one interior/border decision for all rows
+        const int y = I - P.ph_pad, x = J - P.ph_pad;
+        const bool in = y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W;
+        float* base = in ? dx_n + (long)y * P.ph_W + x : bd_n + (long)I * Wp + J;
+        const long cstride = in ? (long)P.ph_H * P.ph_W : (long)Hp * Wp;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ci = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (ci < Cx) base[ci * cstride] = acc[i][j][r];
+          }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int ci = (m0 + (wm * TM + i) * 32 + 8 * g + 4 * hi) >> 2;
-          if (ci >= Cx) continue;
+          const int mb = m0 + (wm * TM + i) * 32 + 8 * g + 4 * hi;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int u = 2 * I + (r >> 1), v = 2 * J + (r & 1);
+            const int ci = ph2 ? mb >> 2 : mb + r;
+            const int u = ph2 ? 2 * I + (r >> 1) : I, v = ph2 ? 2 * J + (r & 1) : J;
+            if (ci >= Cx) continue;
             const int y = u - P.ph_pad, x = v - P.ph_pad;
             const float val = acc[i][j][4 * g + r];
             if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W)

@@ -220,6 +220,8 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
         raise VstError("dgrad: zero padding with upsampling is not on the reference path")
     if stride == 2 and up == 1:
         return conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask, flops)
+    if stride == 1 and up == 1 and gmask is None and 0 < pad < min(H, W):
+        return conv_dgrad_padout(gz, w, x_shape, ks, pad, flops)
     if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
         return conv_dgrad_ring(gz, w, x_shape, ks, up, flops)
     Hp, Wp = H * up + 2 * pad, W * up + 2 * pad
@@ -227,6 +229,22 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
                      algo_flops=flops)
     dx = _empty(x_shape, gz)
     lib.vst_fold_reflect(ptr(dpad), ptr(dx), N * Cin, H, W, pad, up, 0, stream())
+    return dx
+
+
+def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops):
+    """Stride-1 reflect-pad conv input gradient: the transposed GEMM over the padded grid writes
+    its interior straight into dx and its border into a side buffer, folded into dx's border band."""
+    N, Cin, H, W = x_shape
+    Cout, Ho, Wo = w.shape[0], gz.shape[2], gz.shape[3]
+    wp = packed_weight(w, transposed=True)
+    dx = _empty(x_shape, gz)
+    border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
+    tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
+                      (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
+    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad, stream())
+    kprof.end(tok)
+    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
 
 
