@@ -80,6 +80,26 @@ int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int
 int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
                       int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
 int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream);
+/* Thin-channel convolutions (RC/network.py:155 conv1 = ConvLayer(3, 48, 9), :169 deconv3 =
+ * ConvTanh(48, 3, 9) backward, VGG conv1_1): a tensor with C*K <= Cu channels is kw-unfolded,
+ *   out[n][c*K + kw][y][v] = src[n][c][y][v + sgn*kw + off]  (reflect or zero outside; zero channels
+ *   past C*K), Cu a multiple of 16,
+ * so the conv becomes a Kx1 conv over Cu channels on the 16-channel k-tile path:
+ *   forward:  vst_unfold_kw(x, sgn=+1, off=-pad, Wout=W) then vst_conv_gemm_padx(KH=K, KW=1,
+ *             pad_x=0) with A from vst_pack_weight_kwu(transposed=0);
+ *   dgrad (thin Cout, stride 1): vst_unfold_kw(dy, sgn=-1, off=0, Wout=W+2p, zero) then
+ *             vst_conv_dgrad_padout_kwu with A from vst_pack_weight_kwu(transposed=1), then
+ *             vst_fold_border. */
+int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int Wout, int K, int Cu, int sgn, int off,
+                  int reflect, void* stream);
+int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K, int Cu, int transposed, int Mpad,
+                        int Kpad, void* stream);
+int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
+                       int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
+                       int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
+                       void* stream);
+int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
+                              int Cin, int H, int W, int KS, int pad, void* stream);
 /* stride-1 reflect-pad data gradient (ResidualBlock / ConvTanh backward, RC/network.py:72-75,
  * 145-150, 83-85): the transposed GEMM (A = vst_pack_weight(transposed=1)) runs over the padded
  * grid (H+2p) x (W+2p); interior pixels go straight into dx, the p-wide border into border
@@ -142,6 +162,13 @@ int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int 
  * warp_bwd scatters with float atomics into gx (zero it first or accumulate). */
 int vst_warp_fwd(const float* x, const float* flo, float* out, int B, int C, int H, int W, void* stream);
 int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, int H, int W, void* stream);
+/* warp backward in gather form (no float atomics on the gradient): the bilinear taps are inverted
+ * per image into per-source-pixel lists in `workspace` (vst_warp_bwd_workspace bytes), then each
+ * source pixel sums its entries over all channels; gx is overwritten (accumulate=0) or added to.
+ * Sources hit by more than 8 taps (strongly converging flow) take an atomic pass for the excess. */
+long vst_warp_bwd_workspace(int B, int H, int W);
+int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* workspace, int B, int C, int H, int W,
+                        int accumulate, void* stream);
 int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int B, int H, int W, float threshold,
                        void* stream);
 /* F.interpolate(mode="bilinear", align_corners=False) (RC/train_single/train_candy.py:91,97);

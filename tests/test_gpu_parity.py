@@ -63,7 +63,9 @@ def test_warp_mask_gram_norm_golden(golden):
 # ----------------------------------------------------------------------------- conv family vs oracle
 CONV_CASES = [
     # (N, Cin, H, W, Cout, k, stride, pad_mode, up, act)
-    (2, 3, 20, 28, 48, 9, 1, "reflect", 1, None),     # ReCoNet conv1 (Cin=3 slow gather path)
+    (2, 3, 20, 28, 48, 9, 1, "reflect", 1, None),     # ReCoNet conv1 (Cin=3: kw-unfolded input)
+    (1, 3, 13, 22, 48, 9, 1, "reflect", 1, None),     # conv1, width not a multiple of 4 (direct gather)
+    (1, 48, 13, 22, 3, 9, 1, "reflect", 1, "tanh"),   # ConvTanh, padded width 30 (direct dgrad gather)
     (2, 48, 16, 24, 96, 3, 2, "reflect", 1, None),    # conv2 (stride 2)
     (2, 96, 10, 12, 192, 3, 2, "reflect", 1, None),   # conv3
     (1, 32, 15, 21, 64, 3, 2, "reflect", 1, None),    # stride 2, odd sizes (uneven parity phases)
@@ -247,7 +249,7 @@ def test_pool_warp_gram_losses_bwd():
     y = ops.maxpool2x2(xg)
     y.backward(G(gy))
     assert torch.equal(C(y), yr.detach()) and rel_err(C(xg.grad), xr.grad) < 1e-6
-    # warp backward (atomic scatter)
+    # warp backward (gather form)
     x = torch.randn(2, 5, 12, 20, generator=g)
     flo = torch.rand(2, 2, 12, 20, generator=g) * 8 - 4
     xr = x.clone().requires_grad_(True)
@@ -277,6 +279,31 @@ def test_pool_warp_gram_losses_bwd():
     tg = ops.tv_loss(sg, 0.5)
     tg.backward()
     assert rel_err(C(tg), tr.detach()) < 1e-5 and rel_err(C(sg.grad), sr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("flow", ["random", "converging"])
+def test_warp_bwd_gather(flow):
+    """Gather-form warp backward vs the oracle's autograd, with more channels than one channel
+    group and (converging) flows that overflow the per-source tap lists (atomic excess pass)."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(21)
+    B, Cc, H, W = 2, 19, 10, 24
+    x = torch.randn(B, Cc, H, W, generator=g)
+    if flow == "random":
+        flo = torch.rand(B, 2, H, W, generator=g) * 6 - 3
+    else:  # every pixel of a row samples near column 5 / row 4: dozens of taps per source pixel
+        xs = torch.arange(W, dtype=torch.float32).view(1, 1, W).expand(B, H, W)
+        ys = torch.arange(H, dtype=torch.float32).view(1, H, 1).expand(B, H, W)
+        flo = torch.stack([5.3 - xs, 4.6 - ys], 1) + torch.rand(B, 2, H, W, generator=g) * 0.2
+    xr = x.clone().requires_grad_(True)
+    yr = R.warp(xr, flo)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xg = G(x).requires_grad_(True)
+    y = ops.warp(xg, G(flo))
+    y.backward(G(gy))
+    assert rel_err(C(xg.grad), xr.grad) < 1e-5
 
 
 # ----------------------------------------------------------------------------- models vs golden

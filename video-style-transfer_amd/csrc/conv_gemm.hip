@@ -123,6 +123,57 @@ __global__ void pack_phase2_kernel(const float* __restrict__ w, float* __restric
   apack_store(out, k, m, Mpad, v, bsplit);
 }
 
+// kw-unfold of a thin-channel tensor (Cin*K <= Cu, e.g. 3-channel images under a 9x9 kernel):
+//   out[n][c*K + kw][y][v] = src[n][c][y][xs],  xs = v + sgn*kw + off  (reflect or zero outside),
+// channels c*K + kw >= C*K are zero.  A conv over `out` with a Kx1 kernel (pad_x = 0) then runs on
+// the 16-channel k-tile path instead of a per-element tap decode over 3 channels.
+__global__ void unfold_kw_kernel(const float* __restrict__ src, float* __restrict__ out, int N, int C, int H, int Ws,
+                                 int Wout, int K, int Cu, int sgn, int off, int reflect) {
+  // one thread per 4 consecutive outputs of a row (float4 store; Wout % 4 == 0), grid.y = row
+  // (n, cu, y) -- no 64-bit index divisions
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * q >= Wout) return;
+  const int row = blockIdx.y + gridDim.y * blockIdx.z;
+  if (row >= N * Cu * H) return;
+  const int y = row % H, t = row / H, cu = t % Cu, n = t / Cu;
+  const int c = cu / K, kw = cu - c * K;
+  float v4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float* sr = src + (((long)n * C + c) * H + y) * Ws;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int xs = 4 * q + e + sgn * kw + off;
+      if (reflect) {
+        xs = abs(xs);
+        xs = xs >= Ws ? 2 * Ws - 2 - xs : xs;
+      }
+      // (reflect: single reflections only; anything further reads 0, never out of bounds)
+      v4[e] = (xs >= 0 && xs < Ws) ? sr[xs] : 0.f;
+    }
+  }
+  *reinterpret_cast<f32x4*>(out + (long)row * Wout + 4 * q) = f32x4{v4[0], v4[1], v4[2], v4[3]};
+}
+
+// A operand over a kw-unfolded source: k = kh*Cu + c*K + kw (c < Cc, the unfolded tensor's channel),
+// fwd: m = co, Cc = Cin; transposed (data gradient): m = ci, Cc = Cout
+__global__ void pack_kwu_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int K, int Cu,
+                                int transposed, int Mpad, int Kpad, int bsplit) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)Mpad * Kpad) return;
+  const int m = (int)(idx % Mpad);
+  const int k = (int)(idx / Mpad);
+  const int Mm = transposed ? Cin : Cout, Cc = transposed ? Cout : Cin;
+  float v = 0.f;
+  if (m < Mm && k < K * Cu) {
+    const int kh = k / Cu, cu = k - (k / Cu) * Cu, c = cu / K, kw = cu - (cu / K) * K;
+    if (c < Cc) {
+      const int co = transposed ? c : m, ci = transposed ? m : c;
+      v = w[(((long)co * Cin + ci) * K + kh) * K + kw];
+    }
+  }
+  apack_store(out, k, m, Mpad, v, bsplit);
+}
+
 // dx (+)= the reflect-pad border of the padded-grid gradient (the interior went straight to dx):
 // one thread per element of dx's border band (rows/cols within pad+1 of an edge)
 __global__ void fold_border_kernel(const float* __restrict__ border, float* __restrict__ dx, int NC, int Hs, int Ws,
@@ -278,13 +329,22 @@ extern "C" {
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                   int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
                   int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream) {
+  return vst_conv_gemm_padx(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad,
+                            up, epi, a_batch_stride, aux, gmask, stream);
+}
+
+int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
+                       int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
+                       int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
+                       void* stream) {
   VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
   VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
   VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
   VST_CHECK_ARG(!((epi & EPI_BIAS) && !bias) && !((epi & EPI_MASK) && !mask));
-  if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad < Ws * up);
-  return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad, up,
-                          epi, a_batch_stride, aux, gmask, stream);
+  if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad_x < Ws * up);
+  VST_CHECK_ARG(pad >= 0 && pad_x >= 0);
+  return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad_x,
+                          up, epi, a_batch_stride, aux, gmask, stream);
 }
 
 // out[n][m][p] = (sum_k A[n][k][m] B[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]
@@ -315,6 +375,38 @@ int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, f
   return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, 4 * Cin, K2 * K2 * Cout, Hc, Wc, K2, K2,
                           GM_TRANSPOSED, 1, 0, 0, 1, EPI_PHASE2, 0, nullptr, gmask, stream, nullptr, nullptr, nullptr,
                           nullptr, border, H, W, pad);
+}
+
+int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int Wout, int K, int Cu, int sgn, int off,
+                  int reflect, void* stream) {
+  VST_CHECK_ARG(src && out && N > 0 && C > 0 && H > 0 && Ws > 0 && Wout > 0 && K > 0 && Cu >= C * K);
+  VST_CHECK_ARG((sgn == 1 || sgn == -1) && !(reflect && Ws < 2) && Wout % 4 == 0);
+  const long rows = (long)N * Cu * H;
+  VST_CHECK_ARG(rows < (1L << 31));
+  const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
+  dim3 g(ceil_div(Wout / 4, 128), gy, (unsigned)((rows + gy - 1) / gy));
+  unfold_kw_kernel<<<g, 128, 0, (hipStream_t)stream>>>(src, out, N, C, H, Ws, Wout, K, Cu, sgn, off, reflect);
+  return vst_launch_status();
+}
+
+int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K, int Cu, int transposed, int Mpad,
+                        int Kpad, void* stream) {
+  VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && K > 0 && Cu >= (transposed ? Cout : Cin) * K);
+  VST_CHECK_ARG(Mpad >= (transposed ? Cin : Cout) && Kpad >= K * Cu);
+  const long total = (long)Mpad * Kpad;
+  pack_kwu_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, K, Cu, transposed, Mpad,
+                                                                         Kpad, apack_split(vst_gemm_mode_internal()));
+  return vst_launch_status();
+}
+
+int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
+                              int Cin, int H, int W, int KS, int pad, void* stream) {
+  VST_CHECK_ARG(dyu && wpack && dx && border && N > 0 && Cu % 16 == 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
+                pad < W && Ho == H + 2 * pad - KS + 1);
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  return conv_gemm_launch(dyu, wpack, nullptr, nullptr, dx, N, Cu, Ho, Wp, Cin, KS * Cu, Hp, Wp, KS, 1, GM_TRANSPOSED, 1,
+                          0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, stream, nullptr, nullptr, nullptr, nullptr, border,
+                          H, W, pad);
 }
 
 int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,

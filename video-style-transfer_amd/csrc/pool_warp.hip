@@ -111,6 +111,9 @@ __global__ void warp_fwd_kernel(const float* __restrict__ x, const float* __rest
   }
 }
 
+// grid.y: groups of WB_CPT channels (the FTL feature warp has 192 channels on a 64x128 grid: one
+// thread per pixel looping over all of them left the atomics latency-bound at 4 waves per CU)
+constexpr int WB_CPT = 8;
 __global__ void warp_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ flo, float* __restrict__ gx,
                                 int B, int C, int H, int W) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,14 +124,114 @@ __global__ void warp_bwd_kernel(const float* __restrict__ gout, const float* __r
   const int y = (int)(p / W), xx = (int)(p % W);
   const float* f = flo + (long)b * 2 * HW;
   Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
-  const float* gb = gout + (long)b * C * HW;
-  float* xb = gx + (long)b * C * HW;
+  const int c0 = blockIdx.y * WB_CPT, c1 = min(C, c0 + WB_CPT);
+  const float* gb = gout + ((long)b * C + c0) * HW;
+  float* xb = gx + ((long)b * C + c0) * HW;
+  float g[WB_CPT];
+#pragma unroll
+  for (int c = 0; c < WB_CPT; ++c) g[c] = c0 + c < c1 ? gb[c * HW + p] : 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
     if (cx < 0 || cx >= W || cy < 0 || cy >= H) continue;
     long o = (long)cy * W + cx;
-    for (int c = 0; c < C; ++c) atomicAdd(xb + c * HW + o, gb[c * HW + p] * bl.w[k]);
+#pragma unroll
+    for (int c = 0; c < WB_CPT; ++c)
+      if (c0 + c < c1) atomicAdd(xb + c * HW + o, g[c] * bl.w[k]);
+  }
+}
+
+// Gather form of the warp backward (no float atomics on the gradient): the bilinear taps of
+// every output pixel p are inverted once per image into per-source-pixel lists (up to WG_SLOTS
+// entries each; the flow is shared by all channels), then each source pixel sums its entries
+// for every channel.  Entries beyond WG_SLOTS (strongly converging flow) are added afterwards
+// by an atomic pass over just those taps.
+constexpr int WG_SLOTS = 8;
+struct WgEntry {
+  int p;
+  float w;
+};
+
+__global__ void warp_inv_fill_kernel(const float* __restrict__ flo, int* __restrict__ cnt, WgEntry* __restrict__ ent,
+                                     int* __restrict__ rec, int B, int H, int W) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const int y = (int)(p / W), xx = (int)(p % W);
+  const float* f = flo + (long)b * 2 * HW;
+  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
+  // all four counter atomics in flight before any result is used
+  long q[4];
+  int slot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
+    q[k] = (cx >= 0 && cx < W && cy >= 0 && cy < H) ? (long)b * HW + (long)cy * W + cx : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) slot[k] = q[k] >= 0 ? atomicAdd(cnt + q[k], 1) : -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (slot[k] >= 0 && slot[k] < WG_SLOTS) ent[q[k] * WG_SLOTS + slot[k]] = WgEntry{(int)p, bl.w[k]};
+  *reinterpret_cast<int4*>(rec + idx * 4) = make_int4(slot[0], slot[1], slot[2], slot[3]);
+}
+
+// gx[b][c][q] (+)= sum over q's entries of w * gout[b][c][p]; grid.y: channel groups of WB_CPT
+__global__ void warp_inv_gather_kernel(const float* __restrict__ gout, const int* __restrict__ cnt,
+                                       const WgEntry* __restrict__ ent, float* __restrict__ gx, int B, int C, int H,
+                                       int W, int accumulate) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int b = (int)(idx / HW);
+  const long q = idx - b * HW;
+  const int n = min(cnt[idx], WG_SLOTS);
+  const int c0 = blockIdx.y * WB_CPT, c1 = min(C, c0 + WB_CPT);
+  const float* gb = gout + ((long)b * C + c0) * HW;
+  float s[WB_CPT];
+#pragma unroll
+  for (int c = 0; c < WB_CPT; ++c) s[c] = 0.f;
+  for (int j = 0; j < n; ++j) {
+    const WgEntry e = ent[idx * WG_SLOTS + j];
+#pragma unroll
+    for (int c = 0; c < WB_CPT; ++c)
+      if (c0 + c < c1) s[c] += e.w * gb[c * HW + e.p];
+  }
+  float* xb = gx + ((long)b * C + c0) * HW + q;
+#pragma unroll
+  for (int c = 0; c < WB_CPT; ++c)
+    if (c0 + c < c1) xb[c * HW] = accumulate ? xb[c * HW] + s[c] : s[c];
+}
+
+// the taps that did not fit their source pixel's list (rec >= WG_SLOTS), added with atomics;
+// grid.y: channel groups of WB_CPT (a handful of such pixels must not serialise over all channels)
+__global__ void warp_inv_overflow_kernel(const float* __restrict__ gout, const float* __restrict__ flo,
+                                         const int* __restrict__ rec, float* __restrict__ gx, int B, int C, int H,
+                                         int W) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  const int4 r = *reinterpret_cast<const int4*>(rec + idx * 4);
+  if (r.x < WG_SLOTS && r.y < WG_SLOTS && r.z < WG_SLOTS && r.w < WG_SLOTS) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const int y = (int)(p / W), xx = (int)(p % W);
+  const float* f = flo + (long)b * 2 * HW;
+  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
+  const int rk[4] = {r.x, r.y, r.z, r.w};
+  const int c0 = blockIdx.y * WB_CPT, c1 = min(C, c0 + WB_CPT);
+  float g[WB_CPT];
+#pragma unroll
+  for (int c = 0; c < WB_CPT; ++c) g[c] = c0 + c < c1 ? gout[((long)b * C + c0 + c) * HW + p] : 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (rk[k] < WG_SLOTS) continue;  // (-1: out of range; 0..WG_SLOTS-1: gathered)
+    const long o = (long)(bl.y0 + (k >> 1)) * W + bl.x0 + (k & 1);
+#pragma unroll
+    for (int c = 0; c < WB_CPT; ++c)
+      if (c0 + c < c1) atomicAdd(gx + ((long)b * C + c0 + c) * HW + o, bl.w[k] * g[c]);
   }
 }
 
@@ -265,7 +368,34 @@ int vst_warp_fwd(const float* x, const float* flo, float* out, int B, int C, int
 int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, int H, int W, void* stream) {
   VST_CHECK_ARG(gout && flo && gx && B > 0 && C > 0 && H > 0 && W > 0);
   long total = (long)B * H * W;
-  warp_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, flo, gx, B, C, H, W);
+  dim3 g(ceil_div(total, 256), (C + WB_CPT - 1) / WB_CPT);
+  warp_bwd_kernel<<<g, 256, 0, (hipStream_t)stream>>>(gout, flo, gx, B, C, H, W);
+  return vst_launch_status();
+}
+
+long vst_warp_bwd_workspace(int B, int H, int W) {
+  const long n = (long)B * H * W;
+  return n * 16 + n * WG_SLOTS * (long)sizeof(WgEntry) + n * 4;  // rec, entries, cnt
+}
+
+int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* workspace, int B, int C, int H, int W,
+                        int accumulate, void* stream) {
+  VST_CHECK_ARG(gout && flo && gx && workspace && B > 0 && C > 0 && H > 0 && W > 0);
+  VST_CHECK_ARG(((uintptr_t)workspace & 15) == 0);
+  const long n = (long)B * H * W;
+  VST_CHECK_ARG(n * WG_SLOTS < (1L << 31));
+  hipStream_t st = (hipStream_t)stream;
+  // [rec: 4 ints per pixel (16-B aligned int4 reads)][entries][counts]
+  char* base = static_cast<char*>(workspace);
+  int* rec = reinterpret_cast<int*>(base);
+  WgEntry* ent = reinterpret_cast<WgEntry*>(base + n * 16);
+  int* cnt = reinterpret_cast<int*>(base + n * 16 + n * WG_SLOTS * (long)sizeof(WgEntry));
+  hipError_t e = hipMemsetAsync(cnt, 0, n * 4, st);
+  if (e != hipSuccess) return (int)e;
+  warp_inv_fill_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, ent, rec, B, H, W);
+  dim3 g(ceil_div(n, 256), (C + WB_CPT - 1) / WB_CPT);
+  warp_inv_gather_kernel<<<g, 256, 0, st>>>(gout, cnt, ent, gx, B, C, H, W, accumulate);
+  warp_inv_overflow_kernel<<<g, 256, 0, st>>>(gout, flo, rec, gx, B, C, H, W);
   return vst_launch_status();
 }
 

@@ -25,6 +25,7 @@ struct WgParams {
   int M, Mpad, J, Jpad;
   int Cs, Hs, Ws, Ho, Wo;
   int KH, KW, gmode, stride, pad, up;
+  int pad_x;  // column padding (= pad)
   int S, chunk;
   int asplit, Ha;  // row-split A gather: m = co*asplit + kh reads a[co][oy-kh][ox] (a has Ha rows)
   FastDiv fd_Wo, fd_Cs, fd_KW;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       const int r = rt + rr + q;
       const bool rv = r < r_end;
       const int oy = (int)fdiv((uint32_t)r, P.fd_Wo), ox = r - oy * P.Wo;
-      const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad;
+      const int by = oy * P.stride - P.pad, bx = ox * P.stride - P.pad_x;
       if (TAP) {  // one source offset per pixel, shared by all of this thread's channels
         int y = by + tkh, x = bx + tkw;
         bool ok = rv;
@@ -467,6 +468,7 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
   P.gmode = gmode;
   P.stride = stride;
   P.pad = pad;
+  P.pad_x = pad;
   P.up = up;
   P.S = S;
   P.asplit = asplit;

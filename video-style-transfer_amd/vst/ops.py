@@ -159,21 +159,28 @@ def _cache_entry(w):
     return {}
 
 
-def packed_weight(w, transposed, split_kh=False):
-    """Tap-major A[k][m] pack of a conv weight (split_kh: rows (co, kh), k = (kw, ci))."""
-    key = (w._version, w.data_ptr(), bool(transposed), bool(split_kh), gemm_mode())
+def packed_weight(w, transposed, split_kh=False, kwu=False):
+    """Tap-major A[k][m] pack of a conv weight (split_kh: rows (co, kh), k = (kw, ci); kwu: over a
+    kw-unfolded source, k = kh*Cu + c*K + kw)."""
+    key = (w._version, w.data_ptr(), bool(transposed), bool(split_kh), bool(kwu), gemm_mode())
     if not w.requires_grad:
         hit = _cache_entry(w).get(key)
         if hit is not None:
             return hit
     Cout, Cin, KH, KW = w.shape
-    if split_kh:
+    if kwu:
+        Cu = kwu_channels(Cout if transposed else Cin, KW)
+        M, K = (Cin if transposed else Cout), KH * Cu
+    elif split_kh:
         M, K = Cout * KH, KW * Cin
     else:
         M, K = (Cin, KH * KW * Cout) if transposed else (Cout, KH * KW * Cin)
     Mpad, Kpad = pack_dims(M, K)
     out = _empty((pack_floats(Mpad, Kpad),), w)
-    lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, stream())
+    if kwu:
+        lib.vst_pack_weight_kwu(ptr(w), ptr(out), Cout, Cin, KW, Cu, int(transposed), Mpad, Kpad, stream())
+    else:
+        lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, stream())
     if not w.requires_grad:
         entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
         entry[key] = out
@@ -182,13 +189,33 @@ def packed_weight(w, transposed, split_kh=False):
     return out
 
 
+def kwu_channels(C, ks):
+    """channels of the kw-unfolded tensor: C*ks rounded up to the 16-channel k-tile"""
+    return (C * ks + 15) // 16 * 16
+
+
+def kwu_ok(C, ks, stride, up, Wout):
+    """Thin tensors (3-channel images, the ConvTanh output gradient) under a KxK stride-1 kernel:
+    unfold along kw (C*K <= 32 channels) so the GEMM runs on the 16-channel k-tile path."""
+    return C % 16 != 0 and ks > 1 and C * ks <= 32 and stride == 1 and up == 1 and Wout % 4 == 0
+
+
+def unfold_kw(x, ks, off, sgn, Wout, reflect):
+    """out[n][c*ks + kw][y][v] = x[n][c][y][v + sgn*kw + off] (reflect or zero outside)."""
+    N, C, H, W = x.shape
+    Cu = kwu_channels(C, ks)
+    out = _empty((N, Cu, H, Wout), x)
+    lib.vst_unfold_kw(ptr(x), ptr(out), N, C, H, W, Wout, ks, Cu, sgn, off, int(reflect), stream())
+    return out
+
+
 def conv_out_hw(H, W, ks, stride, pad, up):
     return (H * up + 2 * pad - ks) // stride + 1, (W * up + 2 * pad - ks) // stride + 1
 
 
 def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=None, out=None, aux=None, gmask=None,
-              a_batch_stride=0, mask=None, algo_flops=None, kh=None):
-    """ks: kernel width; kh: kernel height (defaults to ks)."""
+              a_batch_stride=0, mask=None, algo_flops=None, kh=None, pad_x=None):
+    """ks: kernel width; kh: kernel height (defaults to ks); pad_x: column padding (defaults to pad)."""
     N, Cs, Hs, Ws = src.shape
     kh = ks if kh is None else kh
     if out is None:
@@ -196,8 +223,9 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh,
                       4.0 * (src.numel() + wpack.numel() + out.numel()),
                       (N, Cs, Hs, Ws, M, Ho, Wo, kh, ks, gmode, stride, pad, up), gemm_mode())
-    lib.vst_conv_gemm(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho, Wo,
-                      kh, ks, gmode, stride, pad, up, epi, a_batch_stride, ptr(aux), ptr(gmask), stream())
+    lib.vst_conv_gemm_padx(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho,
+                           Wo, kh, ks, gmode, stride, pad, pad if pad_x is None else pad_x, up, epi, a_batch_stride,
+                           ptr(aux), ptr(gmask), stream())
     kprof.end(tok)
     return out
 
@@ -221,6 +249,8 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
     if stride == 2 and up == 1:
         return conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask, flops)
     if stride == 1 and up == 1 and gmask is None and 0 < pad < min(H, W):
+        if kwu_ok(Cout, ks, stride, up, W + 2 * pad) and w.shape[2] == ks:
+            return conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops)
         return conv_dgrad_padout(gz, w, x_shape, ks, pad, flops)
     if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
         return conv_dgrad_ring(gz, w, x_shape, ks, up, flops)
@@ -243,6 +273,26 @@ def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops):
     tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
     lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad, stream())
+    kprof.end(tok)
+    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
+    return dx
+
+
+def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops):
+    """conv_dgrad_padout for a thin output gradient (ConvTanh 48->3): dy is kw-unfolded first,
+    dyu[co*K + kw][y][v] = dy[co][y][v - kw] over the padded width, so the transposed GEMM is a
+    Kx1 gather over 16-multiple channels."""
+    N, Cin, H, W = x_shape
+    Ho = gz.shape[2]
+    dyu = unfold_kw(gz, ks, 0, -1, W + 2 * pad, reflect=False)
+    wp = packed_weight(w, True, kwu=True)
+    dx = _empty(x_shape, gz)
+    border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
+    tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
+                      (N, dyu.shape[1], Ho, W + 2 * pad, Cin, H + 2 * pad, W + 2 * pad, 1, ks, GM_TRANSPOSED, 1, 0, 1),
+                      gemm_mode())
+    lib.vst_conv_dgrad_padout_kwu(ptr(dyu), ptr(wp), ptr(dx), ptr(border), N, dyu.shape[1], Ho, Cin, H, W, ks, pad,
+                                  stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -385,6 +435,14 @@ class Conv2dFn(Function):
         gemm_role("fwd_img" if Cin == 3 else "fwd")
         if rowsplit_ok(Cout, ks, stride, pad_mode, up) and pad == ks // 2:
             out = conv_fwd_rowsplit(x, w, bias, epi, aux)
+        elif kwu_ok(Cin, ks, stride, up, W) and 0 < pad < min(H, W) and Ho == H and Wo == W:
+            # thin input (3-channel frames): kw-unfold, then a Kx1 conv on the 16-channel k-tile path
+            xu = unfold_kw(x, ks, -pad, 1, W, pad_mode == "reflect")
+            out = conv_gemm(xu, packed_weight(w, False, kwu=True), Cout, 1, Ho, Wo,
+                            GM_REFLECT if pad_mode == "reflect" else GM_ZERO, 1, pad, 1, epi=epi, bias=bias, aux=aux,
+                            kh=ks, pad_x=0, algo_flops=2.0 * N * Cout * Ho * Wo * Cin * ks * ks)
+            # (the weight gradient stays on x: over the unfolded input its columns pad 243 -> 384,
+            # measured 1.7x slower)
         else:
             out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
                             stride, pad, up, epi=epi, bias=bias, aux=aux)
@@ -536,8 +594,9 @@ class WarpFn(Function):
     def backward(ctx, gout):
         (flo,) = ctx.saved_tensors
         B, C, H, W = ctx.shape
-        gx = _zeros(ctx.shape, flo)
-        lib.vst_warp_bwd(ptr(gout.contiguous()), ptr(flo), ptr(gx), B, C, H, W, stream())
+        gx = _empty(ctx.shape, flo)
+        ws = _empty(((lib.vst_warp_bwd_workspace(B, H, W) + 3) // 4,), flo)
+        lib.vst_warp_bwd_gather(ptr(gout.contiguous()), ptr(flo), ptr(gx), ptr(ws), B, C, H, W, 0, stream())
         return gx, None
 
 
