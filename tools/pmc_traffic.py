@@ -22,7 +22,8 @@ def load(model, counter):
 
 
 def family(name):
-    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").split("<")[0]
+    """kernel family: the unqualified template name (namespaces and arguments dropped)"""
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
 
 
 def main():
