@@ -100,6 +100,11 @@ int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, 
                        void* stream);
 int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
                               int Cin, int H, int W, int KS, int pad, void* stream);
+/* data gradient of a zero-padded stride-1 KxK conv with few input channels (VGG conv1_1, 64 -> 3):
+ * P = tap-split 1x1 transposed GEMM (vst_conv_gemm with A = vst_pack_weight of w viewed as
+ * [Cout][Cin*K*K][1][1], transposed; rows (c, kh, kw)), then
+ *   dx[n][c][y][x] (+)= sum_{kh,kw} P[n][(c*K+kh)*K+kw][y+pad-kh][x+pad-kw]  (zero outside). */
+int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int pad, int accumulate, void* stream);
 /* stride-1 reflect-pad data gradient (ResidualBlock / ConvTanh backward, RC/network.py:72-75,
  * 145-150, 83-85): the transposed GEMM (A = vst_pack_weight(transposed=1)) runs over the padded
  * grid (H+2p) x (W+2p); interior pixels go straight into dx, the p-wide border into border

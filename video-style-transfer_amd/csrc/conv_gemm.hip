@@ -154,6 +154,30 @@ __global__ void unfold_kw_kernel(const float* __restrict__ src, float* __restric
   *reinterpret_cast<f32x4*>(out + (long)row * Wout + 4 * q) = f32x4{v4[0], v4[1], v4[2], v4[3]};
 }
 
+// dx[n][c][y][x] (+)= sum_{kh,kw} P[n][(c*K + kh)*K + kw][y + pad - kh][x + pad - kw]  (zero outside):
+// the data gradient of a zero-padded stride-1 KxK conv with few input channels, after the tap-split
+// 1x1 GEMM P = W^T dY (rows (c, kh, kw): 27 GEMM rows for VGG conv1_1 instead of 3 padded to 32)
+__global__ void tapsum_kernel(const float* __restrict__ P, float* __restrict__ dx, int N, int C, int H, int W, int K,
+                              int pad, int accumulate) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= (long)N * C * HW) return;
+  const long q = idx % HW, nc = idx / HW;
+  const int y = (int)(q / W), x = (int)(q % W);
+  const int c = (int)(nc % C), n = (int)(nc / C);
+  const float* pb = P + ((long)n * C * K * K + (long)c * K * K) * HW;
+  float s = 0.f;
+  for (int kh = 0; kh < K; ++kh) {
+    const int yy = y + pad - kh;
+    if (yy < 0 || yy >= H) continue;
+    for (int kw = 0; kw < K; ++kw) {
+      const int xx = x + pad - kw;
+      if (xx >= 0 && xx < W) s += pb[(long)(kh * K + kw) * HW + (long)yy * W + xx];
+    }
+  }
+  dx[idx] = accumulate ? dx[idx] + s : s;
+}
+
 // A operand over a kw-unfolded source: k = kh*Cu + c*K + kw (c < Cc, the unfolded tensor's channel),
 // fwd: m = co, Cc = Cin; transposed (data gradient): m = ci, Cc = Cout
 __global__ void pack_kwu_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int K, int Cu,
@@ -386,6 +410,13 @@ int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int
   const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
   dim3 g(ceil_div(Wout / 4, 128), gy, (unsigned)((rows + gy - 1) / gy));
   unfold_kw_kernel<<<g, 128, 0, (hipStream_t)stream>>>(src, out, N, C, H, Ws, Wout, K, Cu, sgn, off, reflect);
+  return vst_launch_status();
+}
+
+int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int pad, int accumulate, void* stream) {
+  VST_CHECK_ARG(P && dx && N > 0 && C > 0 && H > 0 && W > 0 && K > 0 && pad >= 0);
+  const long total = (long)N * C * H * W;
+  tapsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(P, dx, N, C, H, W, K, pad, accumulate);
   return vst_launch_status();
 }
 

@@ -162,7 +162,7 @@ def _cache_entry(w):
 def packed_weight(w, transposed, split_kh=False, kwu=False):
     """Tap-major A[k][m] pack of a conv weight (split_kh: rows (co, kh), k = (kw, ci); kwu: over a
     kw-unfolded source, k = kh*Cu + c*K + kw)."""
-    key = (w._version, w.data_ptr(), bool(transposed), bool(split_kh), bool(kwu), gemm_mode())
+    key = (w._version, w.data_ptr(), tuple(w.shape), bool(transposed), bool(split_kh), bool(kwu), gemm_mode())
     if not w.requires_grad:
         hit = _cache_entry(w).get(key)
         if hit is not None:
@@ -238,6 +238,14 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
     Cout = w.shape[0]
     Ho, Wo = gz.shape[2:]
     flops = 2.0 * N * Cout * Ho * Wo * Cin * ks * ks
+    if (pad_mode == "zero" and up == 1 and stride == 1 and dmask is None and gmask is None and Cin % 16 != 0
+            and Cin * ks * ks <= 32 and (H, W) == tuple(gz.shape[2:])):
+        # few input channels (VGG conv1_1): tap-split 1x1 GEMM (rows (c, kh, kw)) + shift-sum
+        P = conv_gemm(gz, packed_weight(w.view(Cout, Cin * ks * ks, 1, 1), transposed=True), Cin * ks * ks, 1, H, W,
+                      GM_ZERO, 1, 0, 1, algo_flops=flops)
+        dx = _empty(x_shape, gz)
+        lib.vst_tapsum(ptr(P), ptr(dx), N, Cin, H, W, ks, pad, 0, stream())
+        return dx
     if pad_mode == "zero" and up == 1:
         return conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1,
                          gmask=gmask, algo_flops=flops, epi=EPI_MASK if dmask is not None else 0,
