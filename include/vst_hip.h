@@ -162,6 +162,10 @@ int vst_channel_sum(const float* x, float* out, float* partial, int N, int C, in
 int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream);
 /* relu_mask: gx also masked by x > 0 (x = ReLU output consumed only by this pool) */
 int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, int relu_mask, void* stream);
+/* VGG slice boundary (a ReLU output x feeding both the losses and the next slice's pool):
+ * gx = [relu_mask: (x > 0) *] (pool_bwd(gy) + addend) in one pass; gy or addend may be NULL */
+int vst_maxpool2x2_bwd_add(const float* x, const float* gy, const float* addend, float* gx, long NC, int H, int W,
+                           int relu_mask, void* stream);
 
 /* ---- flow warp (RC/utilities.py:39-57) / occlusion mask (RC/utilities.py:60-90) ------------
  * warp_bwd scatters with float atomics into gx (zero it first or accumulate). */

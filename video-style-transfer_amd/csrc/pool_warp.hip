@@ -57,6 +57,50 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
   gx[idx] = g;
 }
 
+// gx = relu_mask(pool_bwd(gy) + addend) for a ReLU output x that feeds both a MaxPool2d(2, 2) and
+// another consumer (a VGG slice output used by the losses); gy / addend may be NULL.  One thread
+// per 2x2 cell (trailing odd row/column: cells without a window, addend only).
+__global__ void maxpool_bwd_add_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                       const float* __restrict__ addend, float* __restrict__ gx, long NC, int H, int W,
+                                       int relu_mask) {
+  const int Ho = H / 2, Wo = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * Hc * Wc) return;
+  const int cx = (int)(idx % Wc);
+  const long t = idx / Wc;
+  const int cy = (int)(t % Hc);
+  const long nc = t / Hc;
+  const long base = nc * H * W + (long)(2 * cy) * W + 2 * cx;
+  const bool has_r = 2 * cy + 1 < H, has_c = 2 * cx + 1 < W;
+  float v[4];
+  v[0] = x[base];
+  v[1] = has_c ? x[base + 1] : 0.f;
+  v[2] = has_r ? x[base + W] : 0.f;
+  v[3] = has_r && has_c ? x[base + W + 1] : 0.f;
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  if (gy && cy < Ho && cx < Wo) {  // a full pooling window: route to the first maximum
+    int arg = 0;
+    float m = v[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (v[k] > m || isnan(v[k])) {
+        m = v[k];
+        arg = k;
+      }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = k == arg ? gy[nc * Ho * Wo + (long)cy * Wo + cx] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if ((k & 1) && !has_c) continue;
+    if ((k & 2) && !has_r) continue;
+    const long o = base + (k >> 1) * (long)W + (k & 1);
+    float s = g[k] + (addend ? addend[o] : 0.f);
+    if (relu_mask && !(v[k] > 0.f)) s = 0.f;
+    gx[o] = s;
+  }
+}
+
 struct Bilin {
   int x0, y0;
   float w[4];  // nw, ne, sw, se
@@ -354,6 +398,15 @@ int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int 
   VST_CHECK_ARG(x && gy && gx && NC > 0 && H >= 2 && W >= 2);
   long total = NC * H * W;
   maxpool_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, gx, NC, H, W, relu_mask);
+  return vst_launch_status();
+}
+
+int vst_maxpool2x2_bwd_add(const float* x, const float* gy, const float* addend, float* gx, long NC, int H, int W,
+                           int relu_mask, void* stream) {
+  VST_CHECK_ARG(x && gx && NC > 0 && H >= 2 && W >= 2);
+  const long total = NC * ((H + 1) / 2) * ((W + 1) / 2);
+  maxpool_bwd_add_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, addend, gx, NC, H, W,
+                                                                                 relu_mask);
   return vst_launch_status();
 }
 

@@ -582,6 +582,39 @@ def maxpool2x2(x, relu_mask=False):
     return MaxPool2x2Fn.apply(x, relu_mask)
 
 
+class FeaturePoolFn(Function):
+    """A VGG slice output h (a ReLU output) that is both a loss feature and the next slice's
+    MaxPool2d(2, 2) input (RC/network.py:33-40 slice boundaries): returns (h, maxpool(h)); the
+    backward is relu_mask(pool_bwd(g_pool) + g_feature) in one pass, replacing autograd's sum of
+    the two gradients, the pool backward and the producer's ReLU backward (the producing conv is
+    then built premasked)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        h = _check(h, "feature", 4)
+        N, C, H, W = h.shape
+        p = _empty((N, C, H // 2, W // 2), h)
+        lib.vst_maxpool2x2_fwd(ptr(h), ptr(p), N * C, H, W, stream())
+        ctx.save_for_backward(h)
+        ctx.set_materialize_grads(False)
+        return h.view_as(h), p
+
+    @staticmethod
+    def backward(ctx, g_feat, g_pool):
+        (h,) = ctx.saved_tensors
+        N, C, H, W = h.shape
+        gx = _empty(h.shape, h)
+        lib.vst_maxpool2x2_bwd_add(ptr(h), ptr(g_pool.contiguous() if g_pool is not None else None),
+                                   ptr(g_feat.contiguous() if g_feat is not None else None), ptr(gx), N * C, H, W, 1,
+                                   stream())
+        return gx
+
+
+def feature_pool(h):
+    """(h, maxpool2x2(h)) with the fused slice-boundary backward of FeaturePoolFn."""
+    return FeaturePoolFn.apply(h)
+
+
 class WarpFn(Function):
     """utilities.warp (RC/utilities.py:39-57); gradient w.r.t. x only (flow is data)."""
 

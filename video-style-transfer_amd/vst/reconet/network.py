@@ -36,12 +36,18 @@ def vgg_features(cfg, n_layers):
     return layers[:n_layers]
 
 
-def run_vgg_slice(seq, x):
+def run_vgg_slice(seq, x, skip_pool=False, premasked_out=False):
     """Forward of one VGG slice on HIP kernels: Conv2d followed by ReLU -> fused conv+bias+relu.
     A ReLU output consumed only by the next module of the slice (a conv or a max-pool) never sees
     a separate ReLU-backward pass: the consumer's backward applies the mask (dgrad epilogue /
-    pool backward) and the producer is marked premasked.  Slice outputs (loss features) keep it."""
+    pool backward) and the producer is marked premasked.  Slice outputs (loss features) keep it,
+    unless premasked_out (the output goes through ops.feature_pool, whose backward masks);
+    skip_pool: the slice's leading MaxPool2d already ran in ops.feature_pool."""
     mods = list(seq.children())
+    if skip_pool:
+        if not isinstance(mods[0], nn.MaxPool2d):
+            raise RuntimeError("slice boundary without a leading MaxPool2d")
+        mods = mods[1:]
     i = 0
     fuse_next = False  # the previous conv's ReLU output is consumed only by mods[i]
     while i < len(mods):
@@ -49,7 +55,7 @@ def run_vgg_slice(seq, x):
         if isinstance(m, nn.Conv2d):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             nxt = mods[i + 2] if relu and i + 2 < len(mods) else None
-            internal = relu and isinstance(nxt, (nn.Conv2d, nn.MaxPool2d))
+            internal = relu and (isinstance(nxt, (nn.Conv2d, nn.MaxPool2d)) or (nxt is None and premasked_out))
             x = ops.conv2d(x, m.weight, m.bias, stride=m.stride[0], pad=m.padding[0], pad_mode="zero",
                            act="relu" if relu else None, mask_dx=fuse_next, premasked=internal)
             fuse_next = internal
@@ -100,10 +106,12 @@ class Vgg16(nn.Module):
             p.requires_grad = False
 
     def forward(self, X):
-        h1 = run_vgg_slice(self.slice1, X)
-        h2 = run_vgg_slice(self.slice2, h1)
-        h3 = run_vgg_slice(self.slice3, h2)
-        h4 = run_vgg_slice(self.slice4, h3)
+        # h1..h3 are loss features AND the next slice's pool input: pool, gradient sum and ReLU
+        # backward fuse at each boundary (ops.feature_pool)
+        h1, p1 = ops.feature_pool(run_vgg_slice(self.slice1, X, premasked_out=True))
+        h2, p2 = ops.feature_pool(run_vgg_slice(self.slice2, p1, skip_pool=True, premasked_out=True))
+        h3, p3 = ops.feature_pool(run_vgg_slice(self.slice3, p2, skip_pool=True, premasked_out=True))
+        h4 = run_vgg_slice(self.slice4, p3, skip_pool=True)
         return VggOutputs(h1, h2, h3, h4)
 
 
