@@ -353,22 +353,26 @@ constexpr int WBN = 128;
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int Cout,
                                     int Mpad, int Jpad, int Cs, int KH, int KW, int rowsplit, float scale,
                                     int accumulate) {
+  // threads walk the slab order (ci fastest: coalesced slab reads, the dominant traffic) and
+  // scatter into PyTorch's [co][ci][kh][kw] order
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)Cout * Cs * KH * KW;
   if (idx >= total) return;
-  int kw = (int)(idx % KW);
-  long t = idx / KW;
+  int ci = (int)(idx % Cs);
+  long t = idx / Cs;
+  int kw = (int)(t % KW);
+  t /= KW;
   int kh = (int)(t % KH);
-  t /= KH;
-  int ci = (int)(t % Cs);
-  int co = (int)(t / Cs);
+  int co = (int)(t / KH);
   long off = rowsplit ? (long)(co * KH + kh) * Jpad + kw * Cs + ci : (long)co * Jpad + (kh * KW + kw) * Cs + ci;
   long zs = (long)Mpad * Jpad;
   float s = 0.f;
+#pragma unroll 8
   for (int z = 0; z < nslab; ++z) s += slab[off + z * zs];
   s *= scale;
-  if (accumulate) s += out[idx];
-  out[idx] = s;
+  const long o = (((long)co * Cs + ci) * KH + kh) * KW + kw;
+  if (accumulate) s += out[o];
+  out[o] = s;
 }
 
 // out[n][i][j] = scale * sum_{s<S} slab[n*S+s][i][j],  i < M, j < J

@@ -106,13 +106,22 @@ class Vgg16(nn.Module):
             p.requires_grad = False
 
     def forward(self, X):
-        # h1..h3 are loss features AND the next slice's pool input: pool, gradient sum and ReLU
-        # backward fuse at each boundary (ops.feature_pool)
-        h1, p1 = ops.feature_pool(run_vgg_slice(self.slice1, X, premasked_out=True))
-        h2, p2 = ops.feature_pool(run_vgg_slice(self.slice2, p1, skip_pool=True, premasked_out=True))
-        h3, p3 = ops.feature_pool(run_vgg_slice(self.slice3, p2, skip_pool=True, premasked_out=True))
-        h4 = run_vgg_slice(self.slice4, p3, skip_pool=True)
-        return VggOutputs(h1, h2, h3, h4)
+        return VggOutputs(*self.features_upto(X, 4))
+
+    def features_upto(self, X, n):
+        """relu1_2 .. the n-th slice output only (the trainer's content pass needs relu3_3 alone,
+        so its slice-4 convolutions are skipped; the outputs computed are identical).
+        Slice outputs that feed the next slice are loss features AND that slice's pool input:
+        pool, gradient sum and ReLU backward fuse at each boundary (ops.feature_pool)."""
+        slices = (self.slice1, self.slice2, self.slice3, self.slice4)[:n]
+        outs, x = [], X
+        for i, sl in enumerate(slices):
+            last = i == len(slices) - 1
+            h = run_vgg_slice(sl, x, skip_pool=i > 0, premasked_out=not last)
+            if not last:
+                h, x = ops.feature_pool(h)
+            outs.append(h)
+        return outs
 
 
 class SelectiveLoadModule(torch.nn.Module):

@@ -70,7 +70,10 @@ class ReCoNetTrainer:
             i_n = ops.VggNormalizeFn.apply(x if C == 3 else x[:, C - 3:].contiguous())
         sf = self.vgg(s_n)
         with torch.no_grad():
-            cf = self.vgg(i_n)
+            # the content loss reads relu3_3 only (train_candy.py:126-128): the content pass stops
+            # after slice 3 when the loss net supports it
+            upto = getattr(self.vgg, "features_upto", None)
+            cf = upto(i_n, 3) if upto is not None else self.vgg(i_n)
         out = {}
         if self.temporal:
             Hf, Wf = fmap.shape[2:]
