@@ -60,7 +60,14 @@ POLICIES = {
     "bf16x6": ("bf16x6", {}),
     "bf16x3/stylizer-f32": ("bf16x3", {"stylizer.fwd": "f32", "stylizer.fwd_img": "f32"}),
     "bf16x3/stylizer-bf16x6": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6"}),
+    "parity/res-bf16x3": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6",
+                                     "stylizer.res.fwd": "bf16x3"}),
+    "parity/outer-bf16x3": ("bf16x3", {"stylizer.fwd": "bf16x3", "stylizer.fwd_img": "bf16x6",
+                                       "stylizer.res.fwd": "bf16x6"}),
+    "parity/img-only": ("bf16x3", {"stylizer.fwd_img": "bf16x6"}),
 }
+only = sys.argv[1:]
+POLICIES = {k: v for k, v in POLICIES.items() if not only or k in only}
 for name, (base, pol) in POLICIES.items():
     ops.set_gemm_mode(base, pol)
     for tag in ("b2", "b1r"):
