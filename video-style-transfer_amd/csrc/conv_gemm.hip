@@ -315,6 +315,12 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   P.Ws = Ws;
   P.M = M;
   int cfg = widen_cfg(select_cfg(M), (long)Ho * Wo);
+  {
+    // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
+    static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
+    const int mode = vst_gemm_mode_internal();
+    if (t256 && cfg == T128 && M % 256 == 0 && (mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16)) cfg = T256;
+  }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);
   P.Mpad = (M + bm - 1) / bm * bm;
   P.K = K;

@@ -404,7 +404,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
 }
 
 // tile configurations (BM x BN)
-enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W };
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256 };
 
 inline int select_cfg(int M) {
   if (M <= 32) return T32;
@@ -414,7 +414,7 @@ inline int select_cfg(int M) {
   return T128;
 }
 inline int cfg_bm(int c) {
-  const int bm[] = {32, 64, 96, 128, 192, 64, 96};
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256};
   return bm[c];
 }
 inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
@@ -429,6 +429,9 @@ inline int widen_cfg(int c, long HWo) {
 
 #ifndef VST_MINW_T128
 #define VST_MINW_T128 4
+#endif
+#ifndef VST_MINW_T256
+#define VST_MINW_T256 2
 #endif
 #ifndef VST_MINW_T192
 #define VST_MINW_T192 2
@@ -450,6 +453,9 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
     case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2, PR><<<grid, NT, 0, st>>>(P); break;
     case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P); break;
+    case T256:  // bf16x3 / bf16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
+      if constexpr (PR == 1 || PR == 2) conv_gemm_kernel<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR><<<grid, NT, 0, st>>>(P);
+      break;
     default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR><<<grid, NT, 0, st>>>(P); break;
   }
 }
