@@ -294,6 +294,22 @@ int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, lon
 int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
              long step, float gscale, void* stream);
 
+/* ---- video frames (ReCoNet inference, RC/utilities.py:108-235) -----------------------------
+ * cvframe_to_tensor (RC/utilities.py:108-123, the tensor half; cv2.resize stays on the host):
+ * frames = N x H x W x 3 uint8 (cv2 BGR order), out = N x 3 x H x W fp32, out = (b / 255) * 255
+ * (ToTensor then .mul(255)); swap_rb = 1 applies cv2.COLOR_BGR2RGB. */
+int vst_frames_to_tensor(const void* frames, float* out, int N, int H, int W, int swap_rb, void* stream);
+/* Inference.__iter__ (RC/utilities.py:213-227): y (N x 3 x H x W fp32) -> clamp(0, 255) ->
+ * HWC -> cv2.COLOR_RGB2BGR (swap_rb = 1) -> astype(uint8) (truncation) into frames; clamped
+ * (may be NULL) receives the clamped fp32 tensor (calculate_mse's styled frame). */
+int vst_tensor_to_frames(const float* y, float* clamped, void* frames, int N, int H, int W, int swap_rb,
+                         void* stream);
+/* calculate_mse (RC/utilities.py:151-161): out[0] = mean(((x1 - x0) - (y1 - y0))^2) over n
+ * elements, computed on the device (workspace: VST_FRAME_MSE_WS_BYTES bytes). */
+#define VST_FRAME_MSE_WS_BYTES 16384
+int vst_frame_diff_mse(const float* x0, const float* x1, const float* y0, const float* y1, long n, void* workspace,
+                       float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -317,3 +317,38 @@ def adam_step(params, grads, state, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
         v.mul_(b2).addcmul_(g, g, value=1 - b2)
         denom = (v.sqrt() / np.sqrt(1 - b2 ** t)).add_(eps)
         p.data.addcdiv_(m, denom, value=-lr / (1 - b1 ** t))
+
+
+# ------------------------------------------------------------------ inference (RC/utilities.py:108-235)
+def cvframe_to_tensor(frame):
+    """RC/utilities.py:118-123 for a 360x640 BGR uint8 frame: BGR2RGB, ToTensor, mul(255)."""
+    rgb = torch.from_numpy(np.ascontiguousarray(frame[..., ::-1]))
+    return rgb.permute(2, 0, 1).contiguous().float().div(255).mul(255)
+
+
+def _styled_windows(forward, P, frames, n, first_frame):
+    if first_frame is None or first_frame < n:
+        first_frame = n
+    frames = list(frames)[first_frame - n:]
+    imgs = [cvframe_to_tensor(f) for f in frames]
+    with torch.no_grad():
+        for t in range(n - 1, len(imgs)):
+            x = torch.cat(imgs[t - n + 1:t + 1], 0).unsqueeze(0)
+            yield imgs[t].unsqueeze(0), forward(P, x)[-1].clamp(0, 255)
+
+
+def inference(forward, P, frames, n, first_frame=None):
+    """Inference.__iter__ (RC/utilities.py:209-235): HxWx3 uint8 BGR stylised frames."""
+    return [np.ascontiguousarray(y[0].permute(1, 2, 0).numpy()[..., ::-1]).astype(np.uint8)
+            for _, y in _styled_windows(forward, P, frames, n, first_frame)]
+
+
+def calculate_mse(forward, P, frames, n):
+    """calculate_mse (RC/utilities.py:126-176)."""
+    loss, count, prev = 0, 0, None
+    for x, y in _styled_windows(forward, P, frames, n, None):
+        if prev is not None:
+            loss += F.mse_loss(x - prev[0], y - prev[1]).item()
+            count += 1
+        prev = (x, y)
+    return loss / count

@@ -414,6 +414,64 @@ def gen_adaattn():
     print("adaattn fixtures written")
 
 
+# --------------------------------------------------------------------------------------------
+# ReCoNet inference (RC/utilities.py:108-235): the reference's own Inference / calculate_mse
+# --------------------------------------------------------------------------------------------
+class _FakeCapture:
+    """cv2.VideoCapture over in-memory BGR frames (OpenCV is absent in this image)."""
+
+    def __init__(self, frames):
+        self.frames = list(frames)
+
+    def read(self):
+        return (True, self.frames.pop(0).copy()) if self.frames else (False, None)
+
+    def release(self):
+        pass
+
+
+def gen_infer():
+    from vst.synthetic import video_frames
+
+    _fresh_project(RC_DIR)
+    rc_util = _load("utilities", os.path.join(RC_DIR, "utilities.py"))
+    sys.modules["utilities"] = rc_util
+    rc_net = _load("network", os.path.join(RC_DIR, "network.py"))
+    sys.modules["network"] = rc_net
+    clips = {}
+    cv2 = rc_util.cv2
+    cv2.COLOR_BGR2RGB, cv2.COLOR_RGB2BGR = 4, 5  # channel reversal both ways, as OpenCV's
+    cv2.cvtColor = lambda img, code: np.ascontiguousarray(img[..., ::-1])
+    cv2.VideoCapture = lambda path: _FakeCapture(clips[path])
+    out = {}
+    tmp = os.path.join("/tmp", "vst_gen_infer")
+    os.makedirs(tmp, exist_ok=True)
+    sd2 = torch.load(os.path.join(RC_DIR, "models_old", "SD2_epoch_4_batchSize_2.pth"), weights_only=True,
+                     map_location="cpu")
+    p_sd2 = os.path.join(tmp, "sd2.pth")
+    torch.save(sd2, p_sd2)
+    m2 = rc_net.ReCoNetSD2(2)
+    seed_module(m2, 31)
+    p_win = os.path.join(tmp, "sd2_win2.pth")
+    torch.save(m2.state_dict(), p_win)
+    # case a: trained SD2 checkpoint, 1 frame per window, first_frame=2 (skips one frame)
+    # case b: seeded SD2 with 2-frame windows
+    for tag, cls_n, path, seed, T, ff in (("a", 1, p_sd2, 41, 4, 2), ("b", 2, p_win, 42, 4, None)):
+        clips[tag] = video_frames(seed, T)
+        with torch.no_grad():
+            frames = list(rc_util.Inference(rc_net.ReCoNetSD2, cls_n, path, tag, "cpu", ff))
+            mse = rc_util.calculate_mse(rc_net.ReCoNetSD2, cls_n, path, tag, "cpu")
+        out[f"{tag}_meta"] = np.array([seed, T, -1 if ff is None else ff, cls_n])
+        out[f"{tag}_n_out"] = np.array(len(frames))
+        out[f"{tag}_frame0"] = frames[0]
+        out[f"{tag}_rows"] = np.stack([f[:48] for f in frames])
+        out[f"{tag}_sums"] = np.stack([f.reshape(-1, 3).astype(np.int64).sum(0) for f in frames])
+        out[f"{tag}_mse"] = np.array(mse, dtype=np.float64)
+    out["b_ckpt_seed"] = np.array(31)
+    np.savez_compressed(os.path.join(HERE, "rc_infer.npz"), **out)
+    print("inference fixtures written")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["reconet", "adaattn", "sd"]
     if "reconet" in which:
@@ -422,3 +480,5 @@ if __name__ == "__main__":
         gen_adaattn()
     if "sd" in which:
         gen_sd()
+    if "infer" in which:
+        gen_infer()

@@ -1,0 +1,192 @@
+// Video-frame I/O kernels of the ReCoNet inference path (RC/utilities.py:108-235):
+//   * cvframe_to_tensor (RC/utilities.py:108-123): BGR uint8 HWC frame -> RGB fp32 CHW in
+//     [0,255] as `transforms.ToTensor()` then `.mul(255)` computes it (x / 255 * 255, IEEE
+//     division, so a few byte values come back one ulp off x, exactly like the reference);
+//   * Inference.__iter__ (RC/utilities.py:213-227): `clamp(0, 255)` of the stylised frame,
+//     `permute(1, 2, 0)`, `cv2.cvtColor(RGB2BGR)`, `astype("uint8")` (truncation) in one pass,
+//     optionally also writing the clamped fp32 frame (calculate_mse keeps it);
+//   * calculate_mse (RC/utilities.py:126-176): `MSELoss(mean)(x_t1 - x_t, y_t1 - y_t)` of two
+//     consecutive content/stylised frame pairs, written to a device slot (no host sync per frame).
+// All three are HBM-bound streams: 4 pixels per thread, dwordx4 fp32 accesses per plane and
+// three dword accesses for the 12 interleaved bytes.
+#include "vst_common.h"
+#include "vst_hip.h"
+
+namespace {
+
+constexpr int FT = 256;
+constexpr int MAXB = 2048;
+
+__device__ __forceinline__ float to255(uint32_t b) { return ((float)b / 255.0f) * 255.0f; }
+
+__device__ __forceinline__ uint32_t to_u8(float v) {
+  // clamp(0, 255) then numpy float32 -> uint8 (C truncation); NaN stays NaN in the fp32 copy
+  return (uint32_t)(int)v;
+}
+
+__device__ __forceinline__ float clamp255(float v) { return v < 0.f ? 0.f : (v > 255.f ? 255.f : v); }
+
+// one thread = 4 consecutive pixels of one frame; HW % 4 == 0
+__global__ void frames_to_tensor_v4(const uint32_t* __restrict__ src, float* __restrict__ out, long groups,
+                                    long HW4, int swap) {
+  long i = (long)blockIdx.x * FT + threadIdx.x;
+  for (; i < groups; i += (long)gridDim.x * FT) {
+    long n = i / HW4, q = i - n * HW4;
+    const uint32_t* s = src + 3 * i;
+    uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+    uint32_t b[12] = {w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u, w0 >> 24,
+                      w1 & 255u, (w1 >> 8) & 255u, (w1 >> 16) & 255u, w1 >> 24,
+                      w2 & 255u, (w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24};
+    float4* o = reinterpret_cast<float4*>(out) + n * 3 * HW4 + q;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      int sc = swap ? 2 - c : c;
+      o[c * HW4] = make_float4(to255(b[sc]), to255(b[3 + sc]), to255(b[6 + sc]), to255(b[9 + sc]));
+    }
+  }
+}
+
+__global__ void frames_to_tensor_s(const uint8_t* __restrict__ src, float* __restrict__ out, long total, long HW,
+                                   int swap) {
+  long i = (long)blockIdx.x * FT + threadIdx.x;
+  for (; i < total; i += (long)gridDim.x * FT) {
+    long n = i / HW, p = i - n * HW;
+    const uint8_t* s = src + 3 * i;
+    float* o = out + n * 3 * HW + p;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c * HW] = to255(s[swap ? 2 - c : c]);
+  }
+}
+
+__global__ void tensor_to_frames_v4(const float* __restrict__ y, float* __restrict__ clamped, uint32_t* __restrict__ dst,
+                                    long groups, long HW4, int swap) {
+  long i = (long)blockIdx.x * FT + threadIdx.x;
+  for (; i < groups; i += (long)gridDim.x * FT) {
+    long n = i / HW4, q = i - n * HW4;
+    const float4* src = reinterpret_cast<const float4*>(y) + n * 3 * HW4 + q;
+    float4 v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float4 t = src[c * HW4];
+      v[c] = make_float4(clamp255(t.x), clamp255(t.y), clamp255(t.z), clamp255(t.w));
+      if (clamped) reinterpret_cast<float4*>(clamped)[n * 3 * HW4 + q + c * HW4] = v[c];
+    }
+    uint32_t b[12];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      int dc = swap ? 2 - c : c;
+      b[dc] = to_u8(v[c].x);
+      b[3 + dc] = to_u8(v[c].y);
+      b[6 + dc] = to_u8(v[c].z);
+      b[9 + dc] = to_u8(v[c].w);
+    }
+    uint32_t* d = dst + 3 * i;
+    d[0] = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    d[1] = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    d[2] = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
+  }
+}
+
+__global__ void tensor_to_frames_s(const float* __restrict__ y, float* __restrict__ clamped, uint8_t* __restrict__ dst,
+                                   long total, long HW, int swap) {
+  long i = (long)blockIdx.x * FT + threadIdx.x;
+  for (; i < total; i += (long)gridDim.x * FT) {
+    long n = i / HW, p = i - n * HW;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      long k = n * 3 * HW + c * HW + p;
+      float v = clamp255(y[k]);
+      if (clamped) clamped[k] = v;
+      dst[3 * i + (swap ? 2 - c : c)] = (uint8_t)to_u8(v);
+    }
+  }
+}
+
+__global__ void diff_mse_partial(const float* __restrict__ x0, const float* __restrict__ x1,
+                                 const float* __restrict__ y0, const float* __restrict__ y1, long n,
+                                 double* __restrict__ partial) {
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * FT + threadIdx.x; i < n; i += (long)gridDim.x * FT) {
+    float d = (x1[i] - x0[i]) - (y1[i] - y0[i]);
+    s += (double)(d * d);
+  }
+  __shared__ double sh[FT / 64];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < FT / 64; ++w) t += sh[w];
+    partial[blockIdx.x] = t;
+  }
+}
+
+__global__ void diff_mse_finish(const double* __restrict__ partial, int nb, long n, float* __restrict__ out) {
+  __shared__ double sh[FT / 64];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += FT) s += partial[i];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < FT / 64; ++w) t += sh[w];
+    out[0] = (float)(t / (double)n);
+  }
+}
+
+int grid_for(long work) {
+  long b = (work + FT - 1) / FT;
+  return (int)(b < 1 ? 1 : (b > MAXB ? MAXB : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+int vst_frames_to_tensor(const void* frames, float* out, int N, int H, int W, int swap_rb, void* stream) {
+  VST_CHECK_ARG(frames && out && N >= 0 && H >= 0 && W >= 0);
+  long HW = (long)H * W, total = (long)N * HW;
+  if (total == 0) return VST_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (HW % 4 == 0 && ((uintptr_t)frames % 4) == 0 && ((uintptr_t)out % 16) == 0) {
+    long groups = total / 4;
+    hipLaunchKernelGGL(frames_to_tensor_v4, dim3(grid_for(groups)), dim3(FT), 0, s, (const uint32_t*)frames, out,
+                       groups, HW / 4, swap_rb);
+  } else {
+    hipLaunchKernelGGL(frames_to_tensor_s, dim3(grid_for(total)), dim3(FT), 0, s, (const uint8_t*)frames, out, total,
+                       HW, swap_rb);
+  }
+  return vst_launch_status();
+}
+
+int vst_tensor_to_frames(const float* y, float* clamped, void* frames, int N, int H, int W, int swap_rb,
+                         void* stream) {
+  VST_CHECK_ARG(y && frames && N >= 0 && H >= 0 && W >= 0);
+  long HW = (long)H * W, total = (long)N * HW;
+  if (total == 0) return VST_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (HW % 4 == 0 && ((uintptr_t)frames % 4) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)clamped % 16) == 0) {
+    long groups = total / 4;
+    hipLaunchKernelGGL(tensor_to_frames_v4, dim3(grid_for(groups)), dim3(FT), 0, s, y, clamped, (uint32_t*)frames,
+                       groups, HW / 4, swap_rb);
+  } else {
+    hipLaunchKernelGGL(tensor_to_frames_s, dim3(grid_for(total)), dim3(FT), 0, s, y, clamped, (uint8_t*)frames,
+                       total, HW, swap_rb);
+  }
+  return vst_launch_status();
+}
+
+static_assert(MAXB * sizeof(double) == VST_FRAME_MSE_WS_BYTES, "workspace size");
+
+int vst_frame_diff_mse(const float* x0, const float* x1, const float* y0, const float* y1, long n, void* workspace,
+                       float* out, void* stream) {
+  VST_CHECK_ARG(x0 && x1 && y0 && y1 && workspace && out && n > 0);
+  hipStream_t s = (hipStream_t)stream;
+  int nb = grid_for(n);
+  hipLaunchKernelGGL(diff_mse_partial, dim3(nb), dim3(FT), 0, s, x0, x1, y0, y1, n, (double*)workspace);
+  hipLaunchKernelGGL(diff_mse_finish, dim3(1), dim3(FT), 0, s, (const double*)workspace, nb, n, out);
+  return vst_launch_status();
+}
+
+}  // extern "C"

@@ -934,3 +934,52 @@ def flow_warp_mask(flo01, flo10, threshold=2.0):
     mask = _empty((B, H, W), f01)
     lib.vst_flow_warp_mask(ptr(f01), ptr(f10), ptr(mask), B, H, W, float(threshold), stream())
     return mask[0] if single else mask
+
+
+# ---------------------------------------------------------------- video frames (inference path)
+def _ptr_u8(t, name):
+    if not t.is_cuda or t.dtype != torch.uint8 or not t.is_contiguous():
+        raise VstError(f"{name}: need a contiguous uint8 HIP (cuda) tensor; there is no CPU path")
+    return t.data_ptr()
+
+
+def frames_to_tensor(frames, bgr=True, out=None):
+    """RC/utilities.py:108-123 (tensor half of cvframe_to_tensor) on N frames at once:
+    (N,H,W,3) uint8 cv2 frames -> (N,3,H,W) fp32 RGB in [0,255] (ToTensor then mul(255))."""
+    if frames.dim() != 4 or frames.shape[-1] != 3:
+        raise VstError(f"frames must be (N,H,W,3) uint8, got {tuple(frames.shape)}")
+    N, H, W, _ = frames.shape
+    out = torch.empty((N, 3, H, W), dtype=torch.float32, device=frames.device) if out is None else out
+    lib.vst_frames_to_tensor(_ptr_u8(frames, "frames"), ptr(out), N, H, W, int(bgr), stream())
+    return out
+
+
+def tensor_to_frames(y, bgr=True, clamped=None, frames=None):
+    """RC/utilities.py:213-219 on N frames at once: (N,3,H,W) fp32 -> clamp(0,255) -> (N,H,W,3)
+    uint8 (cv2 BGR order, truncating astype).  `clamped` optionally receives the clamped fp32."""
+    y = _check(y, "y", 4)
+    N, C, H, W = y.shape
+    if C != 3:
+        raise VstError(f"stylised frames must have 3 channels, got {C}")
+    if frames is None:
+        frames = torch.empty((N, H, W, 3), dtype=torch.uint8, device=y.device)
+    lib.vst_tensor_to_frames(ptr(y), ptr(clamped), _ptr_u8(frames, "frames"), N, H, W, int(bgr), stream())
+    return frames
+
+
+_DIFF_WS = {}
+FRAME_MSE_WS_BYTES = 16384  # VST_FRAME_MSE_WS_BYTES (include/vst_hip.h)
+
+
+def frame_diff_mse(x0, x1, y0, y1, out):
+    """RC/utilities.py:151-161: out[0] = MSELoss(mean)(x1 - x0, y1 - y0), on the device."""
+    for t, n in ((x0, "x0"), (x1, "x1"), (y0, "y0"), (y1, "y1")):
+        _check(t, n)
+        if t.shape != x0.shape:
+            raise VstError(f"{n}: shape {tuple(t.shape)} != {tuple(x0.shape)}")
+    dev = x0.device
+    ws = _DIFF_WS.get(dev)
+    if ws is None:
+        ws = _DIFF_WS[dev] = torch.empty(FRAME_MSE_WS_BYTES // 4, dtype=torch.float32, device=dev)
+    lib.vst_frame_diff_mse(ptr(x0), ptr(x1), ptr(y0), ptr(y1), x0.numel(), ptr(ws), ptr(out), stream())
+    return out

@@ -46,3 +46,11 @@ def content_style_batch(seed, B, H, W, device="cpu"):
     rng = np.random.default_rng(seed)
     out = [torch.from_numpy(rng.uniform(0.0, 255.0, (B, 3, H, W)).astype(np.float32)).to(device) for _ in range(3)]
     return tuple(out)
+
+
+def video_frames(seed, T, H=360, W=640, step=3):
+    """Synthetic cv2-style clip for the inference path: T x H x W x 3 uint8 BGR frames, frame t
+    the window [t*step, t*step + W) of one seeded noise strip (a horizontal pan)."""
+    rng = np.random.default_rng(seed)
+    strip = rng.integers(0, 256, size=(H, W + step * max(T - 1, 0), 3), dtype=np.uint8)
+    return np.stack([strip[:, t * step:t * step + W] for t in range(T)])
