@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn"),
+    ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn", "reconet_infer"),
                     help="reconet: BASELINE configs 2/3 (the metric); adaattn: config 4's train_video step")
     ap.add_argument("--batch", type=int, default=None, help="frame pairs per GPU (default 8 reconet, 4 adaattn)")
     ap.add_argument("--height", type=int, default=256)
@@ -216,10 +216,54 @@ def build_adaattn(args, dev, rank):
     return lambda: trainer.step(triple)
 
 
+def build_reconet_infer(args, dev, rank):
+    """ReCoNet video inference (RC/utilities.py:179-235) on B frames per
+    step: uint8 BGR frames resident in HBM -> frames_to_tensor -> ReCoNet forward (no_grad) ->
+    clamp + BGR + uint8 (tensor_to_frames).  Frames are independent (input_frame_num=1)."""
+    from vst import ops
+    from vst.reconet import network as N
+    from vst.reconet.dist import shard_seed
+    from vst.synthetic import video_frames
+
+    model = N.ReCoNet().to(dev).eval()
+    frames = torch.from_numpy(video_frames(shard_seed(1234, rank), args.batch, args.height, args.width)).to(dev)
+    out = torch.empty_like(frames)
+
+    def step():
+        with torch.no_grad():
+            x = ops.frames_to_tensor(frames)
+            *_, y = model(x)
+            ops.tensor_to_frames(y, frames=out)
+        return {}
+
+    return step
+
+
+def cpu_baseline_infer(args):
+    """Oracle ReCoNet inference (oracle/reconet_ref.py) on one 360x640 frame."""
+    import oracle
+    from oracle import reconet_ref as R
+    from oracle import shapes
+    from vst.synthetic import video_frames
+
+    torch.set_num_threads(args.cpu_threads)
+    P = oracle.seeded_params(shapes.reconet(), 1)
+    frames = video_frames(5, 1 + args.cpu_steps, args.height, args.width)
+    R.inference(R.reconet_forward, P, frames[:1], 1)  # warm-up
+    t0 = time.perf_counter()
+    R.inference(R.reconet_forward, P, frames[1:], 1)
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {"value": 1.0 / dt, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{args.cpu_steps} frames (+1 warm-up) of synthetic 3x{args.height}x{args.width} video, "
+                      f"oracle/reconet_ref.py inference on torch-CPU fp32, {args.cpu_threads} threads"}
+
+
 def main():
     args = parse()
     if args.batch is None:
-        args.batch = 8 if args.model == "reconet" else 4
+        args.batch = {"reconet": 8, "adaattn": 4, "reconet_infer": 16}[args.model]
+    if args.model == "reconet_infer" and (args.height, args.width) == (256, 512):
+        args.height, args.width = 360, 640  # RC/utilities.py:121 (inference frame size)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -234,7 +278,8 @@ def main():
     ops.use_policy(args.gemm)
     torch.manual_seed(0)  # identical random-init replicas on every rank
     B, H, W = args.batch, args.height, args.width
-    step = (build_reconet if args.model == "reconet" else build_adaattn)(args, dev, rank)
+    step = {"reconet": build_reconet, "adaattn": build_adaattn, "reconet_infer": build_reconet_infer}[args.model](
+        args, dev, rank)
 
     for _ in range(args.warmup):
         out = step()
@@ -256,7 +301,7 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     ks = timer.summary()
-    loss = float(out["loss"].item())
+    loss = float(out["loss"].item()) if "loss" in out else None
 
     result = None
     if rank == 0:
@@ -268,6 +313,11 @@ def main():
             workload = (f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), B={B} frame pairs/GPU, "
                         f"3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}")
             data = "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights"
+        elif args.model == "reconet_infer":
+            metric = f"inference frames/sec at {H}\u00d7{W}, ReCoNet (Inference.__iter__ per-frame chain)"
+            workload = (f"ReCoNet inference: B={B} uint8 BGR frames/GPU resident in HBM -> fp32 planes -> ReCoNet "
+                        f"forward -> clamp/BGR/uint8, 3x{H}x{W}")
+            data = "synthetic (numpy PCG64 noise strip panned 3 px/frame); random-init weights"
         else:
             metric = f"training frame-pairs/sec at {H}\u00d7{W}, AdaAttN train_video step (VGG19 encoder/loss)"
             shape = "config5 shape" if (H, W, B) == (512, 1024, 8) else "config4 shape"
@@ -277,7 +327,7 @@ def main():
         result = {
             "metric": metric,
             "value": value,
-            "unit": "frame-pairs/s",
+            "unit": "frames/s" if args.model == "reconet_infer" else "frame-pairs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -306,10 +356,13 @@ def main():
                          "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
                          "share_of_step": ks["total_ms"] / (1e3 * elapsed)},
         }
-        if world == 1 and not args.no_vgg19:
+        if args.model == "reconet_infer":
+            del result["frames_per_s"]
+        if world == 1 and not args.no_vgg19 and args.model != "reconet_infer":
             result["north_star_vgg19"] = vgg19_subbench(dev)
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = (cpu_baseline if args.model == "reconet" else cpu_baseline_adaattn)(args)
+            result["cpu_baseline"] = {"reconet": cpu_baseline, "adaattn": cpu_baseline_adaattn,
+                                      "reconet_infer": cpu_baseline_infer}[args.model](args)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
