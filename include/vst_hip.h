@@ -294,6 +294,17 @@ int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, lon
 int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
              long step, float gscale, void* stream);
 
+/* ---- RTNSTV (RT/train.py, RT/network.py) --------------------------------------------------
+ * sqrt-TV regulariser (RT/train.py:57-61): out[0] = weight * mean over (nc, y < H-1, x < W-1) of
+ * sqrt(clamp((s[y][x+1]-s[y][x])^2 + (s[y+1][x]-s[y][x])^2, 1e-8)); ws/out as vst_tv_fwd */
+int vst_tv_sqrt_fwd(const float* s, long NC, int H, int W, float weight, float* ws, float* out, void* stream);
+int vst_tv_sqrt_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs,
+                    void* stream);
+/* stylizer output (RT/network.py:93 after the Tanh Conv): y = (tanh(v) + 1) / 2 * 255 (image = 1)
+ * or y = tanh(v) (image = 0, a standalone nn.Tanh); t = tanh(v) is kept for the backward */
+int vst_tanh_image_fwd(const float* v, float* y, float* t, long n, int image, void* stream);
+int vst_tanh_image_bwd(const float* gy, const float* t, float* gv, long n, int image, void* stream);
+
 /* ---- video frames (ReCoNet inference, RC/utilities.py:108-235) -----------------------------
  * cvframe_to_tensor (RC/utilities.py:108-123, the tensor half; cv2.resize stays on the host):
  * frames = N x H x W x 3 uint8 (cv2 BGR order), out = N x 3 x H x W fp32, out = (b / 255) * 255

@@ -9,7 +9,7 @@ Pinned by golden vectors produced by running the reference itself in the build c
 """
 import torch
 
-from . import adaattn_ref, reconet_ref, seeding, shapes  # noqa: F401
+from . import adaattn_ref, reconet_ref, rtnstv_ref, seeding, shapes  # noqa: F401
 
 
 def seeded_params(spec, seed, requires_grad=False):

@@ -80,3 +80,27 @@ def stylizing_network():
         key = f"decoder.{name}.conv.conv" if relu else f"decoder.{name}.conv"
         s += [(key + ".weight", (cout, cin, 3, 3)), (key + ".bias", (cout,))]
     return s
+
+
+def _rt_conv(name, cin, cout, k):
+    return [(name + ".conv.weight", (cout, cin, k, k)), (name + ".conv.bias", (cout,)),
+            (name + ".norm.weight", (cout,)), (name + ".norm.bias", (cout,))]
+
+
+def _rt_deconv(name, cin, cout, k):
+    return [(name + ".deconv.weight", (cin, cout, k, k)), (name + ".deconv.bias", (cout,)),
+            (name + ".norm.weight", (cout,)), (name + ".norm.bias", (cout,))]
+
+
+def rtnstv():
+    """RT/network.py:65-78 StylizingNetwork."""
+    s = _rt_conv("conv1", 3, 16, 3) + _rt_conv("conv2", 16, 32, 3) + _rt_conv("conv3", 32, 48, 3)
+    for i in range(1, 6):
+        s += _rt_conv(f"res{i}.conv1", 48, 48, 3) + _rt_conv(f"res{i}.conv2", 48, 48, 3)
+    return s + _rt_deconv("deconv1", 48, 32, 3) + _rt_deconv("deconv2", 32, 16, 3) + _rt_conv("conv4", 16, 3, 3)
+
+
+def vgg19_rt():
+    """RT/vgg19.py:8-36: torchvision VGG19 features[0:23] as slice1..4 (relu1_2 .. relu4_2)."""
+    return _vgg([(1, 0, 64), (1, 2, 64), (2, 5, 128), (2, 7, 128), (3, 10, 256), (3, 12, 256), (4, 14, 256),
+                 (4, 16, 256), (4, 19, 512), (4, 21, 512)])

@@ -472,6 +472,88 @@ def gen_infer():
     print("inference fixtures written")
 
 
+# --------------------------------------------------------------------------------------------
+# RTNSTV (RT/): the reference's own train.train() for one step
+# --------------------------------------------------------------------------------------------
+RT_DIR = os.path.join(REF, "Real-Time-Neural-Style-Transfer-for-Videos-(RTNSTV)")
+
+
+def gen_rtnstv():
+    _fresh_project(RT_DIR)
+    rt_util = _load("utilities", os.path.join(RT_DIR, "utilities.py"))
+    sys.modules["utilities"] = rt_util
+    rt_net = _load("network", os.path.join(RT_DIR, "network.py"))
+    sys.modules["network"] = rt_net
+    rt_vgg = _load("vgg19", os.path.join(RT_DIR, "vgg19.py"))
+    sys.modules["vgg19"] = rt_vgg
+    out = {}
+    # units: ConvTranspose2d (the one new conv kind) and the forward of the stylizer
+    rng = np.random.default_rng(300)
+    with torch.no_grad():
+        d = rt_net.Deconv(6, 5, 3, 2, torch.nn.ReLU())
+        seed_module(d, 301)
+        x = torch.from_numpy(rng.standard_normal((2, 6, 7, 9)).astype(f32))
+        out["deconv_x"], out["deconv_y"] = _np(x), _np(d.deconv(x))
+        out["deconv_block_y"] = _np(d(x))
+        m = rt_net.StylizingNetwork()
+        seed_module(m, 302)
+        x = torch.from_numpy(rng.uniform(0, 255, (2, 3, 36, 60)).astype(f32))
+        out["net_x"], out["net_y"] = _np(x), _np(m(x))
+    for tag, (B, H, W, seeds) in {"b2": (2, 32, 64, (51, 52, 53, 54)), "b1r": (1, 36, 60, (61, 62, 63, 64))}.items():
+        fake_ds = types.ModuleType("datasets")
+        fake_ds.FlyingThings3D_Monkaa = lambda *a, **k: None
+        fake_ds.Videvo = lambda *a, **k: None
+        sys.modules["datasets"] = fake_ds
+        tr = _load(f"rt_train_{tag}", os.path.join(RT_DIR, "train.py"))
+        style = style_image(seeds[3], H, W)
+        img1, img2, flow, mask = frame_pair_batch(seeds[2], B, H, W, mask_fn=rt_util.flow_warp_mask)
+
+        def net_factory(_s=seeds[0]):
+            net = rt_net.StylizingNetwork()
+            seed_module(net, _s)
+            tr.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(net.named_parameters())))
+            return net
+
+        def vgg_factory(_s=seeds[1]):
+            v = rt_vgg.VGG19()
+            seed_module(v, _s)
+            return v
+
+        class _Img:
+            @staticmethod
+            def open(_p):
+                class _O:
+                    def convert(self, *_):
+                        return self
+
+                return _O()
+
+        tr.device, tr.batch_size, tr.epoch_start, tr.epoch_end = "cpu", B, 1, 1
+        tr.DataLoader = lambda *a, **k: [(img1.clone(), img2.clone(), flow.clone(), mask.clone())]
+        tr.StylizingNetwork, tr.VGG19, tr.Image, tr.tqdm = net_factory, vgg_factory, _Img, _TqdmRecorder
+        tr.toTensor255 = lambda _img, _s=style: _s[0].clone()
+        tr.plt = types.SimpleNamespace(**{k: (lambda *a, **kw: None) for k in
+                                          ("figure", "plot", "xlabel", "ylabel", "title", "legend", "savefig", "close")})
+        tr.os = types.SimpleNamespace(makedirs=lambda *a, **k: None)
+        _TqdmRecorder.records = []
+        save = torch.save
+        torch.save = lambda *a, **k: None
+        try:
+            tr.train()
+        finally:
+            torch.save = save
+        rec = _TqdmRecorder.records[-1]
+        out[f"{tag}_img1"], out[f"{tag}_img2"] = _np(img1), _np(img2)
+        out[f"{tag}_flow"], out[f"{tag}_mask"], out[f"{tag}_style"] = _np(flow), _np(mask), _np(style)
+        out[f"{tag}_seeds"] = np.array(seeds)
+        for k in ("loss", "CL", "SL", "RL", "TL"):
+            out[f"{tag}_{k}"] = np.array(rec[k], dtype=np.float64)
+        adam = tr.optim.Adam
+        _grad_summary(f"{tag}_", adam.grads, adam.after, out, seed=seeds[0] + 1000)
+    np.savez_compressed(os.path.join(HERE, "rt_step.npz"), **out)
+    print("rtnstv fixtures written")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["reconet", "adaattn", "sd"]
     if "reconet" in which:
@@ -482,3 +564,5 @@ if __name__ == "__main__":
         gen_sd()
     if "infer" in which:
         gen_infer()
+    if "rtnstv" in which:
+        gen_rtnstv()

@@ -275,6 +275,87 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   p[i] = p[i] + (-step_size) * (mi / denom);
 }
 
+// RTNSTV regularisation (RT/train.py:57-61): mean over (n, c, y < H-1, x < W-1) of
+// sqrt(clamp(d1^2 + d2^2, 1e-8)), d1 = s[y][x+1] - s[y][x], d2 = s[y+1][x] - s[y][x]
+__device__ __forceinline__ float tv_sqrt_term(const float* p, int W) {
+  float d1 = p[1] - p[0], d2 = p[W] - p[0];
+  float q = d1 * d1 + d2 * d2;
+  return sqrtf(q < 1e-8f ? 1e-8f : q);
+}
+
+__global__ void tv_sqrt_kernel(const float* __restrict__ s, long NC, int H, int W, float* partial) {
+  float acc = 0.f;
+  const long total = NC * (H - 1) * (W - 1);
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < total; i += (long)gridDim.x * RT) {
+    int x = (int)(i % (W - 1));
+    long t = i / (W - 1);
+    int y = (int)(t % (H - 1));
+    long nc = t / (H - 1);
+    acc += tv_sqrt_term(s + nc * H * W + (long)y * W + x, W);
+  }
+  block_partial(acc, 0.f, partial);
+}
+
+// d term(y,x) / d d1 = d1 / r (0 where the clamp is active, as torch's clamp backward), same for d2;
+// gather form: a pixel is p[0] of its own term, p[1] of term (y, x-1) and p[W] of term (y-1, x)
+__device__ __forceinline__ void tv_sqrt_grads(const float* p, int W, float& g1, float& g2) {
+  float d1 = p[1] - p[0], d2 = p[W] - p[0];
+  float q = d1 * d1 + d2 * d2;
+  if (q < 1e-8f) {
+    g1 = g2 = 0.f;
+  } else {
+    float inv = 1.f / (2.f * sqrtf(q));
+    g1 = inv * (2.f * d1);
+    g2 = inv * (2.f * d2);
+  }
+}
+
+__global__ void tv_sqrt_bwd_kernel(const float* __restrict__ s, long NC, int H, int W, const float* __restrict__ gout,
+                                   const float* __restrict__ scale, float* __restrict__ gs) {
+  const float k = gout[0] * scale[1];
+  const long total = NC * H * W;
+  for (long i = (long)blockIdx.x * RT + threadIdx.x; i < total; i += (long)gridDim.x * RT) {
+    int x = (int)(i % W);
+    long t = i / W;
+    int y = (int)(t % H);
+    const float* p = s + i;
+    float g = 0.f, g1, g2;
+    if (y < H - 1 && x < W - 1) {
+      tv_sqrt_grads(p, W, g1, g2);
+      g -= g1 + g2;
+    }
+    if (x >= 1 && y < H - 1) {
+      tv_sqrt_grads(p - 1, W, g1, g2);
+      g += g1;
+    }
+    if (y >= 1 && x < W - 1) {
+      tv_sqrt_grads(p - W, W, g1, g2);
+      g += g2;
+    }
+    gs[i] = k * g;
+  }
+}
+
+// RTNSTV output (RT/network.py:40-44 with Tanh, :93): y = (tanh(v) + 1) / 2 * 255, t saved
+// image = 0: plain nn.Tanh (y = t)
+__global__ void tanh_image_kernel(const float* __restrict__ v, float* __restrict__ y, float* __restrict__ t, long n,
+                                  int image) {
+  long i = (long)blockIdx.x * RT + threadIdx.x;
+  if (i >= n) return;
+  float th = tanhf(v[i]);
+  t[i] = th;
+  y[i] = image ? ((th + 1.0f) / 2.0f) * 255.0f : th;
+}
+
+__global__ void tanh_image_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ t, float* __restrict__ gv,
+                                      long n, int image) {
+  long i = (long)blockIdx.x * RT + threadIdx.x;
+  if (i >= n) return;
+  float th = t[i];
+  float g = image ? (gy[i] * 255.0f) / 2.0f : gy[i];
+  gv[i] = g * (1.0f - th * th);
+}
+
 static int nblocks(long work) {
   long b = (work + RT - 1) / RT;
   return (int)(b < 1 ? 1 : (b > MAXB ? MAXB : b));
@@ -352,6 +433,35 @@ int vst_tv_fwd(const float* s, long NC, int H, int W, float weight, float* ws, f
 int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs, void* stream) {
   VST_CHECK_ARG(s && gout && out && gs && NC > 0 && H > 1 && W > 1);
   tv_bwd_kernel<<<nblocks(NC * H * W), RT, 0, (hipStream_t)stream>>>(s, NC, H, W, gout, out, gs);
+  return vst_launch_status();
+}
+
+int vst_tv_sqrt_fwd(const float* s, long NC, int H, int W, float weight, float* ws, float* out, void* stream) {
+  VST_CHECK_ARG(s && ws && out && NC > 0 && H > 1 && W > 1);
+  hipStream_t st = (hipStream_t)stream;
+  long terms = NC * (H - 1) * (W - 1);
+  int g = nblocks(terms);
+  tv_sqrt_kernel<<<g, RT, 0, st>>>(s, NC, H, W, ws);
+  finish_kernel<<<1, RT, 0, st>>>(ws, g, out, weight, (double)terms, 0);
+  return vst_launch_status();
+}
+
+int vst_tv_sqrt_bwd(const float* s, long NC, int H, int W, const float* gout, const float* out, float* gs,
+                    void* stream) {
+  VST_CHECK_ARG(s && gout && out && gs && NC > 0 && H > 1 && W > 1);
+  tv_sqrt_bwd_kernel<<<nblocks(NC * H * W), RT, 0, (hipStream_t)stream>>>(s, NC, H, W, gout, out, gs);
+  return vst_launch_status();
+}
+
+int vst_tanh_image_fwd(const float* v, float* y, float* t, long n, int image, void* stream) {
+  VST_CHECK_ARG(v && y && t && n > 0);
+  tanh_image_kernel<<<ceil_div(n, RT), RT, 0, (hipStream_t)stream>>>(v, y, t, n, image);
+  return vst_launch_status();
+}
+
+int vst_tanh_image_bwd(const float* gy, const float* t, float* gv, long n, int image, void* stream) {
+  VST_CHECK_ARG(gy && t && gv && n > 0);
+  tanh_image_bwd_kernel<<<ceil_div(n, RT), RT, 0, (hipStream_t)stream>>>(gy, t, gv, n, image);
   return vst_launch_status();
 }
 

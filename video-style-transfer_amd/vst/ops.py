@@ -660,13 +660,15 @@ class GramFn(Function):
     """gram_matrix (RC/utilities.py:93-98): F F^T / (C H W) per sample, MFMA split-K."""
 
     @staticmethod
-    def forward(ctx, y):
+    def forward(ctx, y, per_hw=False):
+        """per_hw: divide by H*W only (RT/utilities.py:155-160) instead of C*H*W."""
         y = _check(y, "gram input", 4)
         N, C, H, W = y.shape
         g = _empty((N, C, C), y)
         ws = _empty((lib.vst_wgrad_workspace(N, C, C, H * W),), y)
         gemm_role("fwd")
-        lib.vst_gram(ptr(y), ptr(g), ptr(ws), N, C, H * W, 1.0 / (C * H * W), stream())
+        ctx.scale = 1.0 / (H * W) if per_hw else 1.0 / (C * H * W)
+        lib.vst_gram(ptr(y), ptr(g), ptr(ws), N, C, H * W, ctx.scale, stream())
         ctx.save_for_backward(y)
         return g
 
@@ -677,13 +679,13 @@ class GramFn(Function):
         Mpad, Kpad = pack_dims(C, C)
         S = _empty((N * pack_floats(Mpad, Kpad),), y)
         gemm_role("dgrad")
-        lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, 1.0 / (C * H * W), stream())
+        lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, ctx.scale, stream())
         dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=pack_floats(Mpad, Kpad))
-        return dy.view(N, C, H, W)
+        return dy.view(N, C, H, W), None
 
 
-def gram_matrix(y):
-    return GramFn.apply(y)
+def gram_matrix(y, per_hw=False):
+    return GramFn.apply(y, per_hw)
 
 
 class VggNormalizeFn(Function):
@@ -983,3 +985,119 @@ def frame_diff_mse(x0, x1, y0, y1, out):
         ws = _DIFF_WS[dev] = torch.empty(FRAME_MSE_WS_BYTES // 4, dtype=torch.float32, device=dev)
     lib.vst_frame_diff_mse(ptr(x0), ptr(x1), ptr(y0), ptr(y1), x0.numel(), ptr(ws), ptr(out), stream())
     return out
+
+
+# ---------------------------------------------------------------- RTNSTV (RT/network.py, RT/train.py)
+class ConvTranspose2dFn(Function):
+    """nn.ConvTranspose2d(Cin, Cout, k, stride, padding, output_padding) (RT/network.py:50-52) as the
+    data gradient of the zero-padded strided conv it transposes: forward = transposed implicit GEMM
+    (the conv dgrad kernel), input grad = that conv's forward GEMM, weight grad = its wgrad GEMM
+    with the roles of input and output-gradient swapped.  bias_const as in Conv2dFn (the following
+    InstanceNorm's backward produces the bias gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, out_pad, bias_const=None):
+        x = _check(x, "conv_transpose input", 4)
+        w = w.contiguous()
+        N, Cin, H, W = x.shape
+        if w.shape[0] != Cin or w.shape[2] != w.shape[3]:
+            raise VstError(f"conv_transpose: weight {tuple(w.shape)} does not match input channels {Cin}")
+        Cout, ks = w.shape[1], w.shape[2]
+        Ho = (H - 1) * stride - 2 * pad + ks + out_pad
+        Wo = (W - 1) * stride - 2 * pad + ks + out_pad
+        if conv_out_hw(Ho, Wo, ks, stride, pad, 1) != (H, W):
+            raise VstError("conv_transpose: output size is not the transposed conv's input size")
+        if bias_const is not None:
+            b = bias_const
+        gemm_role("fwd")
+        flops = 2.0 * N * Cin * H * W * Cout * ks * ks
+        out = conv_gemm(x, packed_weight(w, transposed=True), Cout, ks, Ho, Wo, GM_TRANSPOSED, stride, pad, 1,
+                        epi=EPI_BIAS if b is not None else 0, bias=b.contiguous() if b is not None else None,
+                        algo_flops=flops)
+        ctx.geom = (ks, stride, pad)
+        ctx.has_bias = b is not None and bias_const is None
+        ctx.params = (w, b)
+        ctx.save_for_backward(x, w)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        ks, stride, pad = ctx.geom
+        gy = gy.contiguous()
+        N, Cin, H, W = x.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            gemm_role("dgrad")
+            dx = conv_gemm(gy, packed_weight(w, False), Cin, ks, H, W, GM_ZERO, stride, pad, 1)
+        if ctx.needs_input_grad[1]:
+            sink = grad_sink(ctx.params[0])
+            dw = conv_wgrad(x, gy, w.shape, ks, stride, pad, "zero", 1, out=sink)
+            dw = None if sink is not None else dw
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            sink = grad_sink(ctx.params[1])
+            db = channel_sum(gy, out=sink)
+            db = None if sink is not None else db
+        return dx, dw, db, None, None, None, None
+
+
+def conv_transpose2d(x, w, b=None, stride=2, pad=1, out_pad=1):
+    return ConvTranspose2dFn.apply(x, w, b, stride, pad, out_pad)
+
+
+def conv_transpose_instance_norm(x, w, b, gamma, beta, stride=2, pad=1, out_pad=1, relu=False, eps=1e-5):
+    """ConvTranspose2d [+bias] -> InstanceNorm(affine) [-> ReLU] (RT/network.py:55-60)."""
+    if b is None:
+        return instance_norm(conv_transpose2d(x, w, None, stride, pad, out_pad), gamma, beta, relu, None, eps)
+    y = ConvTranspose2dFn.apply(x, w, None, stride, pad, out_pad, b.detach())
+    return InstanceNormFn.apply(y, gamma, beta, None, relu, eps, b)
+
+
+class TanhImageFn(Function):
+    """(tanh(v) + 1) / 2 * 255 (RT/network.py:93 after conv4's Tanh), or plain tanh (image=False)."""
+
+    @staticmethod
+    def forward(ctx, v, image=True):
+        v = _check(v, "tanh_image input")
+        y, t = _empty(v.shape, v), _empty(v.shape, v)
+        lib.vst_tanh_image_fwd(ptr(v), ptr(y), ptr(t), v.numel(), int(image), stream())
+        ctx.image = bool(image)
+        ctx.save_for_backward(t)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (t,) = ctx.saved_tensors
+        gv = _empty(t.shape, t)
+        lib.vst_tanh_image_bwd(ptr(gy.contiguous()), ptr(t), ptr(gv), t.numel(), int(ctx.image), stream())
+        return gv, None
+
+
+def tanh_image(v, image=True):
+    return TanhImageFn.apply(v, image)
+
+
+class TVSqrtFn(Function):
+    """weight * mean(sqrt(clamp(dx^2 + dy^2, 1e-8))) over [:, :, :-1, :-1] (RT/train.py:57-61)."""
+
+    @staticmethod
+    def forward(ctx, s, weight):
+        s = _check(s, "tv input", 4)
+        N, C, H, W = s.shape
+        ws = _empty((LOSS_WS,), s)
+        st = _empty((3,), s)
+        lib.vst_tv_sqrt_fwd(ptr(s), N * C, H, W, float(weight), ptr(ws), ptr(st), stream())
+        ctx.save_for_backward(s, st)
+        return st[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        s, st = ctx.saved_tensors
+        N, C, H, W = s.shape
+        gs = _empty(s.shape, s)
+        lib.vst_tv_sqrt_bwd(ptr(s), N * C, H, W, ptr(g.contiguous()), ptr(st), ptr(gs), stream())
+        return gs, None
+
+
+def tv_sqrt_loss(s, weight):
+    return TVSqrtFn.apply(s, weight)
