@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn", "reconet_infer"),
+    ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn", "reconet_infer", "dataprep"),
                     help="reconet: BASELINE configs 2/3 (the metric); adaattn: config 4's train_video step")
     ap.add_argument("--batch", type=int, default=None, help="frame pairs per GPU (default 8 reconet, 4 adaattn)")
     ap.add_argument("--height", type=int, default=256)
@@ -258,10 +258,109 @@ def cpu_baseline_infer(args):
                       f"oracle/reconet_ref.py inference on torch-CPU fp32, {args.cpu_threads} threads"}
 
 
+def run_dataprep(args, dev, rank, world):
+    """the device half of FlyingThings3D / Monkaa `__getitem__`
+    (RC/datasets.py:114-146) for B frame pairs per step, inputs resident in HBM at the dataset's
+    source size (960x540 PNG frames / PGM motion boundaries as uint8, PFM flows as raw float bits)
+    -> 640x360 training items (vst.reconet.datasets.prepare_staged's kernels)."""
+    import numpy as np
+
+    from vst import ops
+    from vst.reconet.dist import shard_seed
+
+    B, (Hs, Ws), (Ho, Wo) = args.batch, (540, 960), (360, 640)
+    rng = np.random.default_rng(shard_seed(1234, rank))
+    frames = torch.from_numpy(rng.integers(0, 256, (2 * B, Hs, Ws, 3), dtype=np.uint8)).to(dev)
+    motion = torch.from_numpy(np.where(rng.random((B, Hs, Ws)) < 0.05, 255, 0).astype(np.uint8)).to(dev)
+    flows = torch.from_numpy(rng.uniform(-20, 20, (2 * B, Hs, Ws, 3)).astype("<f4").view(np.int32)).to(dev)
+    img = torch.empty((2 * B, 3, Ho, Wo), device=dev)
+    fl = torch.empty((2 * B, 2, Ho, Wo), device=dev)
+
+    def resize_frames():
+        ops.pil_resize_to_tensor255(frames, (Wo, Ho), out=img)
+
+    def step():
+        resize_frames()
+        ops.flow_prep(flows, False, (Wo, Ho), out=fl)
+        mask = ops.flow_warp_mask(fl[:B], fl[B:])
+        ops.apply_motion_mask(mask, motion)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    # dominant kernel: the Pillow-exact frame resize, timed with HIP events on its own stream
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record(st)
+    for _ in range(reps):
+        resize_frames()
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = 1e3 * e0.elapsed_time(e1) / reps
+    algo = 2 * B * (Hs * Ws * 3 + 3 * Ho * Wo * 4)  # uint8 HWC frames in, fp32 planes out
+    if rank != 0:
+        return None
+    result = {
+        "metric": "frame-pair items/sec, FlyingThings3D __getitem__ device half (960x540 -> 640x360)",
+        "value": B * world * args.steps / elapsed, "unit": "items/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32",
+        "data": "synthetic (numpy PCG64 uint8 frames, 5% motion-boundary pixels, U(-20,20) flows)",
+        "config": {"workload": f"dataprep: B={B} items/GPU, frames+motion 960x540 uint8, PFM flows 960x540x3 "
+                               f"-> img1/img2 3x360x640, flow 2x360x640, mask 360x640", "global_batch": B * world,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": "pil_resize_kernel (frames, mode 0)", "achieved": algo / us / 1e3,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo / us / 1e3 / HBM_PEAK_GBS,
+                     "traffic": None, "algo_bytes_per_launch": algo, "avg_launch_us": us},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_dataprep(args)
+    print(json.dumps(result), flush=True)
+    return result
+
+
+def cpu_baseline_dataprep(args):
+    """The oracle's item pipeline (Pillow resize + torch-CPU flow resize + oracle mask) per item."""
+    import numpy as np
+
+    from oracle import dataprep_ref as D
+    from oracle import reconet_ref as R
+
+    torch.set_num_threads(args.cpu_threads)
+    rng = np.random.default_rng(7)
+    n = max(args.cpu_steps, 2)
+    items = [([rng.integers(0, 256, (540, 960, 3), dtype=np.uint8) for _ in range(2)],
+              rng.uniform(-20, 20, (540, 960, 3)).astype(np.float32),
+              rng.uniform(-20, 20, (540, 960, 3)).astype(np.float32),
+              np.where(rng.random((540, 960)) < 0.05, 255, 0).astype(np.uint8)) for _ in range(n + 1)]
+    D.getitem(*items[0], (640, 360), R.flow_warp_mask)
+    t0 = time.perf_counter()
+    for it in items[1:]:
+        D.getitem(*it, (640, 360), R.flow_warp_mask)
+    dt = (time.perf_counter() - t0) / n
+    return {"value": 1.0 / dt, "unit": "items/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{n} items (+1 warm-up), decoded inputs, oracle/dataprep_ref.getitem (numpy Pillow "
+                      f"restatement + torch-CPU bilinear + oracle flow_warp_mask), {args.cpu_threads} threads"}
+
+
 def main():
     args = parse()
     if args.batch is None:
-        args.batch = {"reconet": 8, "adaattn": 4, "reconet_infer": 16}[args.model]
+        args.batch = {"reconet": 8, "adaattn": 4, "reconet_infer": 16, "dataprep": 8}[args.model]
     if args.model == "reconet_infer" and (args.height, args.width) == (256, 512):
         args.height, args.width = 360, 640  # RC/utilities.py:121 (inference frame size)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,6 +374,8 @@ def main():
 
     from vst import kprof, ops
 
+    if args.model == "dataprep":
+        return run_dataprep(args, dev, rank, world)
     ops.use_policy(args.gemm)
     torch.manual_seed(0)  # identical random-init replicas on every rank
     B, H, W = args.batch, args.height, args.width

@@ -321,6 +321,32 @@ int vst_tensor_to_frames(const float* y, float* clamped, void* frames, int N, in
 int vst_frame_diff_mse(const float* x0, const float* x1, const float* y0, const float* y1, long n, void* workspace,
                        float* out, void* stream);
 
+/* ---- frame-pair preparation of the flow datasets (RC/datasets.py:114-155, 210-251) ----------
+ * Pillow Image.resize(size, BILINEAR) coefficient tables for one axis (Pillow Resample.c
+ * precompute_coeffs + normalize_coeffs_8bpc, host-side, no GPU): bounds = out_size x {min, count},
+ * kk = out_size x ksize 22-bit fixed-point taps.  Returns 0, or the needed ksize (> 0) when
+ * ksize_cap is too small. */
+int vst_pil_bilinear_coeffs(int in_size, int out_size, int* bounds, int* kk, int ksize_cap);
+/* src = N x Hs x Ws x C uint8 (PIL raster, C = 3 for .convert("RGB") frames, 1 for the motion
+ * boundary images); tables from vst_pil_bilinear_coeffs on the device.  mode 0: out = N x C x Ho x Wo
+ * fp32 = toTensor255 of the resized image (RC/datasets.py:116-118); mode 1 (C = 1): out = N x Ho x Wo
+ * flow mask, multiplied in place by the motion mask 1 - (resized != 0) (RC/datasets.py:138-144). */
+int vst_pil_resize_u8(const void* src, float* out, int N, int Hs, int Ws, int C, int Ho, int Wo, const void* hbounds,
+                      const void* hk, int hks, const void* vbounds, const void* vk, int vks, int mode, void* stream);
+/* raw = N x Hs x Ws x Cr float32 PFM payloads in file order (bottom-up rows; byte-swapped on the
+ * fly when big_endian) -> out = N x 2 x Ho x Wo: flipud, [:-1] channel drop (first 2 channels),
+ * F.interpolate(bilinear, align_corners=False), channel 0 * sx, channel 1 * sy
+ * (RC/datasets.py:121-136; the reference scales x by Ho/Hs and y by Wo/Ws). */
+int vst_flow_prep(const void* raw, float* out, int N, int Hs, int Ws, int Cr, int big_endian, int Ho, int Wo,
+                  float sx, float sy, void* stream);
+/* flowlib.readPFM (RC/flowlib.py:34-64), host-side: header parse ("PF" -> 3 channels, "Pf" -> 1;
+ * "W H" line as re '^(\d+)\s(\d+)\s$'; scale < 0 -> little-endian).  Errors carry the reference's
+ * messages ("Not a PFM file.", "Malformed PFM header."); the payload must hold exactly
+ * W*H*channels floats (np.reshape raised otherwise).  vst_pfm_read copies the raw payload bytes. */
+int vst_pfm_read_header(const char* path, int* width, int* height, int* channels, int* big_endian, int* offset,
+                        float* scale);
+int vst_pfm_read(const char* path, void* dst, long bytes, int offset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -554,6 +554,50 @@ def gen_rtnstv():
     print("rtnstv fixtures written")
 
 
+# --------------------------------------------------------------------------------------------
+# Flow-dataset frame-pair preparation: the reference's own FlyingThings3D / Monkaa __getitem__
+# over tiny on-disk trees written by oracle/dataprep_ref.write_tree (deterministic in the seed)
+# --------------------------------------------------------------------------------------------
+DP_CASES = (
+    # tag, kind, seed, source H, W, folders, frames/folder, resolution (W, H), frame_num, items
+    ("ft", "ft3d", 61, 36, 60, 1, 10, (40, 24), 1, (0, 4, 13, 26)),
+    ("mk", "monkaa", 62, 20, 30, 2, 5, (48, 32), 2, (0, 2, 5)),
+)
+
+
+def gen_dataprep():
+    import shutil
+
+    from oracle import dataprep_ref as D
+
+    _fresh_project(RC_DIR)
+    for n in ("utilities", "flowlib", "datasets"):
+        sys.modules[n] = _load(n, os.path.join(RC_DIR, n + ".py"))
+    ds_mod = sys.modules["datasets"]
+    ds_mod.tqdm = lambda *a, **k: _NullBar()
+    out = {}
+    for tag, kind, seed, H, W, folders, fpf, res, fn, items in DP_CASES:
+        root = os.path.join("/tmp", "vst_gen_dp", tag)
+        shutil.rmtree(root, ignore_errors=True)
+        D.write_tree(root, kind, seed, H, W, folders, fpf)
+        cls = ds_mod.FlyingThings3D if kind == "ft3d" else ds_mod.Monkaa
+        ds = cls(root, resolution=res, frame_num=fn)
+        out[f"{tag}_len"] = np.array(len(ds))
+        for i in items:
+            img1, img2, flow, mask = ds[i]
+            out[f"{tag}_{i}_img1"] = _np(img1)
+            out[f"{tag}_{i}_img2"] = _np(img2)
+            out[f"{tag}_{i}_flow"] = _np(flow)
+            out[f"{tag}_{i}_mask"] = _np(mask)
+    np.savez_compressed(os.path.join(HERE, "dp_items.npz"), **out)
+    print("dataprep fixtures written")
+
+
+class _NullBar:
+    def update(self, *_):
+        pass
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["reconet", "adaattn", "sd"]
     if "reconet" in which:
@@ -566,3 +610,5 @@ if __name__ == "__main__":
         gen_infer()
     if "rtnstv" in which:
         gen_rtnstv()
+    if "dataprep" in which:
+        gen_dataprep()

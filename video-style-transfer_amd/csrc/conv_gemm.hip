@@ -255,6 +255,10 @@ const char* vst_strerror(int code) {
   if (code == VST_OK) return "success";
   if (code == VST_EINVAL) return "vst: invalid argument";
   if (code == VST_EUNSUPPORTED) return "vst: unsupported configuration";
+  if (code == VST_EIO) return "vst: cannot open file";
+  if (code == VST_EPFM_MAGIC) return "Not a PFM file.";
+  if (code == VST_EPFM_HEADER) return "Malformed PFM header.";
+  if (code == VST_EPFM_SIZE) return "PFM data size does not match its header";
   return hipGetErrorString((hipError_t)code);
 }
 

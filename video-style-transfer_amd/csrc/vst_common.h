@@ -6,6 +6,10 @@
 #define VST_OK 0
 #define VST_EINVAL (-1)
 #define VST_EUNSUPPORTED (-2)
+#define VST_EIO (-3)
+#define VST_EPFM_MAGIC (-4)
+#define VST_EPFM_HEADER (-5)
+#define VST_EPFM_SIZE (-6)
 
 #define VST_CHECK_ARG(cond) \
   do {                      \

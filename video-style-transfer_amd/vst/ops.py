@@ -1101,3 +1101,94 @@ class TVSqrtFn(Function):
 
 def tv_sqrt_loss(s, weight):
     return TVSqrtFn.apply(s, weight)
+
+
+# ---------------------------------------------------- flow-dataset frame-pair preparation
+def _ptr_typed(t, dtype, name):
+    if not t.is_cuda or t.dtype != dtype or not t.is_contiguous():
+        raise VstError(f"{name}: need a contiguous {dtype} HIP (cuda) tensor; there is no CPU path")
+    return t.data_ptr()
+
+
+def pil_bilinear_coeffs(in_size, out_size):
+    """Host-side Pillow BILINEAR tables for one axis (vst_pil_bilinear_coeffs):
+    (bounds (out, 2) int32, kk (out, ksize) int32)."""
+    import numpy as np
+
+    ksize = 3
+    while True:
+        bounds = np.zeros((out_size, 2), np.int32)
+        kk = np.zeros((out_size, ksize), np.int32)
+        need = lib.load().vst_pil_bilinear_coeffs(
+            in_size, out_size, bounds.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+            kk.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ksize)
+        if need == 0:
+            return bounds, kk
+        if need < 0:
+            raise VstError(f"vst_pil_bilinear_coeffs({in_size}, {out_size}) failed (rc={need})")
+        ksize = need
+
+
+_PIL_TABLES = {}
+
+
+def _pil_tables(in_size, out_size, device):
+    key = (in_size, out_size, str(device))
+    t = _PIL_TABLES.get(key)
+    if t is None:
+        b, k = pil_bilinear_coeffs(in_size, out_size)
+        t = (torch.from_numpy(b).to(device), torch.from_numpy(k).to(device), k.shape[1])
+        _PIL_TABLES[key] = t
+    return t
+
+
+def _pil_resize(src, size, out, mode):
+    N, Hs, Ws, C = src.shape
+    Wo, Ho = size
+    hb, hk, hks = _pil_tables(Ws, Wo, src.device)
+    vb, vk, vks = _pil_tables(Hs, Ho, src.device)
+    ip = lambda t: _ptr_typed(t, torch.int32, "pil table")  # noqa: E731
+    lib.vst_pil_resize_u8(_ptr_u8(src, "images"), ptr(out), N, Hs, Ws, C, Ho, Wo, ip(hb), ip(hk), hks, ip(vb),
+                          ip(vk), vks, mode, stream())
+    return out
+
+
+def pil_resize_to_tensor255(images, size, out=None):
+    """`toTensor255(Image.fromarray(img).resize(size, Image.BILINEAR))` (RC/datasets.py:116-118) for
+    N images at once: (N, Hs, Ws, C) uint8 -> (N, C, H, W) fp32, size = (W, H) as PIL takes it.
+    Bit-exact with Pillow's 8-bit resampler."""
+    if images.dim() != 4:
+        raise VstError(f"images must be (N,H,W,C) uint8, got {tuple(images.shape)}")
+    N, _, _, C = images.shape
+    Wo, Ho = size
+    out = torch.empty((N, C, Ho, Wo), dtype=torch.float32, device=images.device) if out is None else out
+    if tuple(out.shape) != (N, C, Ho, Wo):
+        raise VstError(f"pil resize: out shape {tuple(out.shape)} != {(N, C, Ho, Wo)}")
+    return _pil_resize(images, size, out, 0)
+
+
+def apply_motion_mask(mask, motion):
+    """mask *= 1 - (toTensor(motion.resize(size, BILINEAR)) != 0) (RC/datasets.py:138-144), in place:
+    mask (N, H, W) fp32 0/1, motion (N, Hs, Ws) uint8 boundary images."""
+    if motion.dim() != 3 or mask.dim() != 3 or motion.shape[0] != mask.shape[0]:
+        raise VstError("motion mask: need mask (N,H,W) fp32 and motion (N,Hs,Ws) uint8")
+    N, Ho, Wo = mask.shape
+    _pil_resize(motion.unsqueeze(-1), (Wo, Ho), mask, 1)
+    return mask
+
+
+def flow_prep(raw, big_endian, size, out=None):
+    """RC/datasets.py:121-136 for N flows: raw = (N, Hs, Ws, Cr) int32 tensor holding the PFM
+    payload bits in file order (bottom-up rows, `big_endian` byte order) -> (N, 2, H, W) fp32 =
+    flipud, [:-1], bilinear resize to size = (W, H), then the reference's per-channel rescale
+    (x by H/Hs, y by W/Ws -- the factors RC/datasets.py:133-136 apply)."""
+    if raw.dim() != 4 or raw.shape[-1] < 2:
+        raise VstError(f"raw flows must be (N,H,W,C>=2), got {tuple(raw.shape)}")
+    N, Hs, Ws, Cr = raw.shape
+    Wo, Ho = size
+    out = torch.empty((N, 2, Ho, Wo), dtype=torch.float32, device=raw.device) if out is None else out
+    # the reference multiplies a float32 tensor by a Python float: the factor rounds to fp32
+    sx, sy = Ho / Hs, Wo / Ws
+    lib.vst_flow_prep(_ptr_typed(raw, torch.int32, "raw flows"), ptr(out), N, Hs, Ws, Cr, int(bool(big_endian)), Ho,
+                      Wo, sx, sy, stream())
+    return out
