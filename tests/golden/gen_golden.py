@@ -585,6 +585,8 @@ def gen_dataprep():
         out[f"{tag}_len"] = np.array(len(ds))
         for i in items:
             img1, img2, flow, mask = ds[i]
+            # the reference orders sequence folders by os.listdir (filesystem order): key items by path
+            out[f"{tag}_{i}_key"] = np.array(os.path.relpath(ds.frame[i][0], root))
             out[f"{tag}_{i}_img1"] = _np(img1)
             out[f"{tag}_{i}_img2"] = _np(img2)
             out[f"{tag}_{i}_flow"] = _np(flow)

@@ -20,7 +20,7 @@ from oracle import dataprep_ref as D
 from oracle import reconet_ref as R
 
 SHAPES = [(54, 96, 36, 64), (540, 960, 360, 640), (33, 47, 64, 90), (20, 20, 20, 13), (17, 31, 17, 31),
-          (7, 9, 3, 2)]
+          (7, 9, 3, 2), (200, 400, 20, 30), (130, 70, 31, 17)]
 
 
 def _rand_img(rng, H, W, C):
@@ -93,6 +93,18 @@ def _cases():
     )
 
 
+def _golden_index(ds, root, g, tag, i):
+    """Index of golden item i in `ds`: the reference (and the drop-in) order sequence folders by
+    os.listdir, which is filesystem order, so items are matched by their first frame's path."""
+    import os
+
+    key = str(g[f"{tag}_{i}_key"])
+    for j, entry in enumerate(ds.frame):
+        if os.path.relpath(entry[0], root) == key:
+            return j
+    raise AssertionError(f"{key} not indexed")
+
+
 def _oracle_item(ds, i):
     fpaths, (ffut, fpast), mpath = ds.entries(i)
     frames = [np.asarray(Image.open(p).convert("RGB")) for p in fpaths]
@@ -114,7 +126,7 @@ def test_oracle_items_match_reference(tmp_path, golden, case):
     ds = cls(root, resolution=res, frame_num=fn)
     assert len(ds) == int(g[f"{tag}_len"])
     for i in items:
-        img1, img2, flow, mask = _oracle_item(ds, i)
+        img1, img2, flow, mask = _oracle_item(ds, _golden_index(ds, root, g, tag, i))
         np.testing.assert_array_equal(img1.numpy(), g[f"{tag}_{i}_img1"])
         np.testing.assert_array_equal(img2.numpy(), g[f"{tag}_{i}_img2"])
         np.testing.assert_allclose(flow.numpy(), g[f"{tag}_{i}_flow"], rtol=1e-6, atol=1e-6)
@@ -171,7 +183,7 @@ def test_dataset_items_match_reference(tmp_path, golden, case):
     ds = cls(root, resolution=res, frame_num=fn)
     flips = 0
     for i in items:
-        img1, img2, flow, mask = (t.cpu() for t in ds[i])
+        img1, img2, flow, mask = (t.cpu() for t in ds[_golden_index(ds, root, g, tag, i)])
         assert img1.is_contiguous() or fn > 1
         np.testing.assert_array_equal(img1.numpy(), g[f"{tag}_{i}_img1"])
         np.testing.assert_array_equal(img2.numpy(), g[f"{tag}_{i}_img2"])

@@ -37,45 +37,134 @@ __device__ __forceinline__ int clip8(int v) {
   return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
+constexpr int HALF = 1 << (PIL_PRECISION_BITS - 1);
+
+template <int C>
+__device__ __forceinline__ void store_pixel(float* __restrict__ out, long n, long p, long HWo, const int (&acc)[C],
+                                            int mode) {
+  if (mode == 0) {
+    float* o = out + n * C * HWo + p;
+#pragma unroll
+    for (int c = 0; c < C; ++c) o[c * HWo] = ((float)clip8(acc[c]) / 255.0f) * 255.0f;
+  } else {
+    if (clip8(acc[0]) != 0) out[n * HWo + p] = 0.f;
+  }
+}
+
+// Output tile of one workgroup: TX columns x TY rows of one image.  The source window it needs is
+// staged in LDS (coalesced byte rows), the horizontal pass writes its uint8 rows to LDS, the
+// vertical pass reads them: every source byte is read from HBM/L2 once per tile instead of once
+// per tap of every output pixel.  Windows larger than the LDS budget (strong downscales) take
+// the per-pixel path, block-uniformly.
+constexpr int TX = 64, TY = 16;
+constexpr int SRC_ROWS = 48, SRC_ROW_BYTES = 512;
+
 // src: N x Hs x Ws x C uint8 (PIL's interleaved raster); hb/vb: {min, count} per output column /
-// row; hk/vk: fixed-point taps, hks/vks per output coordinate.
+// row (monotone in the output coordinate); hk/vk: fixed-point taps, hks/vks per output coordinate.
 // mode 0: out = N x C x Ho x Wo fp32, (b / 255) * 255;
 // mode 1 (C == 1): out = N x Ho x Wo flow mask, multiplied by the motion mask (b == 0).
-__global__ void pil_resize_kernel(const uint8_t* __restrict__ src, float* __restrict__ out, int N, int Hs, int Ws,
-                                  int C, int Ho, int Wo, const int* __restrict__ hb, const int* __restrict__ hk,
-                                  int hks, const int* __restrict__ vb, const int* __restrict__ vk, int vks,
-                                  int mode) {
+template <int C>
+__global__ __launch_bounds__(PT) void pil_resize_kernel(const uint8_t* __restrict__ src, float* __restrict__ out,
+                                                        int Hs, int Ws, int Ho, int Wo, int tiles_x, int tiles_y,
+                                                        const int* __restrict__ hb, const int* __restrict__ hk,
+                                                        int hks, const int* __restrict__ vb,
+                                                        const int* __restrict__ vk, int vks, int mode) {
+  __shared__ uint8_t s_src[SRC_ROWS * SRC_ROW_BYTES];
+  __shared__ uint8_t s_h[SRC_ROWS * TX * C];
+  const int tiles = tiles_x * tiles_y;
+  const long n = blockIdx.x / tiles;
+  const int t = blockIdx.x - (int)n * tiles;
+  const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
+  const int txv = min(TX, Wo - tx0), tyv = min(TY, Ho - ty0);
   const long HWo = (long)Ho * Wo;
-  const long total = (long)N * HWo;
-  for (long i = (long)blockIdx.x * PT + threadIdx.x; i < total; i += (long)gridDim.x * PT) {
-    const long n = i / HWo;
-    const long p = i - n * HWo;
-    const int yy = (int)(p / Wo), xx = (int)(p - (long)yy * Wo);
-    const int xmin = hb[2 * xx], xcnt = hb[2 * xx + 1];
-    const int ymin = vb[2 * yy], ycnt = vb[2 * yy + 1];
-    const int* kx = hk + (long)xx * hks;
-    const int* ky = vk + (long)yy * vks;
-    const uint8_t* img = src + (long)n * Hs * Ws * C;
-    int acc[4] = {1 << (PIL_PRECISION_BITS - 1), 1 << (PIL_PRECISION_BITS - 1), 1 << (PIL_PRECISION_BITS - 1),
-                  1 << (PIL_PRECISION_BITS - 1)};
-    for (int y = 0; y < ycnt; ++y) {
-      const uint8_t* row = img + ((long)(ymin + y) * Ws + xmin) * C;
-      int h[4] = {1 << (PIL_PRECISION_BITS - 1), 1 << (PIL_PRECISION_BITS - 1), 1 << (PIL_PRECISION_BITS - 1),
-                  1 << (PIL_PRECISION_BITS - 1)};
-      for (int x = 0; x < xcnt; ++x) {
-        const int k = kx[x];
-        for (int c = 0; c < C; ++c) h[c] += (int)row[x * C + c] * k;
+  const uint8_t* img = src + n * Hs * Ws * C;
+  const int xs0 = hb[2 * tx0], xs1 = hb[2 * (tx0 + txv - 1)] + hb[2 * (tx0 + txv - 1) + 1];
+  const int ys0 = vb[2 * ty0], ys1 = vb[2 * (ty0 + tyv - 1)] + vb[2 * (ty0 + tyv - 1) + 1];
+  const int rw = (xs1 - xs0) * C, rh = ys1 - ys0;
+  if (rw > SRC_ROW_BYTES || rh > SRC_ROWS) {  // per-pixel path
+    for (int i = threadIdx.x; i < txv * tyv; i += PT) {
+      const int yy = ty0 + i / txv, xx = tx0 + i % txv;
+      const int xmin = hb[2 * xx], xcnt = hb[2 * xx + 1], ymin = vb[2 * yy], ycnt = vb[2 * yy + 1];
+      int acc[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = HALF;
+      for (int y = 0; y < ycnt; ++y) {
+        const uint8_t* row = img + ((long)(ymin + y) * Ws + xmin) * C;
+        int h[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) h[c] = HALF;
+        for (int x = 0; x < xcnt; ++x) {
+          const int k = hk[(long)xx * hks + x];
+#pragma unroll
+          for (int c = 0; c < C; ++c) h[c] += (int)row[x * C + c] * k;
+        }
+        const int k = vk[(long)yy * vks + y];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += clip8(h[c]) * k;
       }
-      const int k = ky[y];
-      for (int c = 0; c < C; ++c) acc[c] += clip8(h[c]) * k;
+      store_pixel<C>(out, n, (long)yy * Wo + xx, HWo, acc, mode);
     }
-    if (mode == 0) {
-      float* o = out + n * C * HWo + p;
-      for (int c = 0; c < C; ++c) o[c * HWo] = ((float)clip8(acc[c]) / 255.0f) * 255.0f;
+    return;
+  }
+  // 1. source window -> LDS: aligned dword loads covering each window row (the row start is at
+  //    any byte offset), bytes scattered into the LDS row
+  {
+    const long abs0 = (long)(img - (const uint8_t*)0);
+    const int lead = (int)((abs0 + ((long)ys0 * Ws + xs0) * C) & 3);  // same for every row iff Ws*C % 4 == 0
+    if (((Ws * C) & 3) == 0 && (abs0 & 3) == 0) {  // then no dword crosses a row end
+      const int words = (lead + rw + 3) >> 2;
+      for (int i = threadIdx.x; i < rh * words; i += PT) {
+        const int r = i / words, w = i - r * words;
+        const uint8_t* rowp = img + ((long)(ys0 + r) * Ws + xs0) * C - lead;
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(rowp + 4 * w);
+        uint8_t* d = s_src + r * SRC_ROW_BYTES;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int b = 4 * w + q - lead;
+          if (b >= 0 && b < rw) d[b] = (uint8_t)(v >> (8 * q));
+        }
+      }
     } else {
-      float* o = out + n * HWo + p;
-      if (clip8(acc[0]) != 0) *o = 0.f;
+      for (int i = threadIdx.x; i < rh * rw; i += PT) {
+        const int r = i / rw, b = i - r * rw;
+        s_src[r * SRC_ROW_BYTES + b] = img[((long)(ys0 + r) * Ws + xs0) * C + b];
+      }
     }
+  }
+  __syncthreads();
+  // 2. horizontal pass over every window row (Pillow's intermediate uint8 image)
+  for (int i = threadIdx.x; i < rh * txv; i += PT) {
+    const int r = i / txv, x = i - r * txv, xx = tx0 + x;
+    const int xmin = hb[2 * xx] - xs0, xcnt = hb[2 * xx + 1];
+    const uint8_t* row = s_src + r * SRC_ROW_BYTES + xmin * C;
+    const int* k = hk + (long)xx * hks;
+    int h[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) h[c] = HALF;
+    for (int j = 0; j < xcnt; ++j) {
+      const int kj = k[j];
+#pragma unroll
+      for (int c = 0; c < C; ++c) h[c] += (int)row[j * C + c] * kj;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) s_h[(r * TX + x) * C + c] = (uint8_t)clip8(h[c]);
+  }
+  __syncthreads();
+  // 3. vertical pass, coalesced planar stores
+  for (int i = threadIdx.x; i < tyv * txv; i += PT) {
+    const int y = i / txv, x = i - y * txv, yy = ty0 + y;
+    const int ymin = vb[2 * yy] - ys0, ycnt = vb[2 * yy + 1];
+    const int* k = vk + (long)yy * vks;
+    int acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = HALF;
+    for (int j = 0; j < ycnt; ++j) {
+      const int kj = k[j];
+      const uint8_t* hv = s_h + ((ymin + j) * TX + x) * C;
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += (int)hv[c] * kj;
+    }
+    store_pixel<C>(out, n, (long)yy * Wo + tx0 + x, HWo, acc, mode);
   }
 }
 
@@ -213,11 +302,24 @@ int vst_pil_resize_u8(const void* src, float* out, int N, int Hs, int Ws, int C,
                       const void* hk, int hks, const void* vbounds, const void* vk, int vks, int mode, void* stream) {
   VST_CHECK_ARG(src && out && hbounds && hk && vbounds && vk && N >= 0 && Hs > 0 && Ws > 0 && Ho > 0 && Wo > 0);
   VST_CHECK_ARG(C >= 1 && C <= 4 && hks > 0 && vks > 0 && (mode == 0 || (mode == 1 && C == 1)));
-  const long total = (long)N * Ho * Wo;
-  if (total == 0) return VST_OK;
-  pil_resize_kernel<<<grid_of(total), PT, 0, (hipStream_t)stream>>>((const uint8_t*)src, out, N, Hs, Ws, C, Ho, Wo,
-                                                                     (const int*)hbounds, (const int*)hk, hks,
-                                                                     (const int*)vbounds, (const int*)vk, vks, mode);
+  if ((long)N * Ho * Wo == 0) return VST_OK;
+  const int tiles_x = (Wo + TX - 1) / TX, tiles_y = (Ho + TY - 1) / TY;
+  const long blocks = (long)N * tiles_x * tiles_y;
+  VST_CHECK_ARG(blocks < (1L << 31));
+  const int* hbi = (const int*)hbounds;
+  const int* hki = (const int*)hk;
+  const int* vbi = (const int*)vbounds;
+  const int* vki = (const int*)vk;
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 3) {
+    pil_resize_kernel<3><<<(unsigned)blocks, PT, 0, st>>>((const uint8_t*)src, out, Hs, Ws, Ho, Wo, tiles_x, tiles_y,
+                                                          hbi, hki, hks, vbi, vki, vks, mode);
+  } else if (C == 1) {
+    pil_resize_kernel<1><<<(unsigned)blocks, PT, 0, st>>>((const uint8_t*)src, out, Hs, Ws, Ho, Wo, tiles_x, tiles_y,
+                                                          hbi, hki, hks, vbi, vki, vks, mode);
+  } else {
+    return VST_EUNSUPPORTED;
+  }
   return vst_launch_status();
 }
 
