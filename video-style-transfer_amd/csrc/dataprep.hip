@@ -63,14 +63,15 @@ constexpr int SRC_ROWS = 48, SRC_ROW_BYTES = 512;
 // row (monotone in the output coordinate); hk/vk: fixed-point taps, hks/vks per output coordinate.
 // mode 0: out = N x C x Ho x Wo fp32, (b / 255) * 255;
 // mode 1 (C == 1): out = N x Ho x Wo flow mask, multiplied by the motion mask (b == 0).
-template <int C>
+template <int C, int KX, int KY>
 __global__ __launch_bounds__(PT) void pil_resize_kernel(const uint8_t* __restrict__ src, float* __restrict__ out,
                                                         int Hs, int Ws, int Ho, int Wo, int tiles_x, int tiles_y,
                                                         const int* __restrict__ hb, const int* __restrict__ hk,
                                                         int hks, const int* __restrict__ vb,
                                                         const int* __restrict__ vk, int vks, int mode) {
-  __shared__ uint8_t s_src[SRC_ROWS * SRC_ROW_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t s_src[SRC_ROWS * SRC_ROW_BYTES];
   __shared__ uint8_t s_h[SRC_ROWS * TX * C];
+  static_assert(PT % TX == 0, "tile rows per pass");
   const int tiles = tiles_x * tiles_y;
   const long n = blockIdx.x / tiles;
   const int t = blockIdx.x - (int)n * tiles;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(PT) void pil_resize_kernel(const uint8_t* __restric
   const int xs0 = hb[2 * tx0], xs1 = hb[2 * (tx0 + txv - 1)] + hb[2 * (tx0 + txv - 1) + 1];
   const int ys0 = vb[2 * ty0], ys1 = vb[2 * (ty0 + tyv - 1)] + vb[2 * (ty0 + tyv - 1) + 1];
   const int rw = (xs1 - xs0) * C, rh = ys1 - ys0;
-  if (rw > SRC_ROW_BYTES || rh > SRC_ROWS) {  // per-pixel path
+  if (rw + 6 + KX * C > SRC_ROW_BYTES || rh + KY > SRC_ROWS) {  // per-pixel path (6: dword lead + tail)
     for (int i = threadIdx.x; i < txv * tyv; i += PT) {
       const int yy = ty0 + i / txv, xx = tx0 + i % txv;
       const int xmin = hb[2 * xx], xcnt = hb[2 * xx + 1], ymin = vb[2 * yy], ycnt = vb[2 * yy + 1];
@@ -107,22 +108,18 @@ __global__ __launch_bounds__(PT) void pil_resize_kernel(const uint8_t* __restric
     return;
   }
   // 1. source window -> LDS: aligned dword loads covering each window row (the row start is at
-  //    any byte offset), bytes scattered into the LDS row
+  //    any byte offset); the LDS row keeps that offset (lds_off) so the dwords land unchanged
+  int lds_off = 0;
   {
     const long abs0 = (long)(img - (const uint8_t*)0);
     const int lead = (int)((abs0 + ((long)ys0 * Ws + xs0) * C) & 3);  // same for every row iff Ws*C % 4 == 0
     if (((Ws * C) & 3) == 0 && (abs0 & 3) == 0) {  // then no dword crosses a row end
+      lds_off = lead;
       const int words = (lead + rw + 3) >> 2;
       for (int i = threadIdx.x; i < rh * words; i += PT) {
         const int r = i / words, w = i - r * words;
         const uint8_t* rowp = img + ((long)(ys0 + r) * Ws + xs0) * C - lead;
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(rowp + 4 * w);
-        uint8_t* d = s_src + r * SRC_ROW_BYTES;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int b = 4 * w + q - lead;
-          if (b >= 0 && b < rw) d[b] = (uint8_t)(v >> (8 * q));
-        }
+        reinterpret_cast<uint32_t*>(s_src + r * SRC_ROW_BYTES)[w] = reinterpret_cast<const uint32_t*>(rowp)[w];
       }
     } else {
       for (int i = threadIdx.x; i < rh * rw; i += PT) {
@@ -132,39 +129,50 @@ __global__ __launch_bounds__(PT) void pil_resize_kernel(const uint8_t* __restric
     }
   }
   __syncthreads();
-  // 2. horizontal pass over every window row (Pillow's intermediate uint8 image)
-  for (int i = threadIdx.x; i < rh * txv; i += PT) {
-    const int r = i / txv, x = i - r * txv, xx = tx0 + x;
-    const int xmin = hb[2 * xx] - xs0, xcnt = hb[2 * xx + 1];
-    const uint8_t* row = s_src + r * SRC_ROW_BYTES + xmin * C;
+  // 2. horizontal pass over every window row (Pillow's intermediate uint8 image).  With KX > 0
+  //    the tap loop has a fixed trip count: taps past a column's count are zero in the table and
+  //    read in-bounds LDS bytes (the fallback test keeps KX*C bytes of slack in each row).
+  const int x = threadIdx.x % TX;
+  if (x < txv) {
+    const int xx = tx0 + x;
+    const int xmin = hb[2 * xx] - xs0;
+    const int nx = KX > 0 ? KX : hb[2 * xx + 1];
     const int* k = hk + (long)xx * hks;
-    int h[C];
+    for (int r = threadIdx.x / TX; r < rh; r += PT / TX) {
+      const uint8_t* row = s_src + r * SRC_ROW_BYTES + lds_off + xmin * C;
+      int h[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) h[c] = HALF;
-    for (int j = 0; j < xcnt; ++j) {
-      const int kj = k[j];
+      for (int c = 0; c < C; ++c) h[c] = HALF;
+#pragma unroll 5
+      for (int j = 0; j < nx; ++j) {
+        const int kj = k[j];
 #pragma unroll
-      for (int c = 0; c < C; ++c) h[c] += (int)row[j * C + c] * kj;
+        for (int c = 0; c < C; ++c) h[c] += (int)row[j * C + c] * kj;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) s_h[(r * TX + x) * C + c] = (uint8_t)clip8(h[c]);
     }
-#pragma unroll
-    for (int c = 0; c < C; ++c) s_h[(r * TX + x) * C + c] = (uint8_t)clip8(h[c]);
   }
   __syncthreads();
   // 3. vertical pass, coalesced planar stores
-  for (int i = threadIdx.x; i < tyv * txv; i += PT) {
-    const int y = i / txv, x = i - y * txv, yy = ty0 + y;
-    const int ymin = vb[2 * yy] - ys0, ycnt = vb[2 * yy + 1];
-    const int* k = vk + (long)yy * vks;
-    int acc[C];
+  if (x < txv) {
+    for (int y = threadIdx.x / TX; y < tyv; y += PT / TX) {
+      const int yy = ty0 + y;
+      const int ymin = vb[2 * yy] - ys0;
+      const int ny = KY > 0 ? KY : vb[2 * yy + 1];
+      const int* k = vk + (long)yy * vks;
+      int acc[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc[c] = HALF;
-    for (int j = 0; j < ycnt; ++j) {
-      const int kj = k[j];
-      const uint8_t* hv = s_h + ((ymin + j) * TX + x) * C;
+      for (int c = 0; c < C; ++c) acc[c] = HALF;
+#pragma unroll 5
+      for (int j = 0; j < ny; ++j) {
+        const int kj = k[j];
+        const uint8_t* hv = s_h + ((ymin + j) * TX + x) * C;
 #pragma unroll
-      for (int c = 0; c < C; ++c) acc[c] += (int)hv[c] * kj;
+        for (int c = 0; c < C; ++c) acc[c] += (int)hv[c] * kj;
+      }
+      store_pixel<C>(out, n, (long)yy * Wo + tx0 + x, HWo, acc, mode);
     }
-    store_pixel<C>(out, n, (long)yy * Wo + tx0 + x, HWo, acc, mode);
   }
 }
 
@@ -311,12 +319,18 @@ int vst_pil_resize_u8(const void* src, float* out, int N, int Hs, int Ws, int C,
   const int* vbi = (const int*)vbounds;
   const int* vki = (const int*)vk;
   hipStream_t st = (hipStream_t)stream;
+#define VST_PIL_LAUNCH(CC, KXX, KYY)                                                                            \
+  pil_resize_kernel<CC, KXX, KYY><<<(unsigned)blocks, PT, 0, st>>>((const uint8_t*)src, out, Hs, Ws, Ho, Wo, tiles_x, \
+                                                                   tiles_y, hbi, hki, hks, vbi, vki, vks, mode)
+  const int kfix = (hks == 5 && vks == 5) ? 5 : ((hks == 3 && vks == 3) ? 3 : 0);
   if (C == 3) {
-    pil_resize_kernel<3><<<(unsigned)blocks, PT, 0, st>>>((const uint8_t*)src, out, Hs, Ws, Ho, Wo, tiles_x, tiles_y,
-                                                          hbi, hki, hks, vbi, vki, vks, mode);
+    if (kfix == 5) VST_PIL_LAUNCH(3, 5, 5);
+    else if (kfix == 3) VST_PIL_LAUNCH(3, 3, 3);
+    else VST_PIL_LAUNCH(3, 0, 0);
   } else if (C == 1) {
-    pil_resize_kernel<1><<<(unsigned)blocks, PT, 0, st>>>((const uint8_t*)src, out, Hs, Ws, Ho, Wo, tiles_x, tiles_y,
-                                                          hbi, hki, hks, vbi, vki, vks, mode);
+    if (kfix == 5) VST_PIL_LAUNCH(1, 5, 5);
+    else if (kfix == 3) VST_PIL_LAUNCH(1, 3, 3);
+    else VST_PIL_LAUNCH(1, 0, 0);
   } else {
     return VST_EUNSUPPORTED;
   }
