@@ -198,3 +198,41 @@ def test_dataset_items_match_reference(tmp_path, golden, case):
         assert torch.equal(b1[j], a1) and torch.equal(b2[j], a2)
         assert torch.equal(bf[j], af) and torch.equal(bm[j], am)
     assert len(loader) == (len(ds) + 1) // 2
+
+
+@pytest.mark.gpu
+def test_loader_feeds_training_step(tmp_path):
+    """End to end: on-disk FlyingThings3D tree -> FramePairLoader (GPU prep) -> ReCoNetTrainer
+    losses, against the oracle's items and the oracle's loss on them (1e-3 relative, the
+    north-star fp32 tolerance), then one full optimiser step runs."""
+    import oracle
+    from oracle import shapes
+    from vst.reconet import datasets as DS
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+    from vst.synthetic import style_image
+
+    root = str(tmp_path / "ft")
+    D.write_tree(root, "ft3d", 71, 36, 60, 1, 10)
+    ds = DS.FlyingThings3D(root, resolution=(64, 32), frame_num=1)
+    batch = next(iter(DS.FramePairLoader(ds, batch_size=2)))
+    P = oracle.seeded_params(shapes.reconet(), 5)
+    VP = oracle.seeded_params(shapes.vgg16(), 6)
+    model = N.ReCoNet()
+    model.load_state_dict(P)
+    vgg = N.Vgg16()
+    vgg.load_state_dict(VP)
+    style = style_image(8, 32, 64)
+    tr = ReCoNetTrainer(model.cuda(), vgg.cuda(), style.cuda())
+    img1, img2, flow, mask = batch
+    out = tr.losses(torch.stack([img1, img2]), flow, mask)
+    items = [_oracle_item(ds, j) for j in range(2)]
+    o1, o2, of, om = (torch.stack([it[k] for it in items]) for k in range(4))
+    assert torch.equal(img1.cpu(), o1) and torch.equal(img2.cpu(), o2)
+    assert (mask.cpu() != om).float().mean() <= 0.005
+    ref = R.reconet_losses(P, VP, o1, o2, of, om, R.style_grams(VP, style))
+    for k in ("loss", "CL", "SL", "FTL", "OTL", "RL"):
+        a, b = float(out[k].item()), float(ref[k])
+        assert abs(a - b) <= 1e-3 * abs(b) + 1e-6, (k, a, b)
+    res = tr.step(torch.stack([img1, img2]), flow, mask)
+    assert torch.isfinite(res["loss"]).item()
