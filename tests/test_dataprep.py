@@ -236,3 +236,21 @@ def test_loader_feeds_training_step(tmp_path):
         assert abs(a - b) <= 1e-3 * abs(b) + 1e-6, (k, a, b)
     res = tr.step(torch.stack([img1, img2]), flow, mask)
     assert torch.isfinite(res["loss"]).item()
+
+
+def test_loader_rank_sharding(tmp_path):
+    """FramePairLoader's DP sharding is host logic: disjoint, covering, seeded identically per rank."""
+    from vst.reconet import datasets as DS
+
+    root = str(tmp_path / "mk")
+    D.write_tree(root, "monkaa", 3, 8, 8, 3, 6)
+    ds = DS.Monkaa(root, resolution=(8, 8), frame_num=1)
+    seen = []
+    for r in range(3):
+        ld = DS.FramePairLoader(ds, batch_size=2, shuffle=True, seed=11, rank=r, world_size=3)
+        batches = list(ld._batches())
+        assert len(batches) == len(ld)
+        seen += [e[0][0] for b in batches for e in b]
+    assert sorted(seen) == sorted(f[0] for f in ds.frame)
+    with pytest.raises(Exception):
+        DS.FramePairLoader(ds, rank=3, world_size=3)

@@ -261,19 +261,34 @@ class FramePairLoader:
     yields device batches `(img1, img2, flow_into_past, mask)`; the host decode / PFM read of the
     next batch runs in a background thread while the current batch is on the GPU."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False, drop_last=False, seed=None, device=None):
+    def __init__(self, dataset, batch_size=1, shuffle=False, drop_last=False, seed=None, device=None, rank=None,
+                 world_size=None):
+        """rank / world_size (default: torch.distributed's when initialised): every rank draws the
+        same seeded permutation per epoch and takes its strided share of it (DistributedSampler
+        semantics without padding), so the ranks' frame pairs are disjoint -- the DP trainer's
+        sharding (vst.reconet.dist)."""
         self.dataset, self.batch_size, self.shuffle, self.drop_last = dataset, batch_size, shuffle, drop_last
-        self.rng = random.Random(seed)
+        dist = torch.distributed
+        on = dist.is_available() and dist.is_initialized()
+        self.rank = rank if rank is not None else (dist.get_rank() if on else 0)
+        self.world_size = world_size if world_size is not None else (dist.get_world_size() if on else 1)
+        if not 0 <= self.rank < self.world_size:
+            raise VstError(f"rank {self.rank} outside world_size {self.world_size}")
+        self.rng = random.Random(seed if seed is not None else 0 if self.world_size > 1 else None)
         self.device = device
 
-    def __len__(self):
-        n = len(self.dataset)
-        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
-
-    def _batches(self):
+    def _indices(self):
         order = list(range(len(self.dataset)))
         if self.shuffle:
             self.rng.shuffle(order)
+        return order[self.rank::self.world_size]
+
+    def __len__(self):
+        n = len(range(len(self.dataset))[self.rank::self.world_size])
+        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+
+    def _batches(self):
+        order = self._indices()
         for i in range(0, len(order), self.batch_size):
             idx = order[i:i + self.batch_size]
             if len(idx) < self.batch_size and self.drop_last:
