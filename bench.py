@@ -314,6 +314,7 @@ def run_dataprep(args, dev, rank, world):
     algo = 2 * B * (Hs * Ws * 3 + 3 * Ho * Wo * 4)  # uint8 HWC frames in, fp32 planes out
     if rank != 0:
         return None
+    traffic, traffic_src = pmc_traffic("dataprep", "pil_resize_kernel<3, 5, 5>")
     result = {
         "metric": "frame-pair items/sec, FlyingThings3D __getitem__ device half (960x540 -> 640x360)",
         "value": B * world * args.steps / elapsed, "unit": "items/s", "n_gpus": world, "steps": args.steps,
@@ -323,9 +324,10 @@ def run_dataprep(args, dev, rank, world):
         "config": {"workload": f"dataprep: B={B} items/GPU, frames+motion 960x540 uint8, PFM flows 960x540x3 "
                                f"-> img1/img2 3x360x640, flow 2x360x640, mask 360x640", "global_batch": B * world,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "pil_resize_kernel (frames, mode 0)", "achieved": algo / us / 1e3,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo / us / 1e3 / HBM_PEAK_GBS,
-                     "traffic": None, "algo_bytes_per_launch": algo, "avg_launch_us": us},
+        "roofline": {"bound": "hbm", "kernel": "pil_resize_kernel<3, 5, 5> (frames, mode 0)",
+                     "achieved": algo / us / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": algo / us / 1e3 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "algo_bytes_per_launch": algo, "avg_launch_us": us},
     }
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_dataprep(args)

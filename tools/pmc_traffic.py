@@ -26,15 +26,23 @@ def family(name):
     return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
 
 
+def instance(name):
+    """unqualified name with its template arguments, e.g. pil_resize_kernel<3, 5, 5>"""
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("::")[-1]
+
+
 def main():
     model = sys.argv[1] if len(sys.argv) > 1 else "reconet"
     F, W = load(model, "FETCH_SIZE"), load(model, "WRITE_SIZE")
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for d, r in F.items():
-        a = agg[family(r["Kernel_Name"])]
-        a[0] += 1
-        a[1] += float(r["Counter_Value"]) * 1024 * FETCH_CORRECTION
-        a[2] += float(W[d]["Counter_Value"]) * 1024 if d in W else 0.0
+        name = r["Kernel_Name"]
+        keys = {family(name), instance(name)}  # the family, and the template instance when there is one
+        for key in keys:
+            a = agg[key]
+            a[0] += 1
+            a[1] += float(r["Counter_Value"]) * 1024 * FETCH_CORRECTION
+            a[2] += float(W[d]["Counter_Value"]) * 1024 if d in W else 0.0
     fams = {k: {"launches": n, "read_bytes_per_launch": f / n, "write_bytes_per_launch": w / n,
                 "bytes_per_launch": (f + w) / n} for k, (n, f, w) in agg.items()}
     for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["bytes_per_launch"] * kv[1]["launches"])[:15]:
