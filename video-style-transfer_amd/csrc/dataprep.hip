@@ -51,13 +51,13 @@ __device__ __forceinline__ void store_pixel(float* __restrict__ out, long n, lon
   }
 }
 
-// Output tile of one workgroup: TX columns x TY rows of one image.  The source window it needs is
+// Output tile of one workgroup: TX columns x TY rows of one image (64x8 measured best of 64x{4,8,16,32}).  The source window it needs is
 // staged in LDS (coalesced byte rows), the horizontal pass writes its uint8 rows to LDS, the
 // vertical pass reads them: every source byte is read from HBM/L2 once per tile instead of once
 // per tap of every output pixel.  Windows larger than the LDS budget (strong downscales) take
 // the per-pixel path, block-uniformly.
-constexpr int TX = 64, TY = 16;
-constexpr int SRC_ROWS = 48, SRC_ROW_BYTES = 512;
+constexpr int TX = 64, TY = 8;
+constexpr int SRC_ROWS = 24, SRC_ROW_BYTES = 512;
 
 // src: N x Hs x Ws x C uint8 (PIL's interleaved raster); hb/vb: {min, count} per output column /
 // row (monotone in the output coordinate); hk/vk: fixed-point taps, hks/vks per output coordinate.
