@@ -272,7 +272,12 @@ def run_dataprep(args, dev, rank, world):
     rng = np.random.default_rng(shard_seed(1234, rank))
     frames = torch.from_numpy(rng.integers(0, 256, (2 * B, Hs, Ws, 3), dtype=np.uint8)).to(dev)
     motion = torch.from_numpy(np.where(rng.random((B, Hs, Ws)) < 0.05, 255, 0).astype(np.uint8)).to(dev)
-    flows = torch.from_numpy(rng.uniform(-20, 20, (2 * B, Hs, Ws, 3)).astype("<f4").view(np.int32)).to(dev)
+    # SURVEY.md §8(d) synthetic flow: a 2x(H/16)x(W/16) U(-8, 8) px field bilinearly upsampled
+    # (PFM layout: H x W x 3, third channel zero, rows bottom-up -- the flip is irrelevant to the data)
+    coarse = torch.from_numpy(rng.uniform(-8, 8, (2 * B, 2, Hs // 16, Ws // 16)).astype(np.float32))
+    fine = torch.nn.functional.interpolate(coarse, size=(Hs, Ws), mode="bilinear", align_corners=False)
+    raw = torch.cat([fine, torch.zeros(2 * B, 1, Hs, Ws)], dim=1).permute(0, 2, 3, 1).contiguous().numpy()
+    flows = torch.from_numpy(raw.astype("<f4").view(np.int32)).to(dev)
     img = torch.empty((2 * B, 3, Ho, Wo), device=dev)
     fl = torch.empty((2 * B, 2, Ho, Wo), device=dev)
 
@@ -320,7 +325,8 @@ def run_dataprep(args, dev, rank, world):
         "value": B * world * args.steps / elapsed, "unit": "items/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32",
-        "data": "synthetic (numpy PCG64 uint8 frames, 5% motion-boundary pixels, U(-20,20) flows)",
+        "data": "synthetic (numpy PCG64 uint8 frames, 5% motion-boundary pixels, smooth flows: "
+                "U(-8,8) px at 1/16 resolution, bilinearly upsampled, SURVEY.md §8(d))",
         "config": {"workload": f"dataprep: B={B} items/GPU, frames+motion 960x540 uint8, PFM flows 960x540x3 "
                                f"-> img1/img2 3x360x640, flow 2x360x640, mask 360x640", "global_batch": B * world,
                    "parallelism": f"dp{world}"},
