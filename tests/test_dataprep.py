@@ -254,3 +254,21 @@ def test_loader_rank_sharding(tmp_path):
     assert sorted(seen) == sorted(f[0] for f in ds.frame)
     with pytest.raises(Exception):
         DS.FramePairLoader(ds, rank=3, world_size=3)
+
+
+def test_combined_dataset_indexing(tmp_path):
+    """FlyingThings3D_Monkaa (RC/datasets.py:256-281): Monkaa items first, then FlyingThings3D;
+    both path forms (root string, [monkaa, flyingthings3d] list)."""
+    from vst.reconet import datasets as DS
+
+    D.write_tree(str(tmp_path / "monkaa"), "monkaa", 1, 8, 8, 2, 4)
+    D.write_tree(str(tmp_path / "flyingthings3d"), "ft3d", 2, 8, 8, 1, 10)
+    for path in (str(tmp_path), [str(tmp_path / "monkaa"), str(tmp_path / "flyingthings3d")]):
+        ds = DS.FlyingThings3D_Monkaa(path, resolution=(8, 8), frame_num=1)
+        nm, nf = len(ds.monkaa), len(ds.flyingthings3d)
+        assert (nm, nf) == (2 * 3, 3 * 9) and len(ds) == nm + nf
+        assert ds.entries(0) == ds.monkaa.entries(0)
+        assert ds.entries(nm) == ds.flyingthings3d.entries(0)
+        assert ds.entries(len(ds) - 1) == ds.flyingthings3d.entries(nf - 1)
+    with pytest.raises(ValueError):
+        DS.FlyingThings3D_Monkaa(3)
