@@ -591,6 +591,15 @@ def gen_dataprep():
             out[f"{tag}_{i}_img2"] = _np(img2)
             out[f"{tag}_{i}_flow"] = _np(flow)
             out[f"{tag}_{i}_mask"] = _np(mask)
+    # Coco2014: PNG images of assorted sizes (down- and upscaled to 64x48), the reference's own class
+    root = os.path.join("/tmp", "vst_gen_dp", "coco")
+    shutil.rmtree(root, ignore_errors=True)
+    D.write_coco(root, 63)
+    coco = ds_mod.Coco2014(root, resolution=(64, 48))
+    out["coco_len"] = np.array(len(coco))
+    for i in range(len(coco)):
+        out[f"coco_{i}_key"] = np.array(os.path.relpath(coco.paths[i], root))
+        out[f"coco_{i}"] = _np(coco[i])
     np.savez_compressed(os.path.join(HERE, "dp_items.npz"), **out)
     print("dataprep fixtures written")
 

@@ -272,3 +272,39 @@ def test_combined_dataset_indexing(tmp_path):
         assert ds.entries(len(ds) - 1) == ds.flyingthings3d.entries(nf - 1)
     with pytest.raises(ValueError):
         DS.FlyingThings3D_Monkaa(3)
+
+
+def _coco(tmp_path, golden):
+    import os
+
+    from vst.reconet import datasets as DS
+
+    g = golden("dp_items")
+    root = str(tmp_path / "coco")
+    D.write_coco(root, 63)
+    ds = DS.Coco2014(root, resolution=(64, 48))
+    assert len(ds) == int(g["coco_len"])
+    for i in range(len(ds)):
+        assert os.path.relpath(ds.paths[i], root) == str(g[f"coco_{i}_key"])  # sorted, like list_files
+    return g, ds
+
+
+def test_coco_oracle_matches_reference(tmp_path, golden):
+    """Coco2014.__getitem__ (RC/datasets.py:35-38) restated: Pillow resample + toTensor255."""
+    g, ds = _coco(tmp_path, golden)
+    for i, p in enumerate(ds.paths):
+        a = np.asarray(Image.open(p).convert("RGB"))
+        got = D.to_tensor255(D.pil_resize_bilinear(a, ds.resolution)).numpy()
+        np.testing.assert_array_equal(got, g[f"coco_{i}"])
+
+
+@pytest.mark.gpu
+def test_coco_items_match_reference(tmp_path, golden):
+    from vst.reconet import datasets as DS
+
+    g, ds = _coco(tmp_path, golden)
+    for i in range(len(ds)):
+        np.testing.assert_array_equal(ds[i].cpu().numpy(), g[f"coco_{i}"])
+    batch = DS.load_images(ds.paths, ds.resolution).cpu().numpy()  # mixed sizes, grouped launches
+    for i in range(len(ds)):
+        np.testing.assert_array_equal(batch[i], g[f"coco_{i}"])

@@ -183,6 +183,45 @@ class FlyingThings3D_Monkaa(torch.utils.data.Dataset):  # noqa: N801 (reference 
         return self.flyingthings3d[idx - len(self.monkaa)]
 
 
+class Coco2014(torch.utils.data.Dataset):
+    """RC/datasets.py:16-38: every file of <path>/train2014 (sorted), `Image.open(..).convert("RGB")
+    .resize(resolution, Image.BILINEAR)` then toTensor255 -- the resize and conversion on the GPU
+    (bit-exact with Pillow).  Items are (3, H, W) device tensors; `load_images` batches them."""
+
+    def __init__(self, path: str, resolution: tuple = (256, 256), device=None):
+        self.path = os.path.join(path, "train2014")
+        self.resolution = resolution
+        self.device = torch.device(device) if device is not None else None
+        self.paths = list(list_files(self.path))
+        self.length = len(self.paths)
+
+    def __len__(self):
+        return self.length
+
+    def __getitem__(self, idx):
+        return load_images([self.paths[idx]], self.resolution, self.device)[0]
+
+
+def load_images(paths, resolution, device=None):
+    """(len(paths), 3, H, W) fp32 = toTensor255(Image.open(p).convert("RGB").resize(resolution,
+    BILINEAR)) per path; images sharing a source size go through one kernel launch."""
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    Wo, Ho = resolution
+    out = torch.empty((len(paths), 3, Ho, Wo), dtype=torch.float32, device=dev)
+    groups = {}
+    for i, p in enumerate(paths):
+        a = _decode(p, "RGB")
+        groups.setdefault(a.shape, []).append((i, a))
+    for shape, items in groups.items():
+        host = torch.empty((len(items),) + shape, dtype=torch.uint8).pin_memory()
+        for j, (_, a) in enumerate(items):
+            host[j].numpy()[...] = a
+        imgs = ops.pil_resize_to_tensor255(host.to(dev, non_blocking=True), resolution)
+        idx = torch.tensor([i for i, _ in items], device=dev)
+        out.index_copy_(0, idx, imgs)
+    return out
+
+
 # ------------------------------------------------------------------------------- batch assembly
 def _decode(path, mode):
     img = Image.open(path)
