@@ -3,16 +3,25 @@
 Workload (one "step"): the reference `train_candy` loop body (RC/train_single/train_candy.py:77-152)
 on one batch of B synthetic frame pairs per GPU, 3x256x512, precomputed flow + occlusion mask,
 full loss (FTL + OTL + content + Gram style + TV) through the Vgg16 loss network, backward and
-Adam — config 3 of BASELINE.json (`--config 2` drops the temporal terms).  Random-init weights
+Adam — config 3 of BASELINE.json.  `--config 2` runs the reference's no-temporal script
+(train_coco2014.py: content + Gram style on the 2B single frames of B pairs).  Random-init weights
 (no checkpoint download offline), synthetic data already resident in HBM.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL all-reduce)
 
-Prints ONE JSON line (rank 0).  `roofline` = the dominant kernel family (conv_gemm_kernel: conv
-forward + data-gradient implicit GEMM on fp32 MFMA), algorithmic FLOPs / HIP-event-timed launch
-time inside the timed region vs the 157.3 TFLOP/s fp32 MFMA peak.  `cpu_baseline` = the oracle
-(CPU restatement of the same step, oracle/reconet_ref.py) on a bounded sample, rank 0 at N=1.
+GEMM arithmetic (`--gemm`, vst.ops.POLICIES): the headline runs `bf16x6` -- every conv / Gram
+product on three-way split bf16 MFMAs, per-product error ~2^-24 (fp32-class; the reference's
+golden steps pass at the f32 bar under it, tests/test_gpu_parity.py) at 2500/6 = 417 TFLOP/s
+peak; `f32` is exact fp32 MFMA (157.3 TFLOP/s).
+
+Prints ONE JSON line (rank 0).  `value` comes from K uninstrumented steps.  `roofline` = the
+dominant kernel family (conv_gemm_kernel: conv forward + data-gradient implicit GEMM),
+algorithmic FLOPs / HIP-event-timed launch time over a second, instrumented run of the same step
+(events on the launching stream around every launch) vs the peak of the arithmetic launched.
+`cpu_baseline` = the oracle (CPU restatement of the same step, oracle/reconet_ref.py) on a bounded
+sample, rank 0 at N=1; `full_size_parity` = the HIP step vs that oracle step on the same B=1
+full-size pair (loss terms and gradients).
 """
 import argparse
 import json
@@ -34,8 +43,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=150)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--prof-steps", type=int, default=10, help="instrumented steps for the roofline line")
     ap.add_argument("--model", default="reconet", choices=("reconet", "adaattn", "reconet_infer", "dataprep"),
                     help="reconet: BASELINE configs 2/3 (the metric); adaattn: config 4's train_video step")
     ap.add_argument("--batch", type=int, default=None, help="frame pairs per GPU (default 8 reconet, 4 adaattn)")
@@ -44,46 +54,92 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=(2, 3))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vgg19", action="store_true", help="skip the VGG19 fwd+dgrad north-star sub-benchmark")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=2)
-    ap.add_argument("--gemm", default=os.environ.get("VST_GEMM_POLICY", "parity"),
-                    choices=("parity", "bf16x6", "bf16x3", "f32", "bf16"),
-                    help="GEMM arithmetic policy (vst.ops.POLICIES): parity = bf16x3 split MFMA except the "
-                         "stylizer forwards (fp32 MFMA); bf16x3 / f32 everywhere; bf16 = reduced precision")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads (default: os.cpu_count(), capped by OMP_NUM_THREADS = the box's CPU share)")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed oracle steps (median)")
+    ap.add_argument("--cpu-warmup", type=int, default=2)
+    ap.add_argument("--gemm", default=os.environ.get("VST_GEMM_POLICY"),
+                    choices=("bf16x6", "f32", "parity", "bf16x3", "bf16"),
+                    help="GEMM arithmetic policy (vst.ops.POLICIES); default bf16x6 (fp32-class split products), "
+                         "bf16 for the config-5 AdaAttN shape (BASELINE's half-precision path)")
     return ap.parse_args()
 
 
+def cpu_threads(args):
+    """Threads for the oracle: os.cpu_count(), capped by OMP_NUM_THREADS when set (the GPU box
+    exports the CPU share of one GPU there; os.cpu_count() reports the whole machine)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
+
+
+# oracle / reference time ratio measured in the build container (tools/ref_ratio.py, same step,
+# same host, same threads): relates the on-box oracle number to the reference itself
+RATIO_FILE = os.path.join(REPO, "profiles", "r02_oracle_ref_ratio.json")
+
+
+def oracle_ref_ratio(kind):
+    if not os.path.exists(RATIO_FILE):
+        return None
+    return json.load(open(RATIO_FILE)).get(kind)
+
+
+def _median_rate(one, warmup, steps):
+    for _ in range(warmup):
+        one()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        one()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts
+
+
 def cpu_baseline(args):
-    """Oracle (CPU restatement of the reference step) on a bounded sample: B=1 pair at full size."""
+    """Oracle (CPU restatement of the reference step) on a bounded sample: B=1 pair at full size,
+    `cpu_warmup` + `cpu_steps` steps, median.  Also returns the first step's loss terms and
+    gradients (before its Adam update) for the full-size parity check."""
     import oracle
     from oracle import reconet_ref as R
     from oracle import shapes
     from vst.synthetic import frame_pair_batch, style_image
 
-    torch.set_num_threads(args.cpu_threads)
+    nt = cpu_threads(args)
+    torch.set_num_threads(nt)
     H, W = args.height, args.width
     P = oracle.seeded_params(shapes.reconet(), 1, requires_grad=True)
     VP = oracle.seeded_params(shapes.vgg16(), 2)
     grams = R.style_grams(VP, style_image(3, H, W))
     img1, img2, flow, mask = frame_pair_batch(1234, 1, H, W, mask_fn=R.flow_warp_mask)
     state = {}
+    first = {"P0": {k: p.detach().clone() for k, p in P.items()}, "VP": VP,
+             "inputs": (img1, img2, flow, mask, style_image(3, H, W))}
+    w = dict(R.LOSS_WEIGHTS, BETA=1e10) if args.config == 2 else R.LOSS_WEIGHTS
 
     def one():
-        L = R.reconet_losses(P, VP, img1.clone(), img2.clone(), flow, mask, grams, temporal=args.config == 3)
+        if args.config == 2:  # train_coco2014 on the pair's 2 frames as single images
+            L = R.reconet_single_losses(P, VP, torch.cat([img1, img2]), grams, w)
+        else:
+            L = R.reconet_losses(P, VP, img1.clone(), img2.clone(), flow, mask, grams)
         for p in P.values():
             p.grad = None
         L["loss"].backward()
+        if "terms" not in first:
+            first.update(terms={k: float(v) for k, v in L.items()}, grads={k: p.grad.clone() for k, p in P.items()})
         with torch.no_grad():
             R.adam_step({k: p for k, p in P.items()}, {k: p.grad for k, p in P.items()}, state)
 
-    one()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        one()
-    dt = (time.perf_counter() - t0) / args.cpu_steps
-    return {"value": 1.0 / dt, "unit": "frame-pairs/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of B=1 synthetic 3x{H}x{W} frame pair, "
-                      f"config {args.config}, oracle/reconet_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
+    med, ts = _median_rate(one, args.cpu_warmup, args.cpu_steps)
+    res = {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": nt, "kind": "port",
+           "os_cpu_count": os.cpu_count(),
+           "sample": f"median of {args.cpu_steps} timed steps (+{args.cpu_warmup} warm-up) of a B=1 synthetic "
+                     f"3x{H}x{W} frame pair, config {args.config}, oracle/reconet_ref.py on torch-CPU fp32, "
+                     f"{nt} threads", "step_s": ts,
+           "oracle_to_reference_time_ratio": oracle_ref_ratio("reconet")}
+    return res, first
 
 
 def cpu_baseline_adaattn(args):
@@ -93,7 +149,8 @@ def cpu_baseline_adaattn(args):
     from oracle import shapes
     from vst.synthetic import content_style_batch
 
-    torch.set_num_threads(args.cpu_threads)
+    nt = cpu_threads(args)
+    torch.set_num_threads(nt)
     H, W = args.height, args.width
     P = oracle.seeded_params(shapes.stylizing_network(), 1, requires_grad=True)
     VP = oracle.seeded_params(shapes.vgg19(), 2)
@@ -110,14 +167,12 @@ def cpu_baseline_adaattn(args):
         with torch.no_grad():
             R.adam_step(P, {k: p.grad for k, p in P.items()}, state, lr=1e-4)
 
-    steps = max(1, args.cpu_steps // 2)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one()
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": 1.0 / dt, "unit": "frame-pairs/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"{steps} timed step(s) (no warm-up) of B=1 synthetic 3x{H}x{W} (content1, content2, style) "
-                      f"triple, oracle/adaattn_ref.py on torch-CPU fp32, {args.cpu_threads} threads"}
+    steps, warm = max(1, args.cpu_steps // 2), 1
+    med, ts = _median_rate(one, warm, steps)
+    return {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": nt, "kind": "port", "os_cpu_count": os.cpu_count(),
+            "sample": f"median of {steps} timed step(s) (+{warm} warm-up) of a B=1 synthetic 3x{H}x{W} (content1, "
+                      f"content2, style) triple, oracle/adaattn_ref.py on torch-CPU fp32, {nt} threads",
+            "step_s": ts, "oracle_to_reference_time_ratio": oracle_ref_ratio("adaattn")}
 
 
 def pmc_traffic(model, family="conv_gemm_kernel"):
@@ -189,7 +244,8 @@ def build_reconet(args, dev, rank):
     vgg = N.Vgg16().to(dev)
     B, H, W = args.batch, args.height, args.width
     style = style_image(7, H, W).to(dev)
-    trainer = ReCoNetTrainer(model, vgg, style, temporal=args.config == 3)
+    script = "train_coco2014" if args.config == 2 else "train_candy"
+    trainer = ReCoNetTrainer.for_script(script, model, vgg, style)
 
     def hip_mask(f01, f10):
         return ops.flow_warp_mask(f01.to(dev), f10.to(dev))
@@ -197,7 +253,46 @@ def build_reconet(args, dev, rank):
     img1, img2, flow, mask = frame_pair_batch(shard_seed(1234, rank), B, H, W, mask_fn=hip_mask, device=dev)
     frames = torch.stack([img1, img2]).contiguous()
     del img1, img2
+    if trainer.single:  # config 2: the 2B frames of the B pairs as single images
+        frames = frames.reshape(2 * B, 3, H, W)
+        return lambda: trainer.step(frames)
     return lambda: trainer.step(frames, flow, mask)
+
+
+def full_size_parity(args, dev, first):
+    """The HIP step (current GEMM policy) vs the oracle step on the SAME B=1 full-size frame pair
+    and initial weights (cpu_baseline's first step, before its Adam update): relative error of
+    every loss term, of the flattened gradient, and the worst per-tensor gradient-norm error."""
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+
+    img1, img2, flow, mask, style = first["inputs"]
+    model = N.ReCoNet()
+    model.load_state_dict(first["P0"])
+    vgg = N.Vgg16()
+    vgg.load_state_dict(first["VP"])
+    script = "train_coco2014" if args.config == 2 else "train_candy"
+    tr = ReCoNetTrainer.for_script(script, model.to(dev), vgg.to(dev), style.to(dev))
+    if tr.single:
+        out = tr.losses(torch.cat([img1, img2]).to(dev))
+    else:
+        out = tr.losses(torch.stack([img1, img2]).to(dev), flow.to(dev), mask.to(dev))
+    tr.flat.zero_grad()
+    out["loss"].backward()
+    torch.cuda.synchronize()
+    ref = first["terms"]
+    terms = {k: abs(float(out[k]) - ref[k]) / abs(ref[k]) for k in ref}
+    g = {n: p.grad.detach().double().cpu().reshape(-1) for n, p in model.named_parameters()}
+    gr = {n: first["grads"][n].double().reshape(-1) for n in g}
+    flat = float(torch.cat([g[n] - gr[n] for n in g]).norm() / torch.cat(list(gr.values())).norm())
+    gmax = max(float(v.norm()) for v in gr.values())
+    worst = max((abs(float(g[n].norm()) - float(gr[n].norm())) / (float(gr[n].norm()) + 1e-4 * gmax / 1e-3), n)
+                for n in g)
+    tol = 1e-3
+    return {"workload": f"B=1 3x{args.height}x{args.width} frame pair, config {args.config}, same seeded weights/inputs",
+            "tolerance": tol, "loss_rel_err": terms, "grad_rel_err_flat": flat,
+            "grad_norm_rel_err_worst": {"tensor": worst[1], "err": worst[0]},
+            "pass": bool(max(terms.values()) < tol and flat < tol)}
 
 
 def build_adaattn(args, dev, rank):
@@ -246,16 +341,17 @@ def cpu_baseline_infer(args):
     from oracle import shapes
     from vst.synthetic import video_frames
 
-    torch.set_num_threads(args.cpu_threads)
+    nt = cpu_threads(args)
+    torch.set_num_threads(nt)
     P = oracle.seeded_params(shapes.reconet(), 1)
     frames = video_frames(5, 1 + args.cpu_steps, args.height, args.width)
     R.inference(R.reconet_forward, P, frames[:1], 1)  # warm-up
     t0 = time.perf_counter()
     R.inference(R.reconet_forward, P, frames[1:], 1)
     dt = (time.perf_counter() - t0) / args.cpu_steps
-    return {"value": 1.0 / dt, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
+    return {"value": 1.0 / dt, "unit": "frames/s", "cores": nt, "kind": "port",
             "sample": f"{args.cpu_steps} frames (+1 warm-up) of synthetic 3x{args.height}x{args.width} video, "
-                      f"oracle/reconet_ref.py inference on torch-CPU fp32, {args.cpu_threads} threads"}
+                      f"oracle/reconet_ref.py inference on torch-CPU fp32, {nt} threads"}
 
 
 def run_dataprep(args, dev, rank, world):
@@ -348,7 +444,8 @@ def cpu_baseline_dataprep(args):
     from oracle import dataprep_ref as D
     from oracle import reconet_ref as R
 
-    torch.set_num_threads(args.cpu_threads)
+    nt = cpu_threads(args)
+    torch.set_num_threads(nt)
     rng = np.random.default_rng(7)
     n = max(args.cpu_steps, 2)
     items = [([rng.integers(0, 256, (540, 960, 3), dtype=np.uint8) for _ in range(2)],
@@ -360,9 +457,44 @@ def cpu_baseline_dataprep(args):
     for it in items[1:]:
         D.getitem(*it, (640, 360), R.flow_warp_mask)
     dt = (time.perf_counter() - t0) / n
-    return {"value": 1.0 / dt, "unit": "items/s", "cores": args.cpu_threads, "kind": "port",
+    return {"value": 1.0 / dt, "unit": "items/s", "cores": nt, "kind": "port",
             "sample": f"{n} items (+1 warm-up), decoded inputs, oracle/dataprep_ref.getitem (numpy Pillow "
-                      f"restatement + torch-CPU bilinear + oracle flow_warp_mask), {args.cpu_threads} threads"}
+                      f"restatement + torch-CPU bilinear + oracle flow_warp_mask), {nt} threads"}
+
+
+def default_policy(args):
+    if args.gemm:
+        return args.gemm
+    if args.model == "adaattn" and (args.height, args.width) == (512, 1024):
+        return "bf16"  # config 5: BASELINE's reduced-precision MFMA path
+    return "bf16x6"
+
+
+def arithmetic_label(ops, ks):
+    """dtype string: fp32 operands/accumulation + the product arithmetic actually launched."""
+    names = sorted({ops.gemm_mode_name(m) for m in ks["by_mode"]}) or ops.policy_modes()
+    desc = {"f32": "f32 MFMA", "bf16x6": "bf16x6 split MFMA (~2^-24/product)", "bf16x3": "bf16x3 split MFMA (~2^-16)",
+            "bf16": "bf16 MFMA (~2^-8)"}
+    base = "bf16" if names == ["bf16"] else "f32"
+    return f"{base} ({' + '.join(desc[n] for n in names)})"
+
+
+def timed(step, steps, world, dev):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), out
 
 
 def main():
@@ -384,31 +516,21 @@ def main():
 
     if args.model == "dataprep":
         return run_dataprep(args, dev, rank, world)
+    args.gemm = default_policy(args)
     ops.use_policy(args.gemm)
-    torch.manual_seed(0)  # identical random-init replicas on every rank
+    torch.manual_seed(0)  # identical random-init replicas on every rank (the trainers also broadcast rank 0's)
     B, H, W = args.batch, args.height, args.width
     step = {"reconet": build_reconet, "adaattn": build_adaattn, "reconet_infer": build_reconet_infer}[args.model](
         args, dev, rank)
 
     for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+        step()
+    # headline: K uninstrumented steps
+    elapsed, out = timed(step, args.steps, world, dev)
+    # roofline: a second run of the same step with HIP events around every conv_gemm launch
     timer = kprof.KernelTimer()
-    t0 = time.perf_counter()
     with timer:
-        for _ in range(args.steps):
-            out = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+        prof_elapsed, _ = timed(step, args.prof_steps, world, dev)
     ks = timer.summary()
     loss = float(out["loss"].item()) if "loss" in out else None
 
@@ -419,8 +541,8 @@ def main():
         traffic, traffic_src = pmc_traffic(args.model)
         if args.model == "reconet":
             metric = "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs"
-            workload = (f"config{args.config}: ReCoNet train_candy step (Vgg16 loss net), B={B} frame pairs/GPU, "
-                        f"3x{H}x{W}, {'full loss incl. FTL/OTL warp' if args.config == 3 else 'content+style+TV'}")
+            workload = (f"config{args.config}: ReCoNet {'train_candy step, full loss incl. FTL/OTL warp' if args.config == 3 else 'train_coco2014 step (content + Gram style, no temporal) on the 2B frames'}"
+                        f" (Vgg16 loss net), B={B} frame pairs/GPU, 3x{H}x{W}")
             data = "synthetic (numpy PCG64 frames U[0,255), smooth flow, flow_warp_mask x Bernoulli(0.9)); random-init weights"
         elif args.model == "reconet_infer":
             metric = f"inference frames/sec at {H}\u00d7{W}, ReCoNet (Inference.__iter__ per-frame chain)"
@@ -444,7 +566,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.gemm == "bf16" else "f32",
+            "dtype": arithmetic_label(ops, ks),
             "gemm_policy": {"name": args.gemm, "base": ops.POLICIES[args.gemm][0],
                             "overrides": ops.POLICIES[args.gemm][1]},
             "data": data,
@@ -455,23 +577,35 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (conv fwd + dgrad implicit GEMM, all tile variants)",
                          "achieved": achieved, "peak": ks["peak_tflops"], "unit": "TFLOP/s",
                          "frac": achieved / ks["peak_tflops"], "traffic": traffic,
-                         "peak_note": "algorithmic fp32-operand TFLOP/s; peak = the launches' mix of MFMA peaks "
-                                      "(f32 157.3, bf16x6 2500/6, bf16x3 2500/3, bf16 2500), flops / sum(flops_i / peak_i)",
+                         "peak_note": "algorithmic fp32-operand TFLOP/s vs the MFMA peak of the arithmetic launched "
+                                      "(f32 157.3, bf16x6 2500/6, bf16x3 2500/3, bf16 2500; a mix: flops / "
+                                      "sum(flops_i / peak_i))",
                          "frac_of_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "by_mode": {ops.gemm_mode_name(m): v for m, v in ks["by_mode"].items()},
                          "traffic_source": traffic_src,
                          "algo_bytes_per_launch": ks["bytes"] / max(ks["launches"], 1),
                          "launches": ks["launches"], "avg_launch_us": ks["avg_us"],
                          "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
-                         "share_of_step": ks["total_ms"] / (1e3 * elapsed)},
+                         "measured_over": f"{args.prof_steps} instrumented steps after the timed region "
+                                          f"({1e3 * prof_elapsed / args.prof_steps:.2f} ms/step instrumented)",
+                         "share_of_step": ks["total_ms"] / (1e3 * prof_elapsed)},
         }
+        wg = timer.summary("wgrad")
+        if wg["launches"]:
+            result["roofline"]["wgrad_kernel"] = {"achieved": wg["tflops"], "peak": wg["peak_tflops"],
+                                                  "frac": wg["tflops"] / wg["peak_tflops"],
+                                                  "share_of_step": wg["total_ms"] / (1e3 * prof_elapsed)}
         if args.model == "reconet_infer":
             del result["frames_per_s"]
         if world == 1 and not args.no_vgg19 and args.model != "reconet_infer":
             result["north_star_vgg19"] = vgg19_subbench(dev)
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = {"reconet": cpu_baseline, "adaattn": cpu_baseline_adaattn,
-                                      "reconet_infer": cpu_baseline_infer}[args.model](args)
+            if args.model == "reconet":
+                result["cpu_baseline"], first = cpu_baseline(args)
+                result["full_size_parity"] = full_size_parity(args, dev, first)
+            else:
+                result["cpu_baseline"] = {"adaattn": cpu_baseline_adaattn, "reconet_infer": cpu_baseline_infer}[
+                    args.model](args)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

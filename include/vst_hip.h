@@ -28,20 +28,28 @@ extern "C" {
 /* ---- library ------------------------------------------------------------------------------ */
 int vst_version(void);
 const char* vst_strerror(int code);
-/* GEMM arithmetic of every conv / Gram / attention product (library-global; packed weight
- * operands are written in the layout of the mode current at pack time):
- *   0  exact fp32 MFMA (v_mfma_f32_32x32x2_f32);
- *   1  bf16x3 (default): fp32 operands split into hi + lo bf16, hi*hi + hi*lo + lo*hi on
- *      v_mfma_f32_32x32x16_bf16 with fp32 accumulation (per-product error <= ~2^-16 relative);
- *   2  bf16: hi*hi only (reduced precision, BASELINE config 5's half-precision MFMA path);
- *   3  bf16x6: three-way hi + mid + lo split, six products (fp32-level error, <= ~2^-24); its
- *      packed operands are 1.5x the fp32 size (Kpad*Mpad*3/2 floats); the weight-gradient /
- *      Gram / A*B^T kernels (no packed operand) run bf16x3 under it.
- * The initial mode comes from the environment variable VST_GEMM_MODE (f32 | bf16x3 | bf16 | bf16x6). */
-int vst_set_gemm_mode(int mode);
-int vst_get_gemm_mode(void);
+/* Build provenance: "<fnv1a-64 hex of csrc/* and include/vst_hip.h at build time>" (the Python
+ * loader and the GPU tests compare it with the tree they run from). */
+const char* vst_build_id(void);
 
-/* ---- convolution (implicit GEMM on MFMA, arithmetic per vst_set_gemm_mode) ----------------
+/* GEMM arithmetic: a per-call argument `mode` of every conv / Gram / attention GEMM entry and of
+ * every entry that writes a packed A operand.  The library holds no mode state: calls with
+ * different modes may run concurrently on different streams / threads.  A packed operand is only
+ * valid for GEMM calls with the mode it was packed with.
+ *   VST_GEMM_F32     exact fp32 MFMA (v_mfma_f32_32x32x2_f32), products exact, fp32 accumulate;
+ *   VST_GEMM_BF16X3  fp32 operands split into hi + lo bf16, hi*hi + hi*lo + lo*hi on
+ *                    v_mfma_f32_32x32x16_bf16 with fp32 accumulation (per-product error ~2^-16);
+ *   VST_GEMM_BF16    hi*hi only (reduced precision, BASELINE config 5's half-precision MFMA path);
+ *   VST_GEMM_BF16X6  three-way hi + mid + lo split, the six products of order >= 2^-16 (per-product
+ *                    error ~2^-24, fp32-class); packed operands are 1.5x the fp32 size
+ *                    (Kpad*Mpad*3/2 floats).
+ * An unknown mode returns VST_EINVAL (-1). */
+#define VST_GEMM_F32 0
+#define VST_GEMM_BF16X3 1
+#define VST_GEMM_BF16 2
+#define VST_GEMM_BF16X6 3
+
+/* ---- convolution (implicit GEMM on MFMA, arithmetic per the `mode` argument) ---------------
  * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv
  * (RC/network.py:114-120), torchvision VGG Conv2d(3x3, pad 1) + ReLU (RC/network.py:12-24),
  * and their autograd backward (dgrad / wgrad), the conv1 bias add and ConvTanh's
@@ -53,7 +61,7 @@ int vst_get_gemm_mode(void);
  */
 int vst_conv_pack_dims(int M, int K, int* Mpad, int* Kpad);
 int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, int KW, int transposed, int split_kh,
-                    int Mpad, int Kpad, void* stream);
+                    int Mpad, int Kpad, int mode, void* stream);
 /* out[n][m][Ho][Wo] = epi(sum_k A[k][m] * gather(src[n], k, pixel)).
  * gmode 0: reflect pad, 1: zero pad (forward gather y = oy*stride + kh - pad on the x`up` grid);
  * gmode 2: transposed gather (dgrad) ty = oy + pad - kh, valid iff ty % stride == 0.
@@ -63,7 +71,7 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
  * ReLU backward of the layer that produced src, fused into the dgrad gather. */
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                   int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream);
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, int mode, void* stream);
 /* row-split forward epilogue: out[n][co][y][x] = epi(bias + sum_kh P[n][co*KH+kh][y+kh][x]) where P
  * [N][Cout*KH][H+KH-1][W] came from vst_conv_gemm(KH=1, KW=K, split_kh pack) over the padded rows
  * (RC/network.py:169 deconv3 = ConvTanh(48, 3, 9): 27 GEMM rows instead of 3 padded to 32) */
@@ -76,9 +84,9 @@ int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* au
  * epilogue writes interior pixels straight into dx [N][Cin][H][W] and the reflect-pad border into
  * border [N][Cin][H+2p][W+2p] (only its border is written/read); vst_fold_border then adds the
  * border's reflections into dx.  gmask (optional, dY-shaped) gates dY by (gmask > 0). */
-int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream);
+int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, int mode, void* stream);
 int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
-                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
+                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream);
 /* Thin-channel convolutions (RC/network.py:155 conv1 = ConvLayer(3, 48, 9), :169 deconv3 =
  * ConvTanh(48, 3, 9) backward, VGG conv1_1): a tensor with C*K <= Cu channels is kw-unfolded,
@@ -93,13 +101,13 @@ int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int p
 int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int Wout, int K, int Cu, int sgn, int off,
                   int reflect, void* stream);
 int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K, int Cu, int transposed, int Mpad,
-                        int Kpad, void* stream);
+                        int Kpad, int mode, void* stream);
 int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                        int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
                        int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
-                       void* stream);
+                       int mode, void* stream);
 int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
-                              int Cin, int H, int W, int KS, int pad, void* stream);
+                              int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 /* data gradient of a zero-padded stride-1 KxK conv with few input channels (VGG conv1_1, 64 -> 3):
  * P = tap-split 1x1 transposed GEMM (vst_conv_gemm with A = vst_pack_weight of w viewed as
  * [Cout][Cin*K*K][1][1], transposed; rows (c, kh, kw)), then
@@ -110,7 +118,7 @@ int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int
  * grid (H+2p) x (W+2p); interior pixels go straight into dx, the p-wide border into border
  * [N][Cin][H+2p][W+2p]; then vst_fold_border. */
 int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,
-                          int Wo, int Cin, int H, int W, int KS, int pad, void* stream);
+                          int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 /* Reflect-pad dgrad without the padded grid (ConvLayer / UpsampleConvLayer backward,
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of
@@ -118,7 +126,7 @@ int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float*
  * (vst_dgrad_ring over the [Cout][Cin][KS][KS] weight; ring = N*Cin*vst_dgrad_ring_size floats in
  * four segments top/bottom/left/right), folded into dx's border band by vst_fold_ring
  * (accumulates). */
-int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream);
+int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, int mode, void* stream);
 int vst_dgrad_ring_splits(int Cout, int KS);
 long vst_dgrad_ring_size(int Hv, int Wv, int KS, int Cout);
 int vst_dgrad_ring(const float* dy, const float* w, float* ring, int N, int Cout, int Cin, int KS, int Hv, int Wv,
@@ -133,19 +141,19 @@ int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int 
 long vst_wgrad_workspace(int N, int M, int J, int HWo);
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
                    int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
-                   void* stream);
+                   int mode, void* stream);
 /* same for a stride-1 reflect-padded KxK conv with tiny Cout (row-split, GEMM rows (co,kh));
  * workspace floats = vst_wgrad_workspace(N, Cout*K, K*Cin, (H+K-1)*W) */
 int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
-                            int W, int Cout, int K, int accumulate, void* stream);
+                            int W, int Cout, int K, int accumulate, int mode, void* stream);
 
 /* ---- Gram matrix (RC/utilities.py:93-98): G[n] = F[n] F[n]^T * scale ----------------------
  * workspace floats = vst_wgrad_workspace(N, C, C, HW) */
-int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, void* stream);
+int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, int mode, void* stream);
 /* Gram backward, part 1: S[n] = scale * (gG[n] + gG[n]^T) written as a packed A [Kpad][Mpad]
  * (zero padded); part 2: dF = S F via vst_conv_gemm(KS=1, a_batch_stride=Kpad*Mpad)
  * (bmm backward of RC/utilities.py:97) */
-int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, void* stream);
+int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, int mode, void* stream);
 
 /* ---- InstanceNorm2d(affine) [+ReLU] [+residual] (RC/network.py:91-97, 140-150) ------------
  * stats: [N*C][2] (mean, rstd) saved for backward. */
@@ -217,10 +225,10 @@ int vst_sum_scaled(const float* x, long n, float weight, float* ws, float* out, 
  * as vst_gemm_abt. */
 /* out[n][m][j] = scale * sum_r a[n][m][r] b[n][j][r]; workspace = vst_wgrad_workspace(N, M, J, R) */
 int vst_gemm_abt(const float* a, const float* b, float* out, float* workspace, int N, int M, int J, int R, float scale,
-                 void* stream);
+                 int mode, void* stream);
 /* packed A operand from row-major X[k][m] (transpose 0) or X[m][k] (transpose 1), per batch */
 int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int transpose, int Mpad, int Kpad, long x_bs,
-                    void* stream);
+                    int mode, void* stream);
 /* out[n][p] = ||x[n][:][p]||_2 (LA.vector_norm over channels, AA/network.py:121-122) */
 int vst_channel_norm(const float* x, float* out, int N, int C, int P, void* stream);
 /* A = (S/(qn_i kn_j) + 1) / rowsum_i  (CosineSimilarity, AA/network.py:123-124) */
@@ -264,7 +272,7 @@ int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const f
  * 1/(rowsum qn), e = 1/rowsum from qkbar; attn_bwd_rows: dqn, -r, c r; scale_cols: y = x c[p];
  * attn_dkn: dkn_j = -ks_j^2 sum_c K[c][j](Y[c][j] - qt[c]). */
 int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K, int P, int M, long a_batch_stride,
-                  const float* ra, const float* rb, const float* rd, const float* cg, void* stream);
+                  const float* ra, const float* rb, const float* rd, const float* cg, int mode, void* stream);
 int vst_plane_dot(const float* x, const float* w, float* out, int N, int C, int P, void* stream);
 int vst_channel_dot(const float* x, const float* v, const float* y, float* out, int N, int C, int P, void* stream);
 int vst_attn_fwd_rows(const float* qkbar, const float* qn, float* c, float* e, long n, int Ns, void* stream);

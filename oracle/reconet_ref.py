@@ -252,13 +252,22 @@ def style_grams(VP, style):
     return [gram_matrix(f) for f in vgg_forward(VP, vgg_normalize_(style.clone()), VGG16_PLAN)]
 
 
-def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, temporal=True, forward=None, teacher=None):
+ALL_TERMS = ("FTL", "OTL", "CL", "SL", "RL")
+
+
+def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, temporal=True, forward=None, teacher=None,
+                   terms=None):
     """Loss terms of one `train_candy` step (RC/train_single/train_candy.py:77-148), or of the
     distillation trainers (RC/train_single/train_Flow_SD{1,2}.py:80-160) with
     `forward` = the student's forward and `teacher` = (TP, teacher_forward, t_idx, s_idx): the
     symmetric distillation term SDL = 0.01*BETA*(mse(t1, s1) + mse(t2, s2)) is computed and
     reported but, as in the reference, not added to the total.
+    `terms`: the loss terms summed into `loss` (default all; CL SL RL with temporal=False) -- the
+    reference's clones: train_Flow_noFTL.py:125 (OTL CL SL RL), train_multiple/train_Flow.py (all,
+    12-channel frames, `index` = the last frame's channels).
     Returns dict(loss, CL, SL, FTL, OTL, RL[, SDL]) as 0-d tensors (autograd-connected to P)."""
+    if terms is None:
+        terms = ALL_TERMS if temporal else ("CL", "SL", "RL")
     forward = reconet_forward if forward is None else forward
     o1 = forward(P, img1)
     o2 = forward(P, img2)
@@ -274,13 +283,14 @@ def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, tempora
     cf1 = vgg_forward(VP, i1, VGG16_PLAN)
     cf2 = vgg_forward(VP, i2, VGG16_PLAN)
     out = {}
-    if temporal:
+    if "FTL" in terms:
         Hf, Wf = fmap1.shape[2:]
         ff = resize_bilinear(flow, (Hf, Wf))
         ff = torch.stack([ff[:, 0] * (float(Wf) / flow.shape[3]), ff[:, 1] * (float(Hf) / flow.shape[2])], 1)
         wf = warp(fmap1, ff)
         fm = (resize_bilinear(mask.unsqueeze(1), (Hf, Wf)) > 0).float().expand(-1, fmap1.shape[1], -1, -1)
         out["FTL"] = torch.sum(fm * (fmap2 - wf) ** 2) * (1 / int(fm.count_nonzero())) * w["LAMBDA_F"]
+    if "OTL" in terms:
         ot = s2 - warp(s1, flow)
         it = i2 - warp(i1, flow)
         it = (0.2126 * it[:, 0] + 0.7152 * it[:, 1] + 0.0722 * it[:, 2]).unsqueeze(1).expand(-1, 3, -1, -1)
@@ -296,12 +306,33 @@ def reconet_losses(P, VP, img1, img2, flow, mask, grams, w=LOSS_WEIGHTS, tempora
     reg = ((s1[:, :, :-1, 1:] - s1[:, :, :-1, :-1]) ** 2 + (s1[:, :, 1:, :-1] - s1[:, :, :-1, :-1]) ** 2
            + (s2[:, :, :-1, 1:] - s2[:, :, :-1, :-1]) ** 2 + (s2[:, :, 1:, :-1] - s2[:, :, :-1, :-1]) ** 2)
     out["RL"] = w["GAMMA"] * torch.sum(reg)
-    out["loss"] = sum(out[k] for k in ("FTL", "OTL", "CL", "SL", "RL") if k in out)
+    if "RL" not in terms:
+        del out["RL"]
+    out["loss"] = sum(out[k] for k in ALL_TERMS if k in terms)
     if teacher is not None:
         TP, tfwd, ti, si = teacher
         with torch.no_grad():
             t1, t2 = tfwd(TP, img1)[ti], tfwd(TP, img2)[ti]
         out["SDL"] = (F.mse_loss(t1, o1[si]) + F.mse_loss(t2, o2[si])) * (0.01 * w["BETA"])
+    return out
+
+
+def reconet_single_losses(P, VP, img, grams, w=LOSS_WEIGHTS, forward=None):
+    """Loss terms of one `train_coco2014` step (RC/train_single/train_coco2014.py:65-86): single
+    images, content (relu3_3 MSE x ALPHA) + Gram style (x BETA), no temporal terms, no TV.
+    Returns dict(loss, CL, SL)."""
+    forward = reconet_forward if forward is None else forward
+    s = vgg_normalize_(forward(P, img)[-1])                      # :65, :68
+    i = vgg_normalize_(img.clone())                               # :69 (in place on the batch)
+    sf = vgg_forward(VP, s, VGG16_PLAN)
+    cf = vgg_forward(VP, i, VGG16_PLAN)
+    out = {"CL": F.mse_loss(sf[2], cf[2]) * w["ALPHA"]}          # :74-76
+    sl = 0
+    for k, gs in enumerate(grams):                                # :79-83
+        g = gram_matrix(sf[k])
+        sl = sl + F.mse_loss(g, gs.expand_as(g))
+    out["SL"] = sl * w["BETA"]
+    out["loss"] = out["CL"] + out["SL"]                           # :86
     return out
 
 

@@ -238,6 +238,94 @@ def gen_reconet():
 
 
 # --------------------------------------------------------------------------------------------
+# ReCoNet loop-body clones: train_coco2014 (config 2: single images, content + style only),
+# train_Flow_noFTL (no FTL) and train_multiple/train_Flow (input_frame_num = 4)
+# --------------------------------------------------------------------------------------------
+CLONE_CASES = (
+    # tag, script, single, frames per input, (B, H, W), style (H, W), seeds (model, vgg, data, style)
+    ("coco", ("train_single", "train_coco2014.py"), True, 1, (2, 32, 64), (32, 64), (71, 72, 73, 74)),
+    ("cocor", ("train_single", "train_coco2014.py"), True, 1, (1, 36, 60), (36, 60), (75, 76, 77, 78)),
+    ("noftl", ("train_single", "train_Flow_noFTL.py"), False, 1, (2, 32, 64), (40, 72), (81, 82, 83, 84)),
+    ("multi", ("train_multiple", "train_Flow.py"), False, 4, (2, 32, 64), (40, 72), (91, 92, 93, 94)),
+)
+
+
+def gen_clones():
+    _fresh_project(RC_DIR)
+    rc_util = _load("utilities", os.path.join(RC_DIR, "utilities.py"))
+    sys.modules["utilities"] = rc_util
+    rc_net = _load("network", os.path.join(RC_DIR, "network.py"))
+    sys.modules["network"] = rc_net
+    out = {}
+    for tag, (sub, script), single, nfr, (B, H, W), (Hs, Ws), seeds in CLONE_CASES:
+        style = style_image(seeds[3], Hs, Ws)
+        fake_ds = types.ModuleType("datasets")
+        fake_ds.FlyingThings3D_Monkaa = fake_ds.Coco2014 = lambda *a, **k: None
+        fake_ds.toTensor255 = lambda _img, _s=style: _s[0].clone()
+        sys.modules["datasets"] = fake_ds
+        tr = _load(f"rc_clone_{tag}", os.path.join(RC_DIR, sub, script))
+        if single:
+            img = torch.from_numpy(np.random.default_rng(seeds[2]).uniform(0, 255, (B, 3, H, W)).astype(f32))
+            batch = (img,)
+            out[f"{tag}_img"] = _np(img)
+        else:
+            img1, img2, flow, mask = frame_pair_batch(seeds[2], B, H, W, mask_fn=rc_util.flow_warp_mask)
+            if nfr > 1:  # stacked input frames (RC/datasets.py FlyingThings3D_Monkaa(..., input_frame_num))
+                rng = np.random.default_rng(seeds[2] + 500)
+                prev = torch.from_numpy(rng.uniform(0, 255, (2, B, 3 * (nfr - 1), H, W)).astype(f32))
+                img1 = torch.cat([prev[0], img1], 1)
+                img2 = torch.cat([prev[1], img2], 1)
+            batch = (img1, img2, flow, mask)
+            out[f"{tag}_img1"], out[f"{tag}_img2"] = _np(img1), _np(img2)
+            out[f"{tag}_flow"], out[f"{tag}_mask"] = _np(flow), _np(mask)
+
+        def reconet_factory(n=1, _s=seeds[0], _tr=tr):
+            net = rc_net.ReCoNet(n)
+            seed_module(net, _s)
+            _tr.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(net.named_parameters())))
+            return net
+
+        def vgg_factory(device="cpu", _s=seeds[1]):
+            v = rc_net.Vgg16(device)
+            seed_module(v, _s)
+            return v
+
+        class _Img:
+            BILINEAR = 2
+
+            @staticmethod
+            def open(_p):
+                class _O:
+                    def convert(self, *_):
+                        return self
+
+                    def resize(self, *_):
+                        return self
+
+                return _O()
+
+        tr.device, tr.batch_size, tr.IMG_SIZE, tr.epoch_start, tr.epoch_end = "cpu", B, (W, H), 1, 1
+        tr.DataLoader = lambda *a, _b=batch, **k: [tuple(t.clone() for t in _b)] if len(_b) > 1 else [_b[0].clone()]
+        tr.ReCoNet, tr.Vgg16, tr.Image, tr.tqdm = reconet_factory, vgg_factory, _Img, _TqdmRecorder
+        _TqdmRecorder.records = []
+        save = torch.save
+        torch.save = lambda *a, **k: None
+        try:
+            tr.train()
+        finally:
+            torch.save = save
+        rec = _TqdmRecorder.records[-1]
+        out[f"{tag}_style"], out[f"{tag}_seeds"] = _np(style), np.array(seeds)
+        out[f"{tag}_terms"] = np.array(sorted(k for k in rec if k != "loss"))
+        for k, v in rec.items():
+            out[f"{tag}_{k}"] = np.array(v, dtype=np.float64)
+        adam = tr.optim.Adam
+        _grad_summary(f"{tag}_", adam.grads, adam.after, out, seed=seeds[0] + 1000)
+    np.savez_compressed(os.path.join(HERE, "rc_clones.npz"), **out)
+    print("clone fixtures written")
+
+
+# --------------------------------------------------------------------------------------------
 # ReCoNet distillation trainers (RC/train_single/train_Flow_SD{1,2}.py)
 # --------------------------------------------------------------------------------------------
 def gen_sd():
@@ -617,6 +705,8 @@ if __name__ == "__main__":
         gen_adaattn()
     if "sd" in which:
         gen_sd()
+    if "clones" in which:
+        gen_clones()
     if "infer" in which:
         gen_infer()
     if "rtnstv" in which:

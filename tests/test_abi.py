@@ -15,10 +15,17 @@ def test_header_parses_and_lists_entry_points():
                  "vst_gemm_abt", "vst_pack_matrix", "vst_channel_norm", "vst_cos_attn_rows", "vst_cos_attn_rows_bwd",
                  "vst_softmax_rows", "vst_softmax_rows_bwd", "vst_adaattn_out", "vst_adaattn_out_bwd",
                  "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_copy_planes",
-                 "vst_set_gemm_mode", "vst_get_gemm_mode"):
+                 "vst_build_id"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"
-    assert len(protos["vst_conv_gemm"][1]) == 24
+    assert len(protos["vst_conv_gemm"][1]) == 25
+    # the C ABI is stateless: no global GEMM-mode setter; every GEMM / pack entry takes `mode`
+    assert not [n for n in protos if "set_gemm_mode" in n or "get_gemm_mode" in n]
+    for name in ("vst_pack_weight", "vst_conv_gemm", "vst_conv_gemm_padx", "vst_pack_weight_phase2", "vst_conv_dgrad_s2",
+                 "vst_pack_weight_kwu", "vst_conv_dgrad_padout_kwu", "vst_conv_dgrad_padout", "vst_pack_weight_upsum",
+                 "vst_conv_wgrad", "vst_conv_wgrad_rowsplit", "vst_gram", "vst_symmetrize", "vst_gemm_abt",
+                 "vst_pack_matrix", "vst_attn_gemm"):
+        assert protos[name][1][-2:] == ["int", "void*"], name
 
 
 @pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libvst_hip.so not built (run __graft_entry__.build())")
@@ -36,19 +43,25 @@ def test_host_side_argument_validation_without_gpu():
     """Entry points validate arguments before touching the device: bad calls fail with VST_EINVAL."""
     lib = _lib.lib.load()
     assert lib.vst_conv_gemm(None, None, None, None, None, 1, 3, 8, 8, 4, 27, 8, 8, 3, 3, 0, 1, 1, 1, 0, 0, None, None,
-                             None) == -1
+                             0, None) == -1
     mp, kp = ctypes.c_int(), ctypes.c_int()
     assert lib.vst_conv_pack_dims(48, 243, ctypes.byref(mp), ctypes.byref(kp)) == 0
     assert (mp.value, kp.value) == (64, 256)
     assert lib.vst_conv_pack_dims(192, 1728, ctypes.byref(mp), ctypes.byref(kp)) == 0
     assert (mp.value, kp.value) == (192, 1728)
     assert lib.vst_wgrad_workspace(16, 192, 1728, 8192) > 0
-    # GEMM arithmetic mode: host-side state, validated, default bf16x3 unless VST_GEMM_MODE says otherwise
-    mode = lib.vst_get_gemm_mode()
-    assert mode in (0, 1, 2)
-    assert lib.vst_set_gemm_mode(7) == -1 and lib.vst_get_gemm_mode() == mode
-    assert lib.vst_set_gemm_mode(0) == 0 and lib.vst_get_gemm_mode() == 0
-    assert lib.vst_set_gemm_mode(mode) == 0
+    # GEMM arithmetic is a validated per-call argument: an unknown mode fails before any launch
+    for bad in (-1, 4, 7):
+        assert lib.vst_pack_weight(1, 1, 4, 3, 3, 3, 0, 0, 64, 32, bad, None) == -1
+        assert lib.vst_gemm_abt(1, 1, 1, 1, 1, 4, 4, 16, 1.0, bad, None) == -1
+        assert lib.vst_conv_wgrad(1, 1, 1, 1, 1, 3, 8, 8, 4, 8, 8, 3, 3, 0, 1, 1, 1, 0, bad, None) == -1
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libvst_hip.so not built")
+def test_build_provenance_matches_tree():
+    """vst_build_id() (baked in by csrc/Makefile) equals the hash of this tree's csrc + header."""
+    lib = _lib.lib.load()
+    assert lib.vst_build_id().decode() == _lib.source_build_id()
 
 
 def test_product_fails_loudly_without_hip_tensors():

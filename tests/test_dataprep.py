@@ -256,6 +256,55 @@ def test_loader_rank_sharding(tmp_path):
         DS.FramePairLoader(ds, rank=3, world_size=3)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_loader_shards_pad_to_equal_length(tmp_path, world):
+    """len(dataset) % world != 0: the permutation is padded by wrapping (DistributedSampler), so
+    every rank yields the same number of batches -- no rank blocks in the per-step all-reduce."""
+    from vst.reconet import datasets as DS
+
+    root = str(tmp_path / "mk")
+    D.write_tree(root, "monkaa", 3, 8, 8, 1, 10)  # 9 items
+    ds = DS.Monkaa(root, resolution=(8, 8), frame_num=1)
+    assert len(ds) % world != 0
+    for bs, drop in ((1, False), (2, False), (2, True)):
+        lens, seen = set(), []
+        for r in range(world):
+            ld = DS.FramePairLoader(ds, batch_size=bs, shuffle=True, seed=5, rank=r, world_size=world, drop_last=drop)
+            batches = list(ld._batches())
+            assert len(batches) == len(ld)
+            lens.add(len(batches))
+            seen += [e[0][0] for b in batches for e in b]
+        assert len(lens) == 1, lens
+        if not drop:
+            assert set(seen) == {f[0] for f in ds.frame}  # every item, a few twice
+            assert len(seen) == -(-len(ds) // world) * world
+    # the image loader shares the same sharding
+    class Paths:
+        paths = [f"p{i}" for i in range(7)]
+
+        def __len__(self):
+            return len(self.paths)
+
+    n = {len(list(DS.ImageLoader(Paths(), batch_size=2, rank=r, world_size=world)._index_batches()))
+         for r in range(world)}
+    assert len(n) == 1
+
+
+def test_dataset_items_refuse_dataloader_workers(tmp_path, monkeypatch):
+    """The reference wraps its datasets in DataLoader(num_workers=4); items here are made by HIP
+    kernels, which a forked worker cannot use -- a clear error names the replacement loaders."""
+    import torch
+
+    from vst.reconet import datasets as DS
+
+    root = str(tmp_path / "mk")
+    D.write_tree(root, "monkaa", 3, 8, 8, 1, 4)
+    ds = DS.Monkaa(root, resolution=(8, 8), frame_num=1)
+    monkeypatch.setattr(torch.utils.data, "get_worker_info", lambda: object())
+    with pytest.raises(Exception, match="FramePairLoader"):
+        ds[0]
+
+
 def test_combined_dataset_indexing(tmp_path):
     """FlyingThings3D_Monkaa (RC/datasets.py:256-281): Monkaa items first, then FlyingThings3D;
     both path forms (root string, [monkaa, flyingthings3d] list)."""
@@ -308,3 +357,16 @@ def test_coco_items_match_reference(tmp_path, golden):
     batch = DS.load_images(ds.paths, ds.resolution).cpu().numpy()  # mixed sizes, grouped launches
     for i in range(len(ds)):
         np.testing.assert_array_equal(batch[i], g[f"coco_{i}"])
+
+
+@pytest.mark.gpu
+def test_image_loader_batches_match_reference(tmp_path, golden):
+    """ImageLoader (the DataLoader(Coco2014) replacement of train_coco2014.py:30-36) yields the
+    reference's items batched, bit-exact."""
+    from vst.reconet import datasets as DS
+
+    g, ds = _coco(tmp_path, golden)
+    got = torch.cat(list(DS.ImageLoader(ds, batch_size=3))).cpu().numpy()
+    assert got.shape[0] == len(ds)
+    for i in range(len(ds)):
+        np.testing.assert_array_equal(got[i], g[f"coco_{i}"])

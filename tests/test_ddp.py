@@ -97,3 +97,167 @@ def test_single_process_is_identity():
     assert world_info() == (0, 1)
     assert allreduce_grads(g) == 1.0 and torch.equal(g, torch.ones(5))
     assert shard_seed(1234, 3) == 1237
+
+
+# ----------------------------------------------------------------------------- the product's
+# DP path: FlatParams + GradBuckets (bucketed all-reduce launched from backward hooks) +
+# broadcast_params, driven on CPU tensors with gloo.  The stylizer's top-level blocks keep their
+# nn.Module call structure (that is what the bucket hooks attach to); only their forward bodies are
+# swapped for the oracle's CPU functions (the HIP ops need a GPU).
+def _reconet_cpu(seed):
+    import functools
+
+    import oracle
+    from oracle import reconet_ref as R
+    from oracle import shapes
+    from vst.reconet import network as N
+
+    model = N.ReCoNet()
+    model.load_state_dict(oracle.seeded_params(shapes.reconet(), seed))
+    P = dict(model.named_parameters())
+    body = {"conv1": (R.conv_in_relu, (9, 1)), "conv2": (R.conv_in_relu, (3, 2)), "conv3": (R.conv_in_relu, (3, 2)),
+            "deconv1": (R.conv_in_relu, (3, 1, True)), "deconv2": (R.conv_in_relu, (3, 1, True)),
+            "deconv3": (R.conv_tanh, (9,))}
+    for name, m in model.named_children():
+        fn, extra = body.get(name, (R.residual_block, ()))
+        m.forward = functools.partial(lambda x, _f, _n, _e: _f(x, P, _n, *_e), _f=fn, _n=name, _e=extra)
+    return model
+
+
+def _adaattn_cpu(seed):
+    import functools
+
+    import oracle
+    from oracle import adaattn_ref as A
+    from oracle import shapes
+    from vst.adaattn.network import StylizingNetwork
+
+    model = StylizingNetwork("cosine")
+    model.load_state_dict(oracle.seeded_params(shapes.stylizing_network(), seed))
+    P = dict(model.named_parameters())
+    for i, m in enumerate(model.adaattn):
+        m.forward = functools.partial(lambda c_x, s_x, c_1x, s_1x, _i: A.adaattn(P, f"adaattn.{_i}", c_x, s_x, c_1x, s_1x),
+                                      _i=i)
+    model.decoder.forward = lambda x5, x4, x3: A.decoder(P, x5, x4, x3)
+    return model
+
+
+def _product_dp_step(kind, rank):
+    """One product-trainer step's DP part on CPU: FlatParams views, broadcast from rank 0 (rank 1
+    starts from DIFFERENT weights), per-shard loss through the module call structure, bucketed
+    all-reduce from backward hooks, 1/world scale; returns (flat params after Adam, stats)."""
+    import oracle
+    from oracle import reconet_ref as R
+    from oracle import shapes
+    from vst.reconet._flat import FlatParams
+    from vst.reconet.dist import GradBuckets, broadcast_params, shard_seed
+    from vst.synthetic import content_style_batch, frame_pair_batch, style_image
+
+    if kind == "reconet":
+        model = _reconet_cpu(1 if rank == 0 else 77)
+        flat = FlatParams(model)
+        broadcast_params(flat.p)
+        dp = GradBuckets(model, flat, bucket_bytes=1 << 20)
+        VP = oracle.seeded_params(shapes.vgg16(), 2)
+        img1, img2, flow, mask = frame_pair_batch(shard_seed(40, rank), 1, 32, 64, mask_fn=R.flow_warp_mask)
+        flat.zero_grad()
+        dp.begin()
+        L = R.reconet_losses(None, VP, img1, img2, flow, mask, R.style_grams(VP, style_image(3, 32, 64)),
+                             forward=lambda _P, x: model(x))
+    else:
+        from oracle import adaattn_ref as A
+
+        model = _adaattn_cpu(1 if rank == 0 else 77)
+        flat = FlatParams(model)
+        broadcast_params(flat.p)
+        dp = GradBuckets(model, flat, bucket_bytes=4 << 20)
+        VP = oracle.seeded_params(shapes.vgg19(), 2)
+        c1, c2, s = content_style_batch(shard_seed(50, rank), 1, 32, 64)
+        real = A.stylize
+
+        def stylize(_P, fc, fs):
+            lc, ls = list(fc.values()), list(fs.values())
+            outs = [model.adaattn[i](lc[i + 2], ls[i + 2], A.feature_down_sample(lc, i + 2),
+                                     A.feature_down_sample(ls, i + 2)) for i in range(3)]
+            return model.decoder(outs[2], outs[1], outs[0])
+
+        A.stylize = stylize
+        try:
+            flat.zero_grad()
+            dp.begin()
+            L = A.adaattn_losses(None, VP, c1, c2, s)
+        finally:
+            A.stylize = real
+    L["loss"].backward()
+    gscale = dp.finish()
+    names = [n for n, _ in model.named_parameters()]
+    params = {n: p.detach().clone() for n, p in model.named_parameters()}
+    flat_p = _adam_flat(params, names, flat.g, gscale)
+    return flat_p, flat.g.clone(), dp.stats()
+
+
+def _bucket_worker(rank, world, port, outdir, kind):
+    import sys
+
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "video-style-transfer_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flat_p, g, stats = _product_dp_step(kind, rank)
+    np.save(os.path.join(outdir, f"p{rank}.npy"), flat_p.numpy())
+    np.save(os.path.join(outdir, f"g{rank}.npy"), g.numpy())
+    np.save(os.path.join(outdir, f"stats{rank}.npy"), np.array([stats["buckets"], stats["launched_in_backward"]]))
+    dist.destroy_process_group()
+
+
+def _single_shard_grad(kind, rank):
+    """The same shard's gradient in ONE process with rank 0's weights and no DP (the reference's
+    per-shard step, oracle)."""
+    import oracle
+    from oracle import reconet_ref as R
+    from oracle import shapes
+    from vst.reconet.dist import shard_seed
+    from vst.synthetic import content_style_batch, frame_pair_batch, style_image
+
+    if kind == "reconet":
+        spec = shapes.reconet()
+        P = oracle.seeded_params(spec, 1, requires_grad=True)
+        VP = oracle.seeded_params(shapes.vgg16(), 2)
+        img1, img2, flow, mask = frame_pair_batch(shard_seed(40, rank), 1, 32, 64, mask_fn=R.flow_warp_mask)
+        L = R.reconet_losses(P, VP, img1, img2, flow, mask, R.style_grams(VP, style_image(3, 32, 64)))
+    else:
+        from oracle import adaattn_ref as A
+
+        spec = shapes.stylizing_network()
+        P = oracle.seeded_params(spec, 1, requires_grad=True)
+        VP = oracle.seeded_params(shapes.vgg19(), 2)
+        c1, c2, s = content_style_batch(shard_seed(50, rank), 1, 32, 64)
+        L = A.adaattn_losses(P, VP, c1, c2, s)
+    L["loss"].backward()
+    names = [n for n, _ in spec]
+    return {n: P[n].detach() for n in names}, torch.cat([P[n].grad.reshape(-1) for n in names]), names
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("kind", ["reconet", "adaattn"])
+def test_product_bucketed_dp_equals_mean_of_shard_gradients(tmp_path, kind):
+    world = 2
+    mp.spawn(_bucket_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
+    assert np.array_equal(p0, p1), "replicas diverged (broadcast or all-reduce)"
+    st = np.load(tmp_path / "stats0.npy")
+    assert st[0] > 1, "expected several gradient buckets"
+    assert 0 < st[1] <= st[0], "no bucket was launched from backward (no overlap)"
+    nt = torch.get_num_threads()
+    torch.set_num_threads(2)
+    try:
+        params, g0, names = _single_shard_grad(kind, 0)
+        _, g1, _ = _single_shard_grad(kind, 1)
+    finally:
+        torch.set_num_threads(nt)
+    gsum = np.load(tmp_path / "g0.npy")
+    assert np.abs(gsum - (g0 + g1).numpy()).max() <= 1e-5 * np.abs((g0 + g1).numpy()).max()
+    expect = _adam_flat(params, names, (g0 + g1) / 2, 1.0).numpy()
+    assert np.abs(p0 - expect).max() < 1e-6

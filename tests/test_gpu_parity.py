@@ -98,12 +98,26 @@ def _oracle_conv(x, w, b, stride, pad_mode, up, act):
 
 @pytest.fixture(params=["bf16x3", "f32", "bf16", "bf16x6"])
 def gemm_mode(request):
-    """Runs a test in each GEMM arithmetic mode (vst_set_gemm_mode) and restores the default."""
+    """Runs a test in each GEMM arithmetic mode (the `mode` argument of every GEMM entry) and
+    restores the policy in force before."""
     from vst import ops
 
     ops.gemm_role("fwd")  # applies the environment's policy first
     old = ops.POLICY_NAME[0]
     ops.set_gemm_mode(request.param, policy={})
+    yield request.param
+    ops.use_policy(old)
+
+
+@pytest.fixture(params=["f32", "bf16x6"])
+def step_policy(request):
+    """The fp32-class GEMM policies a whole training step must pass the reference's golden bar
+    under: exact fp32 MFMA (the library default) and bf16x6 everywhere (bench.py's headline)."""
+    from vst import ops
+
+    ops.gemm_role("fwd")
+    old = ops.POLICY_NAME[0]
+    ops.use_policy(request.param)
     yield request.param
     ops.use_policy(old)
 
@@ -357,7 +371,7 @@ def test_sd_checkpoints_forward_golden(golden):
 
 
 @pytest.mark.parametrize("tag", ["b2", "b1r"])
-def test_train_step_golden(golden, tag):
+def test_train_step_golden(golden, tag, step_policy):
     """One full train_candy step (losses, gradients, Adam update) vs the reference's own train()."""
     from vst.reconet import network as N
     from vst.reconet.train import ReCoNetTrainer
@@ -383,6 +397,54 @@ def test_train_step_golden(golden, tag):
         idx = s[f"{tag}_gidx/{n}"]
         assert np.abs(gr[idx].numpy() - s[f"{tag}_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
     tr.step_count = 0
+    tr.flat.adam(1, tr.lr, tr.betas, tr.eps)
+    for n in names:
+        gh = s[f"{tag}_ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        got = C(named[n]).reshape(-1)[:64].numpy()
+        assert np.abs(got - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
+
+
+CLONE_SCRIPTS = {"coco": ("train_coco2014", 1), "cocor": ("train_coco2014", 1), "noftl": ("train_Flow_noFTL", 1),
+                 "multi": ("train_Flow", 4)}
+
+
+@pytest.mark.parametrize("tag", sorted(CLONE_SCRIPTS))
+def test_clone_train_step_golden(golden, tag, step_policy):
+    """The reference's loop-body clones on HIP vs their own train(): train_coco2014 (BASELINE config 2:
+    single images, content + style only), train_Flow_noFTL (no FTL) and train_multiple/train_Flow
+    (input_frame_num = 4, 12-channel conv1, VGG on the last frame's channels).  Losses 1e-3
+    relative; every gradient tensor's norm and 256 sampled elements within 1e-3 of its norm
+    (+1e-4 of the largest); the post-Adam parameter heads 1e-5."""
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+
+    s = golden("rc_clones")
+    script, nfr = CLONE_SCRIPTS[tag]
+    seeds = s[f"{tag}_seeds"]
+    model = _seeded(N.ReCoNet(nfr), shapes.reconet(nfr), int(seeds[0])).to(DEV)
+    vgg = _seeded(N.Vgg16(), shapes.vgg16(), int(seeds[1])).to(DEV)
+    tr = ReCoNetTrainer.for_script(script, model, vgg, G(s[f"{tag}_style"]))
+    terms = sorted(s[f"{tag}_terms"])
+    assert sorted(tr.terms) == terms
+    if tr.single:
+        out = tr.losses(G(s[f"{tag}_img"]))
+    else:
+        frames = torch.stack([G(s[f"{tag}_img1"]), G(s[f"{tag}_img2"])])
+        out = tr.losses(frames, G(s[f"{tag}_flow"]), G(s[f"{tag}_mask"]))
+    for k in ["loss"] + terms:
+        assert rel_err(out[k].item(), s[f"{tag}_{k}"]) < 1e-3, k
+    tr.flat.zero_grad()
+    out["loss"].backward()
+    names = list(s[f"{tag}_names"])
+    named = dict(model.named_parameters())
+    gmax = max(float(s[f"{tag}_gnorm/{n}"]) for n in names)
+    for n in names:
+        gr = C(named[n].grad).reshape(-1)
+        gn = float(s[f"{tag}_gnorm/{n}"])
+        assert abs(float(gr.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"{tag}_gidx/{n}"]
+        assert np.abs(gr[idx].numpy() - s[f"{tag}_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
     tr.flat.adam(1, tr.lr, tr.betas, tr.eps)
     for n in names:
         gh = s[f"{tag}_ghead/{n}"]

@@ -95,6 +95,57 @@ def test_train_step(golden, tag):
         assert np.abs(params[n].reshape(-1)[:64].numpy() - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
 
 
+CLONES = {  # tag: (single, input_frame_num, weights, terms) -- the reference script each golden ran
+    "coco": (True, 1, dict(R.LOSS_WEIGHTS, BETA=1e10), ("CL", "SL")),        # train_coco2014.py
+    "cocor": (True, 1, dict(R.LOSS_WEIGHTS, BETA=1e10), ("CL", "SL")),
+    "noftl": (False, 1, dict(R.LOSS_WEIGHTS, BETA=1e10), ("OTL", "CL", "SL", "RL")),  # train_Flow_noFTL.py
+    "multi": (False, 4, dict(R.LOSS_WEIGHTS, BETA=1e10), R.ALL_TERMS),        # train_multiple/train_Flow.py
+}
+
+
+def check_grads(s, tag, grads, after):
+    """Per-tensor gradient norm / sampled values (1e-3 of the norm + 1e-4 of the largest norm) and
+    the post-Adam parameter heads, against the reference's recorded step."""
+    names = list(s[f"{tag}_names"])
+    assert sorted(names) == sorted(grads)
+    gmax = max(float(s[f"{tag}_gnorm/{n}"]) for n in names)
+    for n in names:
+        g = grads[n].reshape(-1)
+        gn = float(s[f"{tag}_gnorm/{n}"])
+        assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"{tag}_gidx/{n}"]
+        assert np.abs(g[idx].numpy() - s[f"{tag}_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+        gh = s[f"{tag}_ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        assert np.abs(after[n].reshape(-1)[:64].numpy() - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
+
+
+@pytest.mark.parametrize("tag", sorted(CLONES))
+def test_clone_train_steps(golden, tag):
+    """train_coco2014 / train_Flow_noFTL / train_multiple/train_Flow: the oracle vs the
+    reference's own train() (tests/golden/gen_golden.py gen_clones)."""
+    s = golden("rc_clones")
+    single, nfr, w, terms = CLONES[tag]
+    assert sorted(terms) == sorted(s[f"{tag}_terms"])
+    seeds = s[f"{tag}_seeds"]
+    P = oracle.seeded_params(shapes.reconet(nfr), int(seeds[0]), requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg16(), int(seeds[1]))
+    grams = R.style_grams(VP, T(s[f"{tag}_style"]))
+    if single:
+        L = R.reconet_single_losses(P, VP, T(s[f"{tag}_img"]).clone(), grams, w)
+    else:
+        L = R.reconet_losses(P, VP, T(s[f"{tag}_img1"]).clone(), T(s[f"{tag}_img2"]).clone(),
+                             T(s[f"{tag}_flow"]), T(s[f"{tag}_mask"]), grams, w, terms=terms)
+    assert sorted(k for k in L if k != "loss") == sorted(terms)
+    for k in ("loss",) + tuple(terms):
+        assert rel_err(L[k].item(), s[f"{tag}_{k}"]) < 1e-3, k
+    L["loss"].backward()
+    grads = {n: P[n].grad for n in P}
+    params = {n: P[n].detach().clone() for n in P}
+    R.adam_step(params, grads, {})
+    check_grads(s, tag, grads, params)
+
+
 # ----------------------------------------------------------------------------- AdaAttN
 def test_adaattn_units(golden):
     from oracle import adaattn_ref as A

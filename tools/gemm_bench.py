@@ -1,3 +1,4 @@
+import os
 """Microbenchmark of the implicit-GEMM conv kernel on the step's layer shapes, across library
 builds (tuning variants compiled with different -D flags).  Interleaved rounds in one process.
 
@@ -8,6 +9,9 @@ import statistics
 import sys
 
 import torch
+
+# GEMM arithmetic passed to every call (vst_hip.h VST_GEMM_*): 0 f32, 1 bf16x3, 2 bf16, 3 bf16x6
+MODE = int(os.environ.get("BENCH_GEMM_MODE", "3"))
 
 sys.path.insert(0, "video-style-transfer_amd")
 from vst._lib import _CTYPES, parse_header  # noqa: E402
@@ -74,7 +78,7 @@ def main():
                 lib.vst_conv_pack_dims(M, KH * KW * Cs, ctypes.byref(mp), ctypes.byref(kp))
                 wp = torch.randn(kp.value * mp.value, device=dev) * 0.05
                 args = (src.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cs, Hs, Ws, M, KH * KW * Cs, Ho, Wo,
-                        KH, KW, gm, stride, pad, up, 0, 0, None, None, st)
+                        KH, KW, gm, stride, pad, up, 0, 0, None, None, MODE, st)
                 for _ in range(2):
                     assert lib.vst_conv_gemm(*args) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

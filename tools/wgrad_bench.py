@@ -1,3 +1,4 @@
+import os
 """Microbenchmark of the split-K weight-gradient kernel (vst_conv_wgrad) on the step's layer
 shapes, optionally across library builds.  Interleaved rounds, HIP-event timing.
 
@@ -8,6 +9,9 @@ import statistics
 import sys
 
 import torch
+
+# GEMM arithmetic passed to every call (vst_hip.h VST_GEMM_*): 0 f32, 1 bf16x3, 2 bf16, 3 bf16x6
+MODE = int(os.environ.get("BENCH_GEMM_MODE", "3"))
 
 sys.path.insert(0, "video-style-transfer_amd")
 from vst._lib import LIB_PATH, _CTYPES, parse_header  # noqa: E402
@@ -54,7 +58,7 @@ def main():
                 name, N, Cin, H, W, Cout, k, stride, gm, pad, up = s
                 x, dy, dw, ws, Ho, Wo, fl = bufs[name]
                 args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, Ho, Wo, k, k, gm,
-                        stride, pad, up, 0, st)
+                        stride, pad, up, 0, MODE, st)
                 lib.vst_conv_wgrad(*args)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

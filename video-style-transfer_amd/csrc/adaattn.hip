@@ -329,11 +329,12 @@ __global__ void plane_norm_grad_kernel(float* __restrict__ x, const float* __res
 extern "C" {
 
 int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int transpose, int Mpad, int Kpad, long x_bs,
-                    void* stream) {
+                    int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(x && packed && B > 0 && M > 0 && K > 0 && Mpad >= M && Kpad >= K);
   long total = (long)B * Mpad * Kpad;
   pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, apack_split(vst_gemm_mode_internal()));
+      x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, apack_split(mode));
   return vst_launch_status();
 }
 

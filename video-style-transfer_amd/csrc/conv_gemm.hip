@@ -239,17 +239,12 @@ __global__ void fold_border_kernel(const float* __restrict__ border, float* __re
 
 extern "C" {
 
-int vst_version(void) { return 101; }
+int vst_version(void) { return 200; }
 
-static int g_gemm_mode = -1;
-
-int vst_set_gemm_mode(int mode) {
-  VST_CHECK_ARG(mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16 || mode == VST_GEMM_BF16X6);
-  g_gemm_mode = mode;
-  return VST_OK;
-}
-
-int vst_get_gemm_mode(void) { return vst_gemm_mode_internal(); }
+#ifndef VST_BUILD_ID
+#define VST_BUILD_ID "unknown"
+#endif
+const char* vst_build_id(void) { return VST_BUILD_ID; }
 
 const char* vst_strerror(int code) {
   if (code == VST_OK) return "success";
@@ -271,33 +266,21 @@ int vst_conv_pack_dims(int M, int K, int* Mpad, int* Kpad) {
 }
 
 int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, int KW, int transposed, int split_kh,
-                    int Mpad, int Kpad, void* stream) {
+                    int Mpad, int Kpad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && !(transposed && split_kh));
   long total = (long)Mpad * Kpad;
   pack_weight_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
+      w, packed, Cout, Cin, KH, KW, transposed, split_kh, Mpad, Kpad, apack_split(mode));
   return vst_launch_status();
 }
 
 }  // extern "C"
 
-// initial mode from the environment: VST_GEMM_MODE = f32 | bf16x3 (default) | bf16 | bf16x6
-int vst_gemm_mode_internal() {
-  if (g_gemm_mode < 0) {
-    const char* e = getenv("VST_GEMM_MODE");
-    int m = VST_GEMM_BF16X3;
-    if (e && !strcmp(e, "f32")) m = VST_GEMM_F32;
-    if (e && !strcmp(e, "bf16")) m = VST_GEMM_BF16;
-    if (e && !strcmp(e, "bf16x6")) m = VST_GEMM_BF16X6;
-    g_gemm_mode = m;
-  }
-  return g_gemm_mode;
-}
-
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
                             int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
                             int stride, int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux,
-                            const float* gmask, void* stream, const float* ep_ra = nullptr,
+                            const float* gmask, int mode, void* stream, const float* ep_ra = nullptr,
                             const float* ep_rb = nullptr, const float* ep_rd = nullptr,
                             const float* ep_cg = nullptr, float* ph_border = nullptr, int ph_H = 0, int ph_W = 0,
                             int ph_pad = 0) {
@@ -322,7 +305,6 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   {
     // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
     static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
-    const int mode = vst_gemm_mode_internal();
     if (t256 && cfg == T128 && M % 256 == 0 && (mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16)) cfg = T256;
   }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);
@@ -349,7 +331,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   dim3 grid(ceil_div((long)Ho * Wo, bn), P.Mpad / bm, N);
   const bool cfast = (Cs % 16) == 0, gm = gmask != nullptr;
   hipStream_t st = (hipStream_t)stream;
-  switch (vst_gemm_mode_internal()) {
+  switch (mode) {
     case VST_GEMM_F32: launch_prec<0>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16: launch_prec<2>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16X6: launch_prec<3>(cfast, gm, cfg, grid, st, P); break;
@@ -362,15 +344,17 @@ extern "C" {
 
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                   int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* stream) {
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   return vst_conv_gemm_padx(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad,
-                            up, epi, a_batch_stride, aux, gmask, stream);
+                            up, epi, a_batch_stride, aux, gmask, mode, stream);
 }
 
 int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                        int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
                        int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
-                       void* stream) {
+                       int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
   VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
   VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
@@ -378,36 +362,39 @@ int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, 
   if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad_x < Ws * up);
   VST_CHECK_ARG(pad >= 0 && pad_x >= 0);
   return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad_x,
-                          up, epi, a_batch_stride, aux, gmask, stream);
+                          up, epi, a_batch_stride, aux, gmask, mode, stream);
 }
 
 // out[n][m][p] = (sum_k A[n][k][m] B[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]
 // (A packed per image, a_batch_stride floats apart; B = src [N][K][P]; ra, rd may be NULL)
 int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K, int P, int M, long a_batch_stride,
-                  const float* ra, const float* rb, const float* rd, const float* cg, void* stream) {
+                  const float* ra, const float* rb, const float* rd, const float* cg, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(src && apack && out && rb && cg && N > 0 && K > 0 && P > 0 && M > 0);
   return conv_gemm_launch(src, apack, nullptr, nullptr, out, N, K, 1, P, M, K, 1, P, 1, 1, GM_ZERO, 1, 0, 0, 1,
-                          EPI_AFFINE, a_batch_stride, nullptr, nullptr, stream, ra, rb, rd, cg);
+                          EPI_AFFINE, a_batch_stride, nullptr, nullptr, mode, stream, ra, rb, rd, cg);
 }
 
 int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad,
-                           void* stream) {
+                           int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= 4 * Cin);
   VST_CHECK_ARG(Kpad >= (KS + 1) / 2 * ((KS + 1) / 2) * Cout);
   long total = (long)Mpad * Kpad;
   pack_phase2_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-      w, packed, Cout, Cin, KS, Mpad, Kpad, apack_split(vst_gemm_mode_internal()));
+      w, packed, Cout, Cin, KS, Mpad, Kpad, apack_split(mode));
   return vst_launch_status();
 }
 
 int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
-                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* stream) {
+                      int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Ho > 0 && Wo > 0 && Cin > 0 && KS > 0);
   VST_CHECK_ARG(pad >= 0 && pad < H && pad < W && Ho == (H + 2 * pad - KS) / 2 + 1 && Wo == (W + 2 * pad - KS) / 2 + 1);
   const int K2 = (KS + 1) / 2;
   const int Hc = (H + 2 * pad + 1) / 2, Wc = (W + 2 * pad + 1) / 2;
   return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, 4 * Cin, K2 * K2 * Cout, Hc, Wc, K2, K2,
-                          GM_TRANSPOSED, 1, 0, 0, 1, EPI_PHASE2, 0, nullptr, gmask, stream, nullptr, nullptr, nullptr,
+                          GM_TRANSPOSED, 1, 0, 0, 1, EPI_PHASE2, 0, nullptr, gmask, mode, stream, nullptr, nullptr, nullptr,
                           nullptr, border, H, W, pad);
 }
 
@@ -431,31 +418,34 @@ int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int
 }
 
 int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K, int Cu, int transposed, int Mpad,
-                        int Kpad, void* stream) {
+                        int Kpad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && K > 0 && Cu >= (transposed ? Cout : Cin) * K);
   VST_CHECK_ARG(Mpad >= (transposed ? Cin : Cout) && Kpad >= K * Cu);
   const long total = (long)Mpad * Kpad;
   pack_kwu_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, K, Cu, transposed, Mpad,
-                                                                         Kpad, apack_split(vst_gemm_mode_internal()));
+                                                                         Kpad, apack_split(mode));
   return vst_launch_status();
 }
 
 int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
-                              int Cin, int H, int W, int KS, int pad, void* stream) {
+                              int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dyu && wpack && dx && border && N > 0 && Cu % 16 == 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
                 pad < W && Ho == H + 2 * pad - KS + 1);
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   return conv_gemm_launch(dyu, wpack, nullptr, nullptr, dx, N, Cu, Ho, Wp, Cin, KS * Cu, Hp, Wp, KS, 1, GM_TRANSPOSED, 1,
-                          0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, stream, nullptr, nullptr, nullptr, nullptr, border,
+                          0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, mode, stream, nullptr, nullptr, nullptr, nullptr, border,
                           H, W, pad);
 }
 
 int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,
-                          int Wo, int Cin, int H, int W, int KS, int pad, void* stream) {
+                          int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
                 pad < W && Ho == H + 2 * pad - KS + 1 && Wo == W + 2 * pad - KS + 1);
   return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, Cin, KS * KS * Cout, H + 2 * pad,
-                          W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, stream,
+                          W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, mode, stream,
                           nullptr, nullptr, nullptr, nullptr, border, H, W, pad);
 }
 
@@ -717,11 +707,12 @@ __global__ __launch_bounds__(256) void dgrad_ring_kernel(const float* __restrict
 
 extern "C" {
 
-int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, void* stream) {
+int vst_pack_weight_upsum(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(w && packed && Cout > 0 && Cin > 0 && KS > 0 && Mpad >= Cin && Kpad >= (KS + 1) * (KS + 1) * Cout);
   long total = (long)Mpad * Kpad;
   pack_upsum_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, packed, Cout, Cin, KS, Mpad, Kpad,
-                                                                           apack_split(vst_gemm_mode_internal()));
+                                                                           apack_split(mode));
   return vst_launch_status();
 }
 

@@ -465,11 +465,12 @@ int vst_tanh_image_bwd(const float* gy, const float* t, float* gv, long n, int i
   return vst_launch_status();
 }
 
-int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, void* stream) {
+int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, float scale, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(g && S && N > 0 && C > 0 && Kpad >= C && Mpad >= C);
   long total = (long)N * Kpad * Mpad;
   symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale,
-                                                                           apack_split(vst_gemm_mode_internal()));
+                                                                           apack_split(mode));
   return vst_launch_status();
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "vst_hip.h"
+
 #define VST_OK 0
 #define VST_EINVAL (-1)
 #define VST_EUNSUPPORTED (-2)
@@ -61,9 +63,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
-// GEMM arithmetic mode (library-global, see vst_set_gemm_mode in vst_hip.h)
-enum { VST_GEMM_F32 = 0, VST_GEMM_BF16X3 = 1, VST_GEMM_BF16 = 2, VST_GEMM_BF16X6 = 3 };
-int vst_gemm_mode_internal();
+// GEMM arithmetic mode: a per-call argument of every GEMM / pack entry (vst_hip.h VST_GEMM_*);
+// the library keeps no mode state
+static inline bool vst_mode_ok(int mode) {
+  return mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16 || mode == VST_GEMM_BF16X6;
+}
 // packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6)
 static inline int apack_split(int mode) { return mode == VST_GEMM_F32 ? 0 : (mode == VST_GEMM_BF16X6 ? 2 : 1); }
 
@@ -84,8 +88,8 @@ __host__ __device__ inline long apack_index(int k, int m, int Mpad) {
 //   (fp32 MFMA: 2^-24), at 3 x 32 cycles per 32x32x16 instead of 8 x 64: 5.3x the MFMA rate.
 // VST_GEMM_BF16:   hi*hi only (one bf16 MFMA, ~2^-8 relative per product): the reduced-precision
 //   MFMA path of BASELINE config 5 (bf16 keeps fp32's exponent range: no loss scaling).
-// Every packed A operand is written in the layout of the mode current at pack time, so packs
-// must not be reused across a mode change.
+// Every packed A operand is written in the layout of the mode passed to its pack call, so a pack
+// is only valid for GEMM calls with that same mode.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

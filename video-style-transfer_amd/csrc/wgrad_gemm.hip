@@ -1,5 +1,5 @@
-// Split-K "activation-gradient x im2col(input)^T" GEMM on MFMA (fp32 32x32x2, or bf16x3 / bf16 32x32x16
-// per vst_set_gemm_mode).
+// Split-K "activation-gradient x im2col(input)^T" GEMM on MFMA (fp32 32x32x2, or bf16x3 / bf16x6 /
+// bf16 split products on 32x32x16 bf16, per the call's `mode` argument).
 //
 //   slab[z][m][j] = sum_{r in chunk z}  A[n][m][r] * gather(src[n], j, r)
 //
@@ -38,7 +38,8 @@ template <int WM, int TM, int WN, int TN, bool AV, int MINW, int PREC, bool TAP>
 __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int LS = 20;                       // LDS row: fp32 [hi][s] (k = 2s + hi) / bf16 [hi k][lo k]; + 4 pad
+  // LDS row: fp32 [hi][s] (k = 2s + hi) / bf16 [hi k][lo k] / bf16x6 [hi k][mid k][lo k]; + 4 pad
+  constexpr int LS = PREC == 3 ? 28 : 20;
   constexpr int A_F4 = BM * BK / 4;            // vector path: float4 per A tile
   constexpr int A_PV = (A_F4 + NT - 1) / NT;
   // scalar element map: PAIR consecutive pixels per thread (the bf16 paths pack a thread's two
@@ -223,6 +224,20 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       }
     }
   };
+  // one thread's two consecutive pixels of a bf16 row, split per PREC
+  auto store_pair = [&](uint32_t* row, float a, float b) {
+    uint32_t h, l;
+    if constexpr (PREC == 3) {
+      uint32_t md;
+      split3_bf16x2(a, b, h, md, l);
+      row[8 + (rr >> 1)] = md;
+      row[16 + (rr >> 1)] = l;
+    } else {
+      split_bf16x2(a, b, h, l);
+      if (PREC == 1) row[8 + (rr >> 1)] = l;
+    }
+    row[rr >> 1] = h;
+  };
   auto store_tile = [&](int buf) {
     if constexpr (PREC == 0) {
       if constexpr (AV) {
@@ -250,31 +265,27 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
           if (A_F4 % NT == 0 || idx < A_F4) {
             const int m = idx >> 2, q = idx & 3;  // pixels 4q..4q+3 -> bf16 slots 4q..4q+3 = dwords 2q, 2q+1
             uint32_t h0, l0, h1, l1;
-            split_bf16x2(rav[i][0], rav[i][1], h0, l0);
-            split_bf16x2(rav[i][2], rav[i][3], h1, l1);
             uint32_t* row = reinterpret_cast<uint32_t*>(&As[buf][m][0]);
+            if constexpr (PREC == 3) {
+              uint32_t m0, m1;
+              split3_bf16x2(rav[i][0], rav[i][1], h0, m0, l0);
+              split3_bf16x2(rav[i][2], rav[i][3], h1, m1, l1);
+              *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{m0, m1};
+              *reinterpret_cast<u32x2*>(row + 16 + 2 * q) = u32x2{l0, l1};
+            } else {
+              split_bf16x2(rav[i][0], rav[i][1], h0, l0);
+              split_bf16x2(rav[i][2], rav[i][3], h1, l1);
+              if (PREC == 1) *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{l0, l1};
+            }
             *reinterpret_cast<u32x2*>(row + 2 * q) = u32x2{h0, h1};
-            if (PREC == 1) *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{l0, l1};
           }
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < NAR; ++i) {
-          uint32_t h, l;
-          split_bf16x2(ras[2 * i], ras[2 * i + 1], h, l);
-          uint32_t* row = reinterpret_cast<uint32_t*>(&As[buf][cc + i * CPT][0]);
-          row[rr >> 1] = h;
-          if (PREC == 1) row[8 + (rr >> 1)] = l;
-        }
+        for (int i = 0; i < NAR; ++i) store_pair(reinterpret_cast<uint32_t*>(&As[buf][cc + i * CPT][0]), ras[2 * i], ras[2 * i + 1]);
       }
 #pragma unroll
-      for (int i = 0; i < NCOL; ++i) {
-        uint32_t h, l;
-        split_bf16x2(rb[2 * i], rb[2 * i + 1], h, l);
-        uint32_t* row = reinterpret_cast<uint32_t*>(&Bs[buf][crow0 + i * cstep][0]);
-        row[rr >> 1] = h;
-        if (PREC == 1) row[8 + (rr >> 1)] = l;
-      }
+      for (int i = 0; i < NCOL; ++i) store_pair(reinterpret_cast<uint32_t*>(&Bs[buf][crow0 + i * cstep][0]), rb[2 * i], rb[2 * i + 1]);
     }
   };
 
@@ -286,7 +297,9 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) load_tile(t + 1);
-    if constexpr (PREC != 0) {
+    if constexpr (PREC == 3) {
+      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else if constexpr (PREC != 0) {
       mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
     } else {
       f32x4 a[TM][2], b[TN][2];
@@ -411,14 +424,15 @@ static void launch_wg_p(bool av, bool tap, int c, dim3 g, hipStream_t st, const 
     av ? launch_wg_t<true, PR, false>(c, g, st, P) : launch_wg_t<false, PR, false>(c, g, st, P);
 }
 
-static void launch_wg(int c, bool tap, dim3 g, hipStream_t st, const WgParams& P) {
+static void launch_wg(int c, bool tap, dim3 g, int mode, hipStream_t st, const WgParams& P) {
   // float4 A loads need 4 consecutive pixels in one row segment (and, for the row-split gather,
   // in one output row)
   const bool av = (P.Ho * P.Wo) % 4 == 0 && (!P.asplit || P.Wo % 4 == 0);
-  switch (vst_gemm_mode_internal()) {
+  switch (mode) {
     case VST_GEMM_F32: launch_wg_p<0>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg_p<2>(av, tap, c, g, st, P); break;
-    default: launch_wg_p<1>(av, tap, c, g, st, P); break;  // bf16x3 (also under bf16x6: no packed operand here)
+    case VST_GEMM_BF16X6: launch_wg_p<3>(av, tap, c, g, st, P); break;
+    default: launch_wg_p<1>(av, tap, c, g, st, P); break;
   }
 }
 
@@ -452,7 +466,8 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
 }
 
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
-                  int KH, int KW, int gmode, int stride, int pad, int up, int S, int asplit, int Ha, hipStream_t st) {
+                  int KH, int KW, int gmode, int stride, int pad, int up, int S, int asplit, int Ha, int mode,
+                  hipStream_t st) {
   WgParams P;
   P.a = a;
   P.src = src;
@@ -487,7 +502,7 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
   const bool tap = !asplit && KH * KW > 1 && Cs % WBN == 0;
   const int gxn = tap ? KH * KW * ((Cs + WBN - 1) / WBN) : P.Jpad / WBN;
   dim3 g(gxn, P.Mpad / wbm(c), N * S);
-  launch_wg(c, tap, g, st, P);
+  launch_wg(c, tap, g, mode, st, P);
   return vst_launch_status();
 }
 
@@ -515,13 +530,14 @@ long vst_wgrad_workspace(int N, int M, int J, int HWo) {
 
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
                    int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
-                   void* stream) {
+                   int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
   long J = (long)KH * KW * Cin;
   int S = splits_for(N, Cout, J, Ho * Wo);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(dy, x, workspace, N, Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, S, 0, 0, st);
+  int rc = run_wg(dy, x, workspace, N, Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, S, 0, 0, mode, st);
   if (rc) return rc;
   int c = wsel(Cout);
   long Mpad = (Cout + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = (J + WBN - 1) / WBN * WBN;
@@ -536,13 +552,14 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
 // j = (kw, ci), reduction over the (H+K-1) x W grid of padded rows q:
 //   dW[co][ci][kh][kw] = sum_q dy[co][q_y - kh][q_x] * Xpad[ci][q_y][q_x + kw]
 int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
-                            int W, int Cout, int K, int accumulate, void* stream) {
+                            int W, int Cout, int K, int accumulate, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && K > 0 && (K & 1) && K / 2 < H &&
                 K / 2 < W);
   const int M = Cout * K, J = K * Cin, Hq = H + K - 1;
   int S = splits_for(N, M, J, Hq * W);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(dy, x, workspace, N, M, Cin, H, W, Hq, W, 1, K, 0, 1, K / 2, 1, S, K, H, st);
+  int rc = run_wg(dy, x, workspace, N, M, Cin, H, W, Hq, W, 1, K, 0, 1, K / 2, 1, S, K, H, mode, st);
   if (rc) return rc;
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = ((long)J + WBN - 1) / WBN * WBN;
@@ -553,11 +570,12 @@ int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* w
 }
 
 // G[n] = F[n] F[n]^T * scale,  F = [N][C][H*W]
-int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, void* stream) {
+int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, float scale, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(f && g && workspace && N > 0 && C > 0 && HW > 0);
   int S = splits_for(N, C, C, HW);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(f, f, workspace, N, C, C, 1, HW, 1, HW, 1, 1, 1, 1, 0, 1, S, 0, 0, st);
+  int rc = run_wg(f, f, workspace, N, C, C, 1, HW, 1, HW, 1, 1, 1, 1, 0, 1, S, 0, 0, mode, st);
   if (rc) return rc;
   int c = wsel(C);
   long Mpad = (C + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = (C + WBN - 1) / WBN * WBN;
@@ -569,11 +587,12 @@ int vst_gram(const float* f, float* g, float* workspace, int N, int C, int HW, f
 // out[n][m][j] = scale * sum_r a[n][m][r] * b[n][j][r]   (per-image A B^T; AdaAttN moments,
 // attention query gradient, cosine-distance C x C products)
 int vst_gemm_abt(const float* a, const float* b, float* out, float* workspace, int N, int M, int J, int R, float scale,
-                 void* stream) {
+                 int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(a && b && out && workspace && N > 0 && M > 0 && J > 0 && R > 0);
   int S = splits_for(N, M, J, R);
   hipStream_t st = (hipStream_t)stream;
-  int rc = run_wg(a, b, workspace, N, M, J, 1, R, 1, R, 1, 1, 1, 1, 0, 1, S, 0, 0, st);
+  int rc = run_wg(a, b, workspace, N, M, J, 1, R, 1, R, 1, 1, 1, 1, 0, 1, S, 0, 0, mode, st);
   if (rc) return rc;
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c), Jpad = ((long)J + WBN - 1) / WBN * WBN;

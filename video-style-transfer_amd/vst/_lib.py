@@ -5,6 +5,8 @@ single source of truth for the boundary.  There is no CPU fallback: if the share
 missing or fails to load, every op raises.
 """
 import ctypes
+import glob
+import hashlib
 import os
 import re
 
@@ -13,6 +15,20 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvst_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "vst_hip.h")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+
+def source_build_id(csrc=CSRC, header=HEADER_PATH):
+    """sha256 (first 16 hex digits) over the sorted csrc/*.hip, *.h and Makefile, then the public
+    header: the recipe csrc/Makefile bakes into vst_build_id() at build time."""
+    files = sorted(os.path.basename(f) for pat in ("*.hip", "*.h", "Makefile") for f in glob.glob(os.path.join(csrc, pat)))
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    with open(header, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
 
 _CTYPES = {
     "int": ctypes.c_int,
@@ -68,6 +84,13 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = _CTYPES[rt] if rt != "char*" else ctypes.c_char_p
             fn.argtypes = [_CTYPES[a] for a in argts]
+        # provenance: the library must have been built from the sources of this tree
+        built = lib.vst_build_id().decode()
+        want = source_build_id() if os.path.isdir(CSRC) else built
+        if built != want and os.environ.get("VST_ALLOW_STALE_BUILD") != "1":
+            raise VstError(f"libvst_hip.so build id {built} does not match the sources in {CSRC} ({want}): "
+                           "stale build, rebuild with `make -C video-style-transfer_amd/csrc`")
+        self.build_id = built
         self._lib = lib
         return lib
 

@@ -40,7 +40,7 @@ def packed_matrix(x, M, K, transpose, role="attn"):
     Mpad, Kpad = ops.pack_dims(M, K)
     per = ops.pack_floats(Mpad, Kpad)
     ap = _empty((N * per,), x)
-    lib.vst_pack_matrix(ptr(x), ptr(ap), N, M, K, int(transpose), Mpad, Kpad, M * K, stream())
+    lib.vst_pack_matrix(ptr(x), ptr(ap), N, M, K, int(transpose), Mpad, Kpad, M * K, ops.gemm_mode(), stream())
     return ap, per
 
 
@@ -66,7 +66,7 @@ def gemm_abt(a, b, scale=1.0, role="attn"):
     from .. import kprof
 
     tok = kprof.begin(2.0 * N * M * J * R, 4.0 * (a.numel() + b.numel() + out.numel()), ("abt", N, M, J, R), ops.gemm_mode())
-    lib.vst_gemm_abt(ptr(a), ptr(b), ptr(out), ptr(ws), N, M, J, R, float(scale), stream())
+    lib.vst_gemm_abt(ptr(a), ptr(b), ptr(out), ptr(ws), N, M, J, R, float(scale), ops.gemm_mode(), stream())
     kprof.end(tok, family="gemm_abt")
     return out
 
@@ -83,7 +83,7 @@ def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None, role="attn"):
     from .. import kprof
 
     tok = kprof.begin(2.0 * N * M * P * K, 4.0 * (b.numel() + ap.numel() + out.numel()), ("attn", N, M, K, P), ops.gemm_mode())
-    lib.vst_attn_gemm(ptr(b), ptr(ap), ptr(out), N, K, P, M, abs_, ptr(ra), ptr(rb), ptr(rd), ptr(cg), stream())
+    lib.vst_attn_gemm(ptr(b), ptr(ap), ptr(out), N, K, P, M, abs_, ptr(ra), ptr(rb), ptr(rd), ptr(cg), ops.gemm_mode(), stream())
     kprof.end(tok)
     return out
 

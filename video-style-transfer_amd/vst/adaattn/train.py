@@ -21,7 +21,7 @@ import torch
 
 from .. import ops
 from ..reconet._flat import FlatParams
-from ..reconet.dist import allreduce_grads, world_info
+from ..reconet.dist import GradBuckets, broadcast_params, world_info
 from .lossfn import global_stylized_loss, image_similarity_loss, local_feature_loss
 from .network import AdaAttnNoConv
 from .utilities import feature_down_sample
@@ -66,6 +66,9 @@ class AdaAttNTrainer:
         self.step_count = 0
         self.pg = process_group
         self.rank, self.world = world_info(process_group)
+        # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
+        broadcast_params(self.flat.p, process_group)
+        self.dp = GradBuckets(model, self.flat, process_group)
 
     def encode(self, c1, c2=None, s=None):
         """VGG19 features of the data images (no gradient).  c1 may be a [3, B, 3, H, W] buffer."""
@@ -105,9 +108,10 @@ class AdaAttNTrainer:
 
     def step(self, c1, c2=None, s=None):
         self.flat.zero_grad()
+        self.dp.begin()
         out = self.losses(c1, c2, s)
         out["loss"].backward()
-        gscale = allreduce_grads(self.flat.g, self.pg)
+        gscale = self.dp.finish()
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}

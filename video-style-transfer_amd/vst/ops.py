@@ -35,50 +35,62 @@ def _check(t, name, ndim=None):
 
 
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
-_BASE_MODE = [None]  # the mode chosen by the user (set_gemm_mode / VST_GEMM_MODE)
-_LIB_MODE = [None]   # the mode currently set in the library
-# per-role overrides of the base mode; roles: "fwd" (forward products), "dgrad" (data gradients,
-# Gram backward), "wgrad" (weight gradients), "attn" (AdaAttN attention products, fwd + bwd)
+# The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
+# module chooses that argument per call from a named policy (base mode + per-role overrides,
+# optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
+# the pack and GEMM calls that follow it pass to the library.
+_BASE_MODE = [None]  # base mode of the selected policy
+_CUR = [None]        # mode of the GEMM being set up (gemm_role)
+# per-role overrides of the base mode; roles: "fwd" (forward products), "fwd_img" (Cin = 3),
+# "dgrad" (data gradients, Gram backward), "wgrad" (weight gradients, Gram), "attn_cosine" /
+# "attn_softmax" (AdaAttN attention products, fwd + bwd)
 GEMM_POLICY = {}
+DEFAULT_POLICY = "f32"
 
 
 def _mode_id(mode):
-    return int(GEMM_MODES.get(mode, mode))
+    m = GEMM_MODES.get(mode, mode)
+    if m not in GEMM_MODES.values():
+        raise VstError(f"unknown GEMM mode {mode!r} (one of {sorted(GEMM_MODES)})")
+    return int(m)
 
 
-# Named policies (base mode, per-role overrides).  "parity" (default): bf16x3 split MFMA for
-# every GEMM except the stylizer forwards outside the residual blocks, which run bf16x6 (three-way
-# split, fp32-level error): their outputs feed InstanceNorm, whose mean subtraction and ReLU
-# decisions amplify a 5e-6 relative product error into 1e-3 of a gradient element's tensor norm
-# (measured margins, tools/policy_check.py: all stylizer forwards bf16x3 1.07 of the gradient
-# tolerance on the ragged golden step; none 0.002; the residual blocks alone in bf16x3 keep the
-# gradient norms within 0.27 of it but flip single post-Adam elements of res3.in1.bias and the SD2
-# student, so they stay bf16x6 too); and the softmax attention (exp of raw dot products) stays
-# exact fp32.  "bf16x6": fp32-level products
-# everywhere (wgrad-kernel GEMMs bf16x3).  "bf16x3": every GEMM split in two (loss terms within
-# 2e-6 of the reference; gradient elements within ~1e-3 of their tensor norm).  "f32": exact
-# fp32 MFMA everywhere.  "bf16": single bf16 products (reduced-precision path of config 5).
+# Named policies (base mode, per-role overrides).
+#   "f32" (default): exact fp32 MFMA products everywhere.
+#   "bf16x6": every GEMM (conv fwd / dgrad / wgrad, Gram, attention) on three-way split bf16
+#     products, per-product error ~2^-24 (fp32-class) at 2.7x the fp32 MFMA rate; the softmax
+#     attention (exp of raw dot products) stays exact fp32.
+#   "parity": bf16x3 split MFMA (~2^-16 per product) for every GEMM except the stylizer forwards,
+#     which run bf16x6: their outputs feed InstanceNorm, whose mean subtraction and ReLU decisions
+#     amplify a 5e-6 relative product error into 1e-3 of a gradient element's tensor norm
+#     (tools/policy_check.py: all stylizer forwards bf16x3 -> 1.07 of the gradient tolerance on the
+#     ragged golden step; none -> 0.002); the softmax attention stays exact fp32.
+#   "bf16x3": every GEMM split in two (fails the ragged golden step's gradient tolerance, 1.07).
+#   "bf16": single bf16 products (~2^-8): the reduced-precision path of BASELINE config 5.
 POLICIES = {
-    "parity": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6", "attn_softmax": "f32"}),
-    "bf16x6": ("bf16x6", {"attn_softmax": "f32"}),
-    "bf16x3": ("bf16x3", {}),
     "f32": ("f32", {}),
+    "bf16x6": ("bf16x6", {"attn_softmax": "f32"}),
+    "parity": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6", "attn_softmax": "f32"}),
+    "bf16x3": ("bf16x3", {}),
     "bf16": ("bf16", {}),
 }
 
 
+def _ensure_policy():
+    if POLICY_NAME[0] is None:
+        use_policy(os.environ.get("VST_GEMM_POLICY", DEFAULT_POLICY))
+
+
 def base_gemm_mode():
-    """GEMM arithmetic selected for the step (vst_set_gemm_mode): 0 exact fp32 MFMA, 1 bf16x3 split
-    (fp32 operands and accumulation; default), 2 bf16 (reduced precision)."""
-    if _BASE_MODE[0] is None:
-        _BASE_MODE[0] = _LIB_MODE[0] = int(lib.load().vst_get_gemm_mode())
+    """Base GEMM mode of the selected policy (0 f32, 1 bf16x3, 2 bf16, 3 bf16x6)."""
+    _ensure_policy()
     return _BASE_MODE[0]
 
 
 def gemm_mode():
-    """The mode the library currently launches GEMMs (and writes weight packs) with."""
-    base_gemm_mode()
-    return _LIB_MODE[0]
+    """The mode passed to the library by the pack / GEMM calls being issued (set by gemm_role)."""
+    _ensure_policy()
+    return _CUR[0]
 
 
 def gemm_mode_name(mode=None):
@@ -86,14 +98,10 @@ def gemm_mode_name(mode=None):
     return {v: k for k, v in GEMM_MODES.items()}[mode]
 
 
-def _apply_mode(m):
-    if _LIB_MODE[0] != m:
-        lib.vst_set_gemm_mode(m)
-        _LIB_MODE[0] = m
-
-
 def use_policy(name):
     """Select a named policy (POLICIES); returns (base mode, overrides)."""
+    if name not in POLICIES:
+        raise VstError(f"unknown GEMM policy {name!r} (one of {sorted(POLICIES)})")
     base, pol = POLICIES[name]
     set_gemm_mode(base, pol)
     POLICY_NAME[0] = name
@@ -104,14 +112,18 @@ POLICY_NAME = [None]
 
 
 def set_gemm_mode(mode, policy=None):
-    """mode: 0/1/2 or "f32"/"bf16x3"/"bf16"; policy: {role: mode} overrides (replaces GEMM_POLICY)."""
-    base_gemm_mode()
+    """mode: 0..3 or "f32"/"bf16x3"/"bf16"/"bf16x6"; policy: {role: mode} overrides (replaces GEMM_POLICY)."""
     POLICY_NAME[0] = "custom"
-    _BASE_MODE[0] = _mode_id(mode)
+    _BASE_MODE[0] = _CUR[0] = _mode_id(mode)
     if policy is not None:
         GEMM_POLICY.clear()
         GEMM_POLICY.update({r: _mode_id(m) for r, m in policy.items()})
-    _apply_mode(_BASE_MODE[0])
+
+
+def policy_modes():
+    """Names of every mode the selected policy can launch (for labelling results)."""
+    _ensure_policy()
+    return sorted({gemm_mode_name(m) for m in [_BASE_MODE[0], *GEMM_POLICY.values()]})
 
 
 _SCOPE = [None]
@@ -131,18 +143,17 @@ def gemm_scope(name):
 
 
 def gemm_role(role):
-    """Select the library mode for a GEMM of `role` (call before packing its A operand); the
-    first call applies the VST_GEMM_POLICY environment variable (default "parity")."""
-    if POLICY_NAME[0] is None:
-        use_policy(os.environ.get("VST_GEMM_POLICY", "parity"))
+    """Choose the mode for a GEMM of `role` (call before packing its A operand); the first call
+    applies the VST_GEMM_POLICY environment variable (default "f32")."""
+    _ensure_policy()
     m = None
     sc = _SCOPE[0]
     while sc is not None and m is None:
         m = GEMM_POLICY.get(f"{sc}.{role}")
         sc = sc.rpartition(".")[0] or None
     if m is None:
-        m = GEMM_POLICY.get(role, base_gemm_mode())
-    _apply_mode(m)
+        m = GEMM_POLICY.get(role, _BASE_MODE[0])
+    _CUR[0] = m
     return m
 
 
@@ -189,9 +200,10 @@ def packed_weight(w, transposed, split_kh=False, kwu=False):
     Mpad, Kpad = pack_dims(M, K)
     out = _empty((pack_floats(Mpad, Kpad),), w)
     if kwu:
-        lib.vst_pack_weight_kwu(ptr(w), ptr(out), Cout, Cin, KW, Cu, int(transposed), Mpad, Kpad, stream())
+        lib.vst_pack_weight_kwu(ptr(w), ptr(out), Cout, Cin, KW, Cu, int(transposed), Mpad, Kpad, gemm_mode(), stream())
     else:
-        lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, stream())
+        lib.vst_pack_weight(ptr(w), ptr(out), Cout, Cin, KH, KW, int(transposed), int(split_kh), Mpad, Kpad, gemm_mode(),
+                            stream())
     if not w.requires_grad:
         entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
         entry[key] = out
@@ -236,7 +248,7 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
                       (N, Cs, Hs, Ws, M, Ho, Wo, kh, ks, gmode, stride, pad, up), gemm_mode())
     lib.vst_conv_gemm_padx(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho,
                            Wo, kh, ks, gmode, stride, pad, pad if pad_x is None else pad_x, up, epi, a_batch_stride,
-                           ptr(aux), ptr(gmask), stream())
+                           ptr(aux), ptr(gmask), gemm_mode(), stream())
     kprof.end(tok)
     return out
 
@@ -291,7 +303,8 @@ def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops):
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
     tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
-    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad, stream())
+    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad, gemm_mode(),
+                              stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -311,7 +324,7 @@ def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops):
                       (N, dyu.shape[1], Ho, W + 2 * pad, Cin, H + 2 * pad, W + 2 * pad, 1, ks, GM_TRANSPOSED, 1, 0, 1),
                       gemm_mode())
     lib.vst_conv_dgrad_padout_kwu(ptr(dyu), ptr(wp), ptr(dx), ptr(border), N, dyu.shape[1], Ho, Cin, H, W, ks, pad,
-                                  stream())
+                                  gemm_mode(), stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -329,7 +342,7 @@ def conv_dgrad_ring(gz, w, x_shape, ks, up, flops):
     else:
         Mpad, Kpad = pack_dims(Cin, (ks + 1) * (ks + 1) * Cout)
         wp = _empty((pack_floats(Mpad, Kpad),), w)
-        lib.vst_pack_weight_upsum(ptr(w), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
+        lib.vst_pack_weight_upsum(ptr(w), ptr(wp), Cout, Cin, ks, Mpad, Kpad, gemm_mode(), stream())
         dx = conv_gemm(gz, wp, Cin, ks + 1, H, W, GM_ZERO, 2, ks - 1 - p, 1, algo_flops=flops)
     Hv, Wv = H * up, W * up
     ring = _empty((N * Cin * lib.vst_dgrad_ring_size(Hv, Wv, ks, Cout),), gz)
@@ -346,7 +359,7 @@ def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
     k2 = (ks + 1) // 2
     Mpad, Kpad = pack_dims(4 * Cin, k2 * k2 * Cout)
     wp = _empty((pack_floats(Mpad, Kpad),), w)
-    lib.vst_pack_weight_phase2(ptr(w.contiguous()), ptr(wp), Cout, Cin, ks, Mpad, Kpad, stream())
+    lib.vst_pack_weight_phase2(ptr(w.contiguous()), ptr(wp), Cout, Cin, ks, Mpad, Kpad, gemm_mode(), stream())
     dx = _empty(x_shape, gz)
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
     Hc, Wc = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
@@ -354,7 +367,7 @@ def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
                       4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, Cout, Ho, Wo, 4 * Cin, Hc, Wc, k2, k2, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
     lib.vst_conv_dgrad_s2(ptr(gz), ptr(wp), ptr(gmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
-                          stream())
+                          gemm_mode(), stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -371,7 +384,7 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     tok = kprof.begin(2.0 * N * Cout * Ho * Wo * Cin * ks * ks, 4.0 * (gz.numel() + x.numel() + dw.numel()),
                       ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), gemm_mode())
     lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
-                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), stream())
+                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), gemm_mode(), stream())
     kprof.end(tok, family="wgrad")
     return dw
 
@@ -399,7 +412,7 @@ def conv_wgrad_rowsplit(gz, x, w_shape, out=None):
     ws = _empty((lib.vst_wgrad_workspace(N, Cout * K, K * Cin, (H + K - 1) * W),), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
-    lib.vst_conv_wgrad_rowsplit(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, K, int(acc), stream())
+    lib.vst_conv_wgrad_rowsplit(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, K, int(acc), gemm_mode(), stream())
     return dw
 
 
@@ -668,7 +681,7 @@ class GramFn(Function):
         ws = _empty((lib.vst_wgrad_workspace(N, C, C, H * W),), y)
         gemm_role("fwd")
         ctx.scale = 1.0 / (H * W) if per_hw else 1.0 / (C * H * W)
-        lib.vst_gram(ptr(y), ptr(g), ptr(ws), N, C, H * W, ctx.scale, stream())
+        lib.vst_gram(ptr(y), ptr(g), ptr(ws), N, C, H * W, ctx.scale, gemm_mode(), stream())
         ctx.save_for_backward(y)
         return g
 
@@ -679,7 +692,7 @@ class GramFn(Function):
         Mpad, Kpad = pack_dims(C, C)
         S = _empty((N * pack_floats(Mpad, Kpad),), y)
         gemm_role("dgrad")
-        lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, ctx.scale, stream())
+        lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, ctx.scale, gemm_mode(), stream())
         dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=pack_floats(Mpad, Kpad))
         return dy.view(N, C, H, W), None
 

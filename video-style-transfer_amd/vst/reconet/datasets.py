@@ -96,6 +96,7 @@ class _FlowDataset(torch.utils.data.Dataset):
         return self.frame[idx], self.flow[idx], self.motion[idx]
 
     def __getitem__(self, idx):
+        _no_worker(type(self).__name__)
         img1, img2, flow, mask = prepare_batch([self.entries(idx)], self.resolution, self.frame_num, self.device)
         return img1[0], img2[0], flow[0], mask[0]
 
@@ -199,26 +200,48 @@ class Coco2014(torch.utils.data.Dataset):
         return self.length
 
     def __getitem__(self, idx):
+        _no_worker("Coco2014")
         return load_images([self.paths[idx]], self.resolution, self.device)[0]
+
+
+def _no_worker(name):
+    """Items are made by HIP kernels in the calling process; a forked DataLoader worker cannot use
+    the GPU the parent already initialised, so say so instead of failing inside HIP."""
+    if torch.utils.data.get_worker_info() is not None:
+        raise VstError(f"{name} items are prepared on the GPU: iterate it with ImageLoader / FramePairLoader "
+                       "(vst.reconet.datasets) instead of DataLoader(num_workers>0)")
 
 
 def load_images(paths, resolution, device=None):
     """(len(paths), 3, H, W) fp32 = toTensor255(Image.open(p).convert("RGB").resize(resolution,
     BILINEAR)) per path; images sharing a source size go through one kernel launch."""
-    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    Wo, Ho = resolution
-    out = torch.empty((len(paths), 3, Ho, Wo), dtype=torch.float32, device=dev)
+    return prepare_images(stage_images(paths), resolution, device)
+
+
+def stage_images(paths):
+    """Host half of load_images: decode into pinned uint8 staging, grouped by source size."""
     groups = {}
     for i, p in enumerate(paths):
         a = _decode(p, "RGB")
         groups.setdefault(a.shape, []).append((i, a))
+    staged = []
     for shape, items in groups.items():
         host = torch.empty((len(items),) + shape, dtype=torch.uint8).pin_memory()
         for j, (_, a) in enumerate(items):
             host[j].numpy()[...] = a
+        staged.append(([i for i, _ in items], host))
+    return len(paths), staged
+
+
+def prepare_images(staged, resolution, device=None):
+    """Device half of load_images: one H2D copy + one resize launch per source size."""
+    n, groups = staged
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    Wo, Ho = resolution
+    out = torch.empty((n, 3, Ho, Wo), dtype=torch.float32, device=dev)
+    for idx, host in groups:
         imgs = ops.pil_resize_to_tensor255(host.to(dev, non_blocking=True), resolution)
-        idx = torch.tensor([i for i, _ in items], device=dev)
-        out.index_copy_(0, idx, imgs)
+        out.index_copy_(0, torch.tensor(idx, device=dev), imgs)
     return out
 
 
@@ -295,17 +318,14 @@ def prepare_batch(entries, resolution, frame_num, device=None):
     return prepare_staged(stage_batch(entries, frame_num), resolution, frame_num, device)
 
 
-class FramePairLoader:
-    """`DataLoader(dataset, batch_size, shuffle)` replacement (RC/train_single/train_candy.py:34-39):
-    yields device batches `(img1, img2, flow_into_past, mask)`; the host decode / PFM read of the
-    next batch runs in a background thread while the current batch is on the GPU."""
+class _ShardedLoader:
+    """Per-epoch seeded permutation shared by all ranks, padded by wrapping to a multiple of
+    world_size (DistributedSampler semantics), each rank taking its strided share: every rank
+    gets the same number of items and batches, so the per-step gradient all-reduce never waits on
+    a rank that ran out of data."""
 
     def __init__(self, dataset, batch_size=1, shuffle=False, drop_last=False, seed=None, device=None, rank=None,
                  world_size=None):
-        """rank / world_size (default: torch.distributed's when initialised): every rank draws the
-        same seeded permutation per epoch and takes its strided share of it (DistributedSampler
-        semantics without padding), so the ranks' frame pairs are disjoint -- the DP trainer's
-        sharding (vst.reconet.dist)."""
         self.dataset, self.batch_size, self.shuffle, self.drop_last = dataset, batch_size, shuffle, drop_last
         dist = torch.distributed
         on = dist.is_available() and dist.is_initialized()
@@ -316,28 +336,85 @@ class FramePairLoader:
         self.rng = random.Random(seed if seed is not None else 0 if self.world_size > 1 else None)
         self.device = device
 
+    def _per_rank(self):
+        n = len(self.dataset)
+        return -(-n // self.world_size) if self.world_size > 1 else n
+
     def _indices(self):
         order = list(range(len(self.dataset)))
         if self.shuffle:
             self.rng.shuffle(order)
+        if self.world_size > 1 and order:
+            total = self._per_rank() * self.world_size
+            while len(order) < total:  # wrap (repeats only the first items of the permutation)
+                order += order[:total - len(order)]
         return order[self.rank::self.world_size]
 
     def __len__(self):
-        n = len(range(len(self.dataset))[self.rank::self.world_size])
+        n = self._per_rank()
         return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
 
-    def _batches(self):
+    def _index_batches(self):
         order = self._indices()
         for i in range(0, len(order), self.batch_size):
             idx = order[i:i + self.batch_size]
             if len(idx) < self.batch_size and self.drop_last:
                 return
+            yield idx
+
+
+class ImageLoader(_ShardedLoader):
+    """`DataLoader(Coco2014(...), batch_size, shuffle)` replacement (RC/train_single/
+    train_coco2014.py:30-36): yields (B, 3, H, W) device batches made by `load_images` (Pillow-exact
+    resize on the GPU, images sharing a source size in one launch); the host decode of the next
+    batch runs in a background thread."""
+
+    def __iter__(self):
+        ds = self.dataset
+        batches = ([ds.paths[j] for j in idx] for idx in self._index_batches())
+        box = {}
+
+        def stage(paths):
+            try:
+                box["staged"] = stage_images(paths)
+            except BaseException as e:  # re-raised on the consumer side
+                box["error"] = e
+
+        yield from _prefetched(batches, stage, box, lambda st: prepare_images(st, ds.resolution, self.device))
+
+
+def _prefetched(batches, stage, box, finish):
+    nxt = next(batches, None)
+    worker = None
+    if nxt is not None:
+        worker = threading.Thread(target=stage, args=(nxt,))
+        worker.start()
+    while worker is not None:
+        worker.join()
+        if "error" in box:
+            raise box.pop("error")
+        staged = box.pop("staged")
+        nxt = next(batches, None)
+        worker = None
+        if nxt is not None:
+            worker = threading.Thread(target=stage, args=(nxt,))
+            worker.start()
+        yield finish(staged)
+
+
+class FramePairLoader(_ShardedLoader):
+    """`DataLoader(dataset, batch_size, shuffle)` replacement (RC/train_single/train_candy.py:34-39):
+    yields device batches `(img1, img2, flow_into_past, mask)`; the host decode / PFM read of the
+    next batch runs in a background thread while the current batch is on the GPU.  rank /
+    world_size (default: torch.distributed's when initialised): DP sharding as _ShardedLoader."""
+
+    def _batches(self):
+        for idx in self._index_batches():
             yield [self.dataset.entries(j) for j in idx]
 
     def __iter__(self):
         ds = self.dataset
         res, fn = ds.resolution, ds.frame_num
-        batches = self._batches()
         box = {}
 
         def stage(entries):
@@ -346,19 +423,4 @@ class FramePairLoader:
             except BaseException as e:  # re-raised on the consumer side
                 box["error"] = e
 
-        nxt = next(batches, None)
-        worker = None
-        if nxt is not None:
-            worker = threading.Thread(target=stage, args=(nxt,))
-            worker.start()
-        while worker is not None:
-            worker.join()
-            if "error" in box:
-                raise box.pop("error")
-            staged = box.pop("staged")
-            nxt = next(batches, None)
-            worker = None
-            if nxt is not None:
-                worker = threading.Thread(target=stage, args=(nxt,))
-                worker.start()
-            yield prepare_staged(staged, res, fn, self.device)
+        yield from _prefetched(self._batches(), stage, box, lambda st: prepare_staged(st, res, fn, self.device))

@@ -5,6 +5,15 @@ Semantics per step are the reference loop body's:
   FTL (feature-level masked temporal, train_candy.py:91-106), OTL (output-level, :109-123),
   content (relu3_3 MSE, :126-129), style (Gram MSE over 4 layers, :132-138), TV (:141-145),
   backward, Adam(lr=1e-3) step.
+The reference's clones of that loop body are the same step with a different loss-term set
+(`terms`) and weights, selected by name with `ReCoNetTrainer.for_script(...)`:
+  train_candy / train_starry-night  FTL OTL CL SL RL   frame pairs
+  train_Flow_noFTL                  OTL CL SL RL       frame pairs (train_Flow_noFTL.py:124-125)
+  train_multiple/train_Flow         FTL OTL CL SL RL   frame pairs of input_frame_num=4 stacked
+                                                       frames; VGG sees the last 3 channels
+                                                       (train_Flow.py:58-60,83-84)
+  train_coco2014                    CL SL              single images (train_coco2014.py:65-90):
+                                                       content + style only, no TV, BETA 1e10
 Batching choices that do not change the arithmetic:
   * both frames of a pair go through the stylizer / VGG as ONE batch of 2B (InstanceNorm is
     per sample, so this is the reference's two passes fused);
@@ -21,36 +30,71 @@ import torch
 
 from .. import ops
 from ._flat import FlatParams
-from .dist import allreduce_grads, world_info
+from .dist import GradBuckets, broadcast_params, world_info
 
 LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
 # RC/train_single/train_Flow_SD{1,2}.py:24-29
 SD_LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=1e10, GAMMA=1e-2, LAMBDA_F=1e11, LAMBDA_O=1e7)
+ALL_TERMS = ("FTL", "OTL", "CL", "SL", "RL")
+
+# the reference's training scripts: (loss terms, weight overrides, single-image batches)
+SCRIPTS = {
+    "train_candy": (ALL_TERMS, {}, False),                                    # train_candy.py:23-28,148
+    "train_starry-night": (ALL_TERMS, {"BETA": 1e11}, False),                 # train_starry-night.py:24
+    "train_Flow_noFTL": (("OTL", "CL", "SL", "RL"), {"BETA": 1e10}, False),  # train_Flow_noFTL.py:24,125
+    "train_Flow": (ALL_TERMS, {"BETA": 1e10}, False),                         # train_multiple/train_Flow.py:22-25,148
+    "train_coco2014": (("CL", "SL"), {"BETA": 1e10}, True),                   # train_coco2014.py:23-24,86
+}
 
 
 class ReCoNetTrainer:
     def __init__(self, model, vgg, style, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weights=None, temporal=True,
-                 process_group=None, teacher=None, sd_index=(0, 0)):
+                 process_group=None, teacher=None, sd_index=(0, 0), terms=None, single=False):
         """model: ReCoNet / ReCoNetSD1 / ReCoNetSD2 (feature map and styled image are its last two
         outputs).  teacher + sd_index=(teacher output, student output): the distillation trainers
         (train_Flow_SD{1,2}.py), whose symmetric distillation term SDL is reported but, as in the
-        reference, not part of the optimised loss."""
+        reference, not part of the optimised loss.
+        terms: the loss terms summed into the optimised loss (subset of FTL OTL CL SL RL; default
+        all, or CL SL RL with temporal=False).  single: batches are single images [B, C, H, W]
+        (train_coco2014) instead of frame pairs [2, B, C, H, W]; only CL / SL / RL apply."""
         self.model = model
         self.teacher = teacher
         self.sd_index = sd_index
         self.vgg = vgg
         self.w = dict(LOSS_WEIGHTS if weights is None else weights)
-        self.temporal = temporal
+        if terms is None:
+            terms = ALL_TERMS if temporal and not single else ("CL", "SL", "RL")
+        unknown = set(terms) - set(ALL_TERMS)
+        if unknown or not terms:
+            raise ValueError(f"loss terms must be a non-empty subset of {ALL_TERMS}, got {tuple(terms)}")
+        if single and set(terms) & {"FTL", "OTL"}:
+            raise ValueError("single-image batches have no temporal terms (FTL / OTL need frame pairs)")
+        self.terms = tuple(t for t in ALL_TERMS if t in terms)
+        self.single = single
+        self.temporal = bool(set(self.terms) & {"FTL", "OTL"})
         self.lr, self.betas, self.eps = lr, betas, eps
         self.flat = FlatParams(model)
         self.step_count = 0
         self.pg = process_group
         self.rank, self.world = world_info(process_group)
+        # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
+        broadcast_params(self.flat.p, process_group)
+        self.dp = GradBuckets(model, self.flat, process_group)
         dev = self.flat.p.device
         self.chscale_cache = {}
         with torch.no_grad():
             feats = vgg(ops.VggNormalizeFn.apply(style.to(dev)))
             self.style_grams = [ops.gram_matrix(f) for f in feats]
+
+    @classmethod
+    def for_script(cls, script, model, vgg, style, **kw):
+        """The trainer of one of the reference's training scripts (SCRIPTS): its loss terms, its
+        weights (LOSS_WEIGHTS with the script's overrides) and its batch kind."""
+        terms, over, single = SCRIPTS[script]
+        w = dict(LOSS_WEIGHTS)
+        w.update(over)
+        w.update(kw.pop("weights", None) or {})
+        return cls(model, vgg, style, weights=w, terms=terms, single=single, **kw)
 
     def _chscale(self, Hf, Wf, H, W, dev):
         key = (Hf, Wf, H, W)
@@ -58,11 +102,22 @@ class ReCoNetTrainer:
             self.chscale_cache[key] = torch.tensor([float(Wf) / W, float(Hf) / H], dtype=torch.float32, device=dev)
         return self.chscale_cache[key]
 
-    def losses(self, frames, flow, mask):
-        """frames: [2, B, C, H, W] (img1 = frames[0], img2 = frames[1]); returns dict of 0-d tensors."""
+    def losses(self, frames, flow=None, mask=None):
+        """frames: [2, B, C, H, W] frame pairs (img1 = frames[0], img2 = frames[1]), or [B, C, H, W]
+        single images (single=True); returns dict of 0-d tensors."""
         w = self.w
-        _, B, C, H, W = frames.shape
-        x = frames.reshape(2 * B, C, H, W)
+        if self.single:
+            if frames.dim() != 4:
+                raise ValueError(f"single-image trainer: expected [B, C, H, W], got {tuple(frames.shape)}")
+            B, C, H, W = frames.shape
+            x, nf = frames, 1
+        else:
+            if frames.dim() != 5 or frames.shape[0] != 2:
+                raise ValueError(f"frame-pair trainer: expected [2, B, C, H, W], got {tuple(frames.shape)}")
+            _, B, C, H, W = frames.shape
+            x, nf = frames.reshape(2 * B, C, H, W), 2
+            if self.temporal and (flow is None or mask is None):
+                raise ValueError("the temporal terms need flow and mask")
         mout = self.model(x)
         fmap, styled = mout[-2], mout[-1]
         s_n = ops.VggNormalizeFn.apply(styled)
@@ -75,40 +130,43 @@ class ReCoNetTrainer:
             upto = getattr(self.vgg, "features_upto", None)
             cf = upto(i_n, 3) if upto is not None else self.vgg(i_n)
         out = {}
-        if self.temporal:
+        if "FTL" in self.terms:
             Hf, Wf = fmap.shape[2:]
             fflow = ops.resize_bilinear(flow, (Hf, Wf), chscale=self._chscale(Hf, Wf, H, W, flow.device))
             warped_f = ops.warp(fmap[:B], fflow)
             fmask = ops.resize_bilinear(mask.unsqueeze(1), (Hf, Wf), binarize=True)
             out["FTL"] = ops.feature_temporal_loss(fmap[B:], warped_f, fmask, w["LAMBDA_F"])
+        if "OTL" in self.terms:
             warped_s = ops.warp(s_n[:B], flow)
             with torch.no_grad():
                 warped_i = ops.warp(i_n[:B], flow)
             out["OTL"] = ops.output_temporal_loss(s_n[B:], warped_s, i_n[B:], warped_i, mask, w["LAMBDA_O"])
-        out["CL"] = ops.mse(sf[2], cf[2], 2.0 * w["ALPHA"])
+        # mean over the nf*B batch x nf = the reference's sum of nf per-frame means
+        out["CL"] = ops.mse(sf[2], cf[2], nf * w["ALPHA"])
         sl = None
         for f, gs in zip(sf, self.style_grams):
-            term = ops.mse(ops.gram_matrix(f), gs, 2.0 * w["BETA"])
+            term = ops.mse(ops.gram_matrix(f), gs, nf * w["BETA"])
             sl = term if sl is None else sl + term
         out["SL"] = sl
-        out["RL"] = ops.tv_loss(s_n, w["GAMMA"])
+        if "RL" in self.terms:
+            out["RL"] = ops.tv_loss(s_n, w["GAMMA"])
         total = None
-        for k in ("FTL", "OTL", "CL", "SL", "RL"):
-            if k in out:
-                total = out[k] if total is None else total + out[k]
+        for k in self.terms:
+            total = out[k] if total is None else total + out[k]
         out["loss"] = total
         if self.teacher is not None:
             ti, si = self.sd_index
             with torch.no_grad():
                 # mean over the 2B batch = (mse(t1, s1) + mse(t2, s2)) / 2
-                out["SDL"] = ops.mse(self.teacher(x)[ti], mout[si].detach(), 2.0 * 0.01 * w["BETA"])
+                out["SDL"] = ops.mse(self.teacher(x)[ti], mout[si].detach(), nf * 0.01 * w["BETA"])
         return out
 
-    def step(self, frames, flow, mask):
+    def step(self, frames, flow=None, mask=None):
         self.flat.zero_grad()
+        self.dp.begin()
         out = self.losses(frames, flow, mask)
         out["loss"].backward()
-        gscale = allreduce_grads(self.flat.g, self.pg)
+        gscale = self.dp.finish()
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}

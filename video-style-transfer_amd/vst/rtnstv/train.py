@@ -14,7 +14,7 @@ import torch
 
 from .. import ops
 from ..reconet._flat import FlatParams
-from ..reconet.dist import allreduce_grads, world_info
+from ..reconet.dist import GradBuckets, broadcast_params, world_info
 
 # RT/train.py:28-31
 LOSS_WEIGHTS = dict(ALPHA=1e7, BETA=5e7, GAMMA=5e-1, LAMBDA=1e6)
@@ -29,6 +29,9 @@ class RTNSTVTrainer:
         self.step_count = 0
         self.pg = process_group
         self.rank, self.world = world_info(process_group)
+        # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
+        broadcast_params(self.flat.p, process_group)
+        self.dp = GradBuckets(model, self.flat, process_group)
         dev = self.flat.p.device
         with torch.no_grad():
             feats = vgg(style.to(dev))
@@ -58,9 +61,10 @@ class RTNSTVTrainer:
 
     def step(self, frames, flow, mask):
         self.flat.zero_grad()
+        self.dp.begin()
         out = self.losses(frames, flow, mask)
         out["loss"].backward()
-        gscale = allreduce_grads(self.flat.g, self.pg)
+        gscale = self.dp.finish()
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}
