@@ -109,19 +109,6 @@ def gemm_mode(request):
     ops.use_policy(old)
 
 
-@pytest.fixture(params=["f32", "bf16x6"])
-def step_policy(request):
-    """The fp32-class GEMM policies a whole training step must pass the reference's golden bar
-    under: exact fp32 MFMA (the library default) and bf16x6 everywhere (bench.py's headline)."""
-    from vst import ops
-
-    ops.gemm_role("fwd")
-    old = ops.POLICY_NAME[0]
-    ops.use_policy(request.param)
-    yield request.param
-    ops.use_policy(old)
-
-
 # max|err| / max|ref| per mode: fp32 MFMA and bf16x3 (per-product error <= ~2^-16) hold the
 # 1e-4 op bar; single bf16 (2^-8 per product) is the reduced-precision path of config 5, where
 # ReLU decisions flip near zero, so it is held to ||err|| / ||ref|| instead
