@@ -283,6 +283,20 @@ int vst_scale_cols(const float* x, const float* c, float* y, int N, int R, int P
 int vst_attn_dkn(const float* K, const float* Y, const float* qt, const float* ks, float* dkn, int N, int d, int Ns,
                  void* stream);
 
+/* Cosine attention in linear form (A = diag(1/rowsum) (Qhat^T Khat + 1) never formed, see
+ * video-style-transfer_amd/vst/adaattn/attention.py):
+ * vst_outer_axpy: out[n][m][p] = (x[n][m][p] + alpha * u[n][m] * v[n][p]) * w[n][p]  (u, v, w may be
+ *   NULL: no term / 1 / 1; out may alias x);
+ * vst_sum_repeats: out[i] = sum_{r < R} x[r * per + i] (gradient of an operand broadcast over R
+ *   repeats of a batch: the style side shared by both content frames);
+ * vst_normalize_cols_bwd: out = (dxh - xh * t[n][p]) * s[n][p], the adjoint of column normalisation
+ *   xh = x / ||x|| (t = sum_c xh dxh, s = 1 / ||x||). */
+int vst_outer_axpy(const float* x, const float* u, const float* v, const float* w, float alpha, float* out, int N, int M,
+                   long P, void* stream);
+int vst_sum_repeats(const float* x, float* out, int R, long per, void* stream);
+int vst_normalize_cols_bwd(const float* xh, const float* dxh, const float* t, const float* s, float* out, int N, int C,
+                           long P, void* stream);
+
 /* dst[n][0:per] = src[n][0:per] with batch strides (channel concat / split, AA/network.py:87) */
 int vst_copy_planes(const float* src, long src_bs, float* dst, long dst_bs, int N, long per, void* stream);
 /* D = 1 - G / (un_i vn_j + 1e-6) (cosine_distance forward) */

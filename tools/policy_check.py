@@ -56,6 +56,11 @@ def margin(tag):
 
 POLICIES = {
     "f32": ("f32", {}),
+    "bf16x6/wgrad-f32": ("bf16x6", {"wgrad": "f32"}),
+    "bf16x6/dgrad-f32": ("bf16x6", {"dgrad": "f32"}),
+    "bf16x6/stylizer-f32": ("bf16x6", {"stylizer.fwd": "f32", "stylizer.fwd_img": "f32"}),
+    "bf16x6/fwd-f32": ("bf16x6", {"fwd": "f32", "fwd_img": "f32"}),
+    "bf16x6/img-f32": ("bf16x6", {"fwd_img": "f32", "stylizer.fwd_img": "f32"}),
     "bf16x3": ("bf16x3", {}),
     "bf16x6": ("bf16x6", {}),
     "bf16x3/stylizer-f32": ("bf16x3", {"stylizer.fwd": "f32", "stylizer.fwd_img": "f32"}),

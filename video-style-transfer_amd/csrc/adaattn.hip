@@ -34,7 +34,7 @@ __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restric
   int m = (int)(t % Mpad), k = (int)(t / Mpad);
   float v = 0.f;
   if (m < M && k < K) v = transpose ? x[b * x_bs + (long)m * K + k] : x[b * x_bs + (long)k * M + m];
-  apack_store(out + b * per * (bsplit == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
+  apack_store(out + b * per * ((bsplit & 3) == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
 }
 
 // out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
@@ -678,3 +678,65 @@ int vst_attn_dkn(const float* K, const float* Y, const float* qt, const float* k
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Cosine attention in linear form (vst/adaattn/attention.py LinearCosineAttnFn): the rank-1
+// column/row updates and the column-normalisation adjoint around its d x 2dv GEMMs.
+namespace {
+// out[n][m][p] = (x[n][m][p] + alpha * u[n][m] * (v ? v[n][p] : 1)) * (w ? w[n][p] : 1)
+__global__ void outer_axpy_kernel(const float* __restrict__ x, const float* __restrict__ u,
+                                  const float* __restrict__ v, const float* __restrict__ w, float alpha, float* out,
+                                  int M, long P, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const long p = idx % P, nm = idx / P;
+  const long n = nm / M;
+  float a = x[idx];
+  if (u) a += alpha * u[nm] * (v ? v[n * P + p] : 1.0f);
+  if (w) a *= w[n * P + p];
+  out[idx] = a;
+}
+
+// out[i] = sum_{r < R} x[r * per + i]  (gradients of operands broadcast over R repeats of a batch)
+__global__ void sum_repeats_kernel(const float* __restrict__ x, float* __restrict__ out, int R, long per) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += x[r * per + i];
+  out[i] = s;
+}
+
+// out[n][c][p] = (dxh[n][c][p] - xh[n][c][p] * t[n][p]) * s[n][p]
+// (adjoint of xh = x / ||x||_col with t = sum_c xh dxh and s = 1 / ||x||_col)
+__global__ void normalize_cols_bwd_kernel(const float* __restrict__ xh, const float* __restrict__ dxh,
+                                          const float* __restrict__ t, const float* __restrict__ s,
+                                          float* __restrict__ out, int C, long P, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const long p = idx % P, n = idx / P / C;
+  const long np = n * P + p;
+  out[idx] = (dxh[idx] - xh[idx] * t[np]) * s[np];
+}
+}  // namespace
+
+extern "C" int vst_outer_axpy(const float* x, const float* u, const float* v, const float* w, float alpha, float* out,
+                              int N, int M, long P, void* stream) {
+  VST_CHECK_ARG(x && out && N > 0 && M > 0 && P > 0);
+  const long total = (long)N * M * P;
+  outer_axpy_kernel<<<ceil_div(total, RT), RT, 0, (hipStream_t)stream>>>(x, u, v, w, alpha, out, M, P, total);
+  return vst_launch_status();
+}
+
+extern "C" int vst_sum_repeats(const float* x, float* out, int R, long per, void* stream) {
+  VST_CHECK_ARG(x && out && R > 0 && per > 0);
+  sum_repeats_kernel<<<ceil_div(per, RT), RT, 0, (hipStream_t)stream>>>(x, out, R, per);
+  return vst_launch_status();
+}
+
+extern "C" int vst_normalize_cols_bwd(const float* xh, const float* dxh, const float* t, const float* s, float* out,
+                                      int N, int C, long P, void* stream) {
+  VST_CHECK_ARG(xh && dxh && t && s && out && N > 0 && C > 0 && P > 0);
+  const long total = (long)N * C * P;
+  normalize_cols_bwd_kernel<<<ceil_div(total, RT), RT, 0, (hipStream_t)stream>>>(xh, dxh, t, s, out, C, P, total);
+  return vst_launch_status();
+}

@@ -40,14 +40,14 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
   float v = 0.f;
   if (split_kh) {
     if (m < Cout * KH && k < KW * Cin) {
-      int co = m / KH, kh = m % KH, kw = k / Cin, ci = k % Cin;
+      const int co = m / KH, kh = m % KH, kw = k / Cin, ci = k % Cin;
       v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
     }
   } else {
     int Ck = transposed ? Cout : Cin;  // channel count inside the k index
     int Mm = transposed ? Cin : Cout;
     if (m < Mm && k < KH * KW * Ck) {
-      int tap = k / Ck, c = k % Ck;
+      const int tap = k / Ck, c = k % Ck;
       int kh = tap / KW, kw = tap % KW;
       int co = transposed ? c : m, ci = transposed ? m : c;
       v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
@@ -246,6 +246,7 @@ int vst_version(void) { return 200; }
 #endif
 const char* vst_build_id(void) { return VST_BUILD_ID; }
 
+
 const char* vst_strerror(int code) {
   if (code == VST_OK) return "success";
   if (code == VST_EINVAL) return "vst: invalid argument";
@@ -276,6 +277,14 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
 }
 
 }  // extern "C"
+
+// floats of one packed A operand of an M x K GEMM in `mode` (vst_conv_pack_dims padding; bf16x6
+// blocks are 1.5x): per-image packs must be at least this far apart
+static long apack_floats(int M, int K, int mode) {
+  const int bm = cfg_bm(select_cfg(M));
+  const long f = (long)((M + bm - 1) / bm * bm) * ((K + BK - 1) / BK * BK);
+  return mode == VST_GEMM_BF16X6 ? f * 3 / 2 : f;
+}
 
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
                             int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
@@ -361,6 +370,7 @@ int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, 
   VST_CHECK_ARG(!((epi & EPI_BIAS) && !bias) && !((epi & EPI_MASK) && !mask));
   if (gmode == GM_REFLECT) VST_CHECK_ARG(pad < Hs * up && pad_x < Ws * up);
   VST_CHECK_ARG(pad >= 0 && pad_x >= 0);
+  VST_CHECK_ARG(a_batch_stride == 0 || a_batch_stride >= apack_floats(M, K, mode));
   return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad_x,
                           up, epi, a_batch_stride, aux, gmask, mode, stream);
 }
@@ -371,6 +381,7 @@ int vst_attn_gemm(const float* src, const float* apack, float* out, int N, int K
                   const float* ra, const float* rb, const float* rd, const float* cg, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(src && apack && out && rb && cg && N > 0 && K > 0 && P > 0 && M > 0);
+  VST_CHECK_ARG(a_batch_stride == 0 || a_batch_stride >= apack_floats(M, K, mode));
   return conv_gemm_launch(src, apack, nullptr, nullptr, out, N, K, 1, P, M, K, 1, P, 1, 1, GM_ZERO, 1, 0, 0, 1,
                           EPI_AFFINE, a_batch_stride, nullptr, nullptr, mode, stream, ra, rb, rd, cg);
 }

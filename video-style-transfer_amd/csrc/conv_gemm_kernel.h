@@ -158,10 +158,21 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   const __amdgpu_buffer_rsrc_t srd = uniform_rsrc(src_n, src_bytes);
   const __amdgpu_buffer_rsrc_t gsrd = uniform_rsrc(GM ? gm_n : src_n, src_bytes);
   const int ntiles = P.Kpad / BK;
+  // A (packed weights) through a buffer descriptor too: per thread a FIXED byte offset inside the
+  // tile (its float4 slot), per tile a scalar offset -- no per-tile VALU address math, and the
+  // threads past a partial tile's last float4 read the out-of-range zero (their store is skipped)
+  // instead of branching around the load
+  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(A, (uint32_t)((long)P.Kpad / BK * P.Mpad * AW * 4));
+  int a_voff[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int idx = tid + i * NT;
+    a_voff[i] = (A_F4 % NT == 0 || idx < A_F4) ? 16 * (AW == 16 ? a_slot(idx) : idx) : OOR;
+  }
 
-  // CFAST tap walk: tiles are loaded in k order, so the (tap, channel) position advances by 16
-  // channels per tile and the gather offset is decoded once per tap (wave-uniform branch), not once
-  // per k-tile
+  // CFAST tap walk: tiles are loaded in k order (tap-major), so the (tap, channel) position
+  // advances by 16 channels per tile and the gather offset is decoded once per tap (wave-uniform
+  // branch), not once per k-tile
   int st_tap = 0, st_c0 = 0, st_vbase = 0;
   bool st_ok = false;
 
@@ -169,13 +180,10 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
   auto load_tile = [&](int t) {
     const int k0 = t * BK;
+    const int a_soff = __builtin_amdgcn_readfirstlane(((t * P.Mpad + m0) * AW) * 4);
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int idx = tid + i * NT;
-      if (A_F4 % NT == 0 || idx < A_F4) {
-        ra[i] = *reinterpret_cast<const f32x4*>(A + ((long)t * P.Mpad + m0) * AW + 4 * (AW == 16 ? a_slot(idx) : idx));
-      }
-    }
+    for (int i = 0; i < A_PER; ++i)
+      ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
     if (CFAST) {
       // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
       // offset per thread per group; out-of-range taps use an offset past the buffer end, which
@@ -189,12 +197,15 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
         st_ok = pvalid && off0 >= 0;
         st_vbase = ((PREC ? brow0 * B_PER : brow0) * plane_i + off0) * 4;
       }
+      // one address VGPR per tile; the thread's B_PER channels differ by a uniform stride, which
+      // goes into the scalar offset (an out-of-range base stays out of range: OOR + the largest
+      // stride does not wrap 32 bits for any plane that fits the 2^31 B descriptor)
       const int vo = st_ok ? st_vbase + st_c0 * plane_i * 4 : OOR;
-      const int vstep = st_ok ? KSTEP * plane_i * 4 : 0;
+      const int sstep = __builtin_amdgcn_readfirstlane(KSTEP * plane_i * 4);
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo + i * vstep, 0, 0));
-        if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo + i * vstep, 0, 0));
+        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
+        if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, i * sstep, 0));
       }
       st_c0 += 16;
       if (st_c0 == P.Cs) {

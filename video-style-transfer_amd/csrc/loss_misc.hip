@@ -207,7 +207,7 @@ __global__ void symmetrize_kernel(const float* __restrict__ g, float* __restrict
     const float* gn = g + n * C * C;
     v = (gn[k * C + m] + gn[m * C + k]) * scale;
   }
-  apack_store(S + n * (long)Kpad * Mpad * (bsplit == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
+  apack_store(S + n * (long)Kpad * Mpad * ((bsplit & 3) == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
 }
 
 // ReLU backward: gx = gy * (y > 0)

@@ -347,6 +347,262 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-tiled weight-gradient GEMM (the path for every KxK conv / Gram / A*B^T whose output rows are
+// a multiple of 16 pixels wide): a k-tile is 16 consecutive pixels of ONE output row, so its row
+// index oy and first column ox0 are block-uniform scalars advanced once per tile.
+//   * each thread owns ONE B column j = (tap, ci) for the whole loop (decoded once) and 8 of the
+//     tile's 16 pixels: per tile it computes one source row (reflect / zero, nearest-x2 shift) and
+//     one base offset, and loads its 8 source elements with immediate offsets (contiguous for
+//     stride 1; stride 2 / upsample 2 have their own straight-line forms; a tile whose 8-pixel
+//     window crosses the left / right border decodes per element);
+//   * A (dY rows) loads are two float4 per (row, 8-pixel half) at a FIXED per-thread offset plus a
+//     per-tile scalar offset;
+//   * both operands are split (per PREC) in registers and stored with one ds_write_b128 per
+//     section; 8 consecutive lanes take 8 consecutive LDS rows, so the 28- / 20-dword row stride
+//     puts them on 8 distinct 4-bank groups (conflict-free).
+struct Wg2Params {
+  const float* a;    // [N][M][HWo]
+  const float* src;  // [N][Cs][Hs][Ws]
+  float* slab;       // [N*S][Mpad][Jpad]
+  int M, Mpad, J, Jpad;
+  int Cs, Hs, Ws, Ho, Wo;
+  int KH, KW, stride, pad, up;
+  int S, chunk;
+};
+
+template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE>
+__global__ __launch_bounds__(NT, MINW) void wgrad2_kernel(Wg2Params P) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int LS = PREC == 3 ? 28 : 20;
+  constexpr int A_TASKS = 2 * BM, A_IT = (A_TASKS + NT - 1) / NT;
+  constexpr int B_TASKS = 2 * BN, B_IT = (B_TASKS + NT - 1) / NT;
+  constexpr int OOR = 0x7ffffff0;
+  static_assert(BK == 16, "16-pixel k-tiles");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int rest = __builtin_amdgcn_readfirstlane(wk / gx), bz = __builtin_amdgcn_readfirstlane(rest / gy);
+  const int j0 = __builtin_amdgcn_readfirstlane((wk - rest * gx) * BN);
+  const int m0 = __builtin_amdgcn_readfirstlane((rest - bz * gy) * BM);
+  const int n = __builtin_amdgcn_readfirstlane(bz / P.S);
+  const int sidx = bz - n * P.S;
+  const int HWo = P.Ho * P.Wo;
+  const int r_begin = sidx * P.chunk;
+  const int r_end = min(HWo, r_begin + P.chunk);
+  const int ntiles = r_end > r_begin ? (r_end - r_begin) / BK : 0;
+  const int plane = P.Hs * P.Ws;
+  const float* a_n = P.a + (long)n * P.M * HWo;
+  const float* src_n = P.src + (long)n * P.Cs * plane;
+  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)((long)P.M * HWo * 4));
+  const __amdgpu_buffer_rsrc_t bsrd = uniform_rsrc(src_n, (uint32_t)((long)P.Cs * plane * 4));
+  const int Hv = P.Hs * P.up, Wv = P.Ws * P.up, sh = P.up - 1;
+
+  // A tasks: (row, half) with 8 consecutive lanes on 8 consecutive rows of one half
+  int a_voff[A_IT], a_row[A_IT], a_half[A_IT];
+#pragma unroll
+  for (int i = 0; i < A_IT; ++i) {
+    const int q = tid + i * NT;
+    a_row[i] = (q & 7) + 8 * (q >> 4);
+    a_half[i] = (q >> 3) & 1;
+    const int m = m0 + a_row[i];
+    a_voff[i] = (q < A_TASKS && m < P.M) ? (m * HWo + 8 * a_half[i]) * 4 : OOR;
+  }
+  // B tasks: column c = q % BN (consecutive lanes -> consecutive columns), half = q / BN
+  int b_col[B_IT], b_half[B_IT], b_kh[B_IT], b_kw[B_IT], b_cbase[B_IT];
+  bool b_ok[B_IT];
+#pragma unroll
+  for (int i = 0; i < B_IT; ++i) {
+    const int q = tid + i * NT;
+    b_col[i] = q % BN;
+    b_half[i] = q / BN;
+    const int j = j0 + b_col[i];
+    b_ok[i] = q < B_TASKS && j < P.J;
+    const int jj = b_ok[i] ? j : 0;
+    const int tap = jj / P.Cs, ci = jj - tap * P.Cs;
+    b_kh[i] = tap / P.KW;
+    b_kw[i] = tap - b_kh[i] * P.KW;
+    b_cbase[i] = ci * plane;
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  f32x4 ra[A_IT][2];
+  float rb[B_IT][8];
+  // tile position (scalar): output row oy, first column ox0
+  int t_oy = __builtin_amdgcn_readfirstlane(r_begin / P.Wo);
+  int t_ox = __builtin_amdgcn_readfirstlane(r_begin - t_oy * P.Wo);
+
+  auto load_tile = [&](int t) {
+    const int soff = __builtin_amdgcn_readfirstlane((r_begin + t * BK) * 4);
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], soff, 0));
+      ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i] + 16, soff, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      int yv = t_oy * P.stride + b_kh[i] - P.pad;
+      bool ok = b_ok[i];
+      if (GMODE == 0) {
+        yv = abs(yv);
+        yv = min(yv, 2 * Hv - 2 - yv);
+      } else {
+        ok = ok && yv >= 0 && yv < Hv;
+      }
+      const int rowoff = b_cbase[i] + (yv >> sh) * P.Ws;
+      const int xv0 = (t_ox + 8 * b_half[i]) * P.stride + b_kw[i] - P.pad;
+      const int xv7 = xv0 + 7 * P.stride;
+      if (xv0 >= 0 && xv7 < Wv) {  // interior window: one base, immediate offsets
+        if (P.up == 2) {           // nearest x2: 8 virtual columns over 4-5 source columns
+          const int vo = ok ? (rowoff + (xv0 >> 1)) * 4 : OOR;
+          float s[5];
+#pragma unroll
+          for (int e = 0; e < 5; ++e) s[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 4 * e, 0, 0));
+          const bool odd = xv0 & 1;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rb[i][e] = odd ? s[(e + 1) >> 1] : s[e >> 1];
+        } else if (P.stride == 2) {
+          const int vo = ok ? (rowoff + xv0) * 4 : OOR;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 8 * e, 0, 0));
+        } else {
+          const int vo = ok ? (rowoff + xv0) * 4 : OOR;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 4 * e, 0, 0));
+        }
+      } else {  // border window: per element
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          int xv = xv0 + e * P.stride;
+          bool oke = ok;
+          if (GMODE == 0) {
+            xv = abs(xv);
+            xv = min(xv, 2 * Wv - 2 - xv);
+          } else {
+            oke = oke && xv >= 0 && xv < Wv;
+          }
+          const int vo = oke ? (rowoff + (xv >> sh)) * 4 : OOR;
+          rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
+        }
+      }
+    }
+  };
+
+  // 8 consecutive k (pixels 8*half .. 8*half+7) of one LDS row, in the layout of PREC
+  auto store8 = [&](float* row, int half, const float* v) {
+    if constexpr (PREC == 0) {  // fp32 [hi][s]: k = 2s + hi -> even k at dwords 4*half.., odd at 8 + 4*half..
+      *reinterpret_cast<f32x4*>(row + 4 * half) = f32x4{v[0], v[2], v[4], v[6]};
+      *reinterpret_cast<f32x4*>(row + 8 + 4 * half) = f32x4{v[1], v[3], v[5], v[7]};
+    } else if constexpr (PREC == 3) {
+      uint32_t h[4], md[4], l[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split3_bf16x2(v[2 * q], v[2 * q + 1], h[q], md[q], l[q]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(row) + 4 * half;
+      *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+      *reinterpret_cast<u32x4*>(d + 8) = u32x4{md[0], md[1], md[2], md[3]};
+      *reinterpret_cast<u32x4*>(d + 16) = u32x4{l[0], l[1], l[2], l[3]};
+    } else {
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split_bf16x2(v[2 * q], v[2 * q + 1], h[q], l[q]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(row) + 4 * half;
+      *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+      if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      if (A_TASKS % NT == 0 || tid + i * NT < A_TASKS) {
+        const float v[8] = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
+                            ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
+        store8(&As[buf][a_row[i]][0], a_half[i], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i)
+      if (B_TASKS % NT == 0 || tid + i * NT < B_TASKS) store8(&Bs[buf][b_col[i]][0], b_half[i], rb[i]);
+  };
+  auto advance = [&]() {
+    t_ox += BK;
+    if (t_ox == P.Wo) {
+      t_ox = 0;
+      ++t_oy;
+    }
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    advance();
+    store_tile(0);
+  }
+  __syncthreads();
+  const int lo = lane & 31, hi = lane >> 5;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) {
+      load_tile(t + 1);
+      advance();
+    }
+    if constexpr (PREC == 3) {
+      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else if constexpr (PREC != 0) {
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+    } else {
+      f32x4 a[TM][2], b[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        a[i][0] = *reinterpret_cast<const f32x4*>(r);
+        a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        b[j][0] = *reinterpret_cast<const f32x4*>(r);
+        b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < BK / 2; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  float* slab = P.slab + (long)bz * P.Mpad * P.Jpad;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int jj = j0 + (wn * TN + j) * 32 + lo;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        slab[(long)m * P.Jpad + jj] = acc[i][j][r];
+      }
+  }
+}
+
 enum { W32 = 0, W64, W96, W128, W192 };
 static int wsel(int M) {
   if (M <= 32) return W32;
@@ -465,9 +721,64 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
   return best;
 }
 
+template <int PR, int GMD>
+static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
+  switch (c) {
+    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
+  }
+}
+
+template <int GMD>
+static void launch_wg2(int c, dim3 g, int mode, hipStream_t st, const Wg2Params& P) {
+  switch (mode) {
+    case VST_GEMM_F32: launch_wg2_p<0, GMD>(c, g, st, P); break;
+    case VST_GEMM_BF16: launch_wg2_p<2, GMD>(c, g, st, P); break;
+    case VST_GEMM_BF16X6: launch_wg2_p<3, GMD>(c, g, st, P); break;
+    default: launch_wg2_p<1, GMD>(c, g, st, P); break;
+  }
+}
+
+// row-tiled kernel applies: plain (not row-split) gather, output rows a multiple of 16 wide, and
+// every source offset within the 2^31 B buffer range
+static bool wg2_ok(int asplit, int Wo) {
+  static const bool off = getenv("VST_WGRAD2") && atoi(getenv("VST_WGRAD2")) == 0;  // A/B switch
+  return !off && !asplit && Wo % BK == 0;
+}
+
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
                   int KH, int KW, int gmode, int stride, int pad, int up, int S, int asplit, int Ha, int mode,
                   hipStream_t st) {
+  if (wg2_ok(asplit, Wo)) {
+    Wg2Params Q;
+    Q.a = a;
+    Q.src = src;
+    Q.slab = slab;
+    Q.M = M;
+    const int c = wsel(M);
+    Q.Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
+    Q.J = KH * KW * Cs;
+    Q.Jpad = (Q.J + WBN - 1) / WBN * WBN;
+    Q.Cs = Cs;
+    Q.Hs = Hs;
+    Q.Ws = Ws;
+    Q.Ho = Ho;
+    Q.Wo = Wo;
+    Q.KH = KH;
+    Q.KW = KW;
+    Q.stride = stride;
+    Q.pad = pad;
+    Q.up = up;
+    Q.S = S;
+    Q.chunk = ((Ho * Wo + S - 1) / S + BK - 1) / BK * BK;
+    dim3 g(Q.Jpad / WBN, Q.Mpad / wbm(c), N * S);
+    if (gmode == 0) launch_wg2<0>(c, g, mode, st, Q);
+    else launch_wg2<1>(c, g, mode, st, Q);
+    return vst_launch_status();
+  }
   WgParams P;
   P.a = a;
   P.src = src;

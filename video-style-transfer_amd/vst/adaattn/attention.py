@@ -210,7 +210,145 @@ class AdaAttnFn(Function):
         return dQ, dK, dV, None, None
 
 
+# ---------------------------------------------------------------------------------------------
+# Cosine attention in linear form.  CosineSimilarity (AA/network.py:111-125) is
+#   A_ij = s_ij / sum_j s_ij,  s_ij = qh_i . kh_j + 1,  qh = q / ||q||, kh = k / ||k||
+# so with U = [V; V^2] (2dv x Ns) the two moments AdaAttN needs (AA/network.py:209-213) are
+#   [M; E2]_i = sum_j A_ij U_j = (G^T qh_i + us) / rs_i,   G = Kh U^T (d x 2dv),  us = sum_j U_j,
+#   rs_i = qh_i . ksum + Ns,  ksum = sum_j kh_j
+# -- an exact re-association of the reference's bmm(A, V) / bmm(A, V**2): the Nc x Ns matrix A is
+# never formed (HBM O(N d) instead of O(Nc Ns)) and the products cost 2 Ns d 2dv + 2 Nc d 2dv
+# instead of 2 Nc Ns (d + 2dv) FLOPs (17x fewer at 256x512 level 3, 4x more per 2x resolution
+# instead of 16x).  The backward is the same algebra transposed (all GEMMs of d x 2dv operands):
+#   dRh = dMV / rs;  te = rs^-1 sum_v dMV MV (= -d rs);  dqh = G dRh - ksum te;  dG = Qh dRh^T;
+#   dus = sum_i dRh;  dksum = -Qh te;  dkh = dG U + dksum;  dU = dG^T Kh + dus;
+#   dV = dU[:dv] + 2 V dU[dv:];  dq = (dqh - qh (qh . dqh)) / ||q||  (likewise k).
+# The style side (K, V) may carry fewer images than Q: Q image n attends to K / V image n % Nk
+# (the train_video step's two content frames share one style encoding), and its gradients are
+# summed over the repeats.
+def _repeat(x, r):
+    """x [Nk, ...] repeated r times along the batch (plane-copy kernel); x itself when r == 1."""
+    if r == 1:
+        return x
+    out = torch.empty((r * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=torch.float32)
+    for i in range(r):
+        ops.copy_into(x, out[i * x.shape[0]:(i + 1) * x.shape[0]])
+    return out
+
+
+def _sum_repeats(x, r):
+    if r == 1:
+        return x
+    per = x[: x.shape[0] // r].numel()
+    out = torch.empty((x.shape[0] // r,) + tuple(x.shape[1:]), device=x.device, dtype=torch.float32)
+    lib.vst_sum_repeats(ptr(x), ptr(out), r, per, stream())
+    return out
+
+
+def _axpy(x, u=None, v=None, w=None, alpha=1.0, out=None):
+    """out[n][m][p] = (x + alpha u[n][m] v[n][p]) w[n][p] over x viewed [N][M][P]."""
+    N, M = x.shape[:2]
+    P = x[0, 0].numel()
+    out = x if out is None else out
+    lib.vst_outer_axpy(ptr(x), ptr(u), ptr(v), ptr(w), float(alpha), ptr(out), N, M, P, stream())
+    return out
+
+
+def _normalized(x, nrm_inv):
+    return _axpy(x, w=nrm_inv, out=_empty(x.shape, x))
+
+
+def _normalize_bwd(xh, dxh, nrm_inv):
+    N, C, P = xh.shape
+    t = channel_dot(xh, y=dxh)
+    out = _empty(xh.shape, xh)
+    lib.vst_normalize_cols_bwd(ptr(xh), ptr(dxh), ptr(t), ptr(nrm_inv), ptr(out), N, C, P, stream())
+    return out
+
+
+def _recip(x):
+    y = _empty(x.shape, x)
+    lib.vst_reciprocal(ptr(x), ptr(y), x.numel(), stream())
+    return y
+
+
+class LinearCosineAttnFn(Function):
+    """out = sqrt(clamp(E2 - M^2, 1e-6)) * cn + M with [M; E2] the cosine-attention moments in
+    linear form (see above); gradients for Q, K, V."""
+
+    @staticmethod
+    def forward(ctx, Q, K, V, cn):
+        Nq, d, h, w = Q.shape
+        Nk, _, hs, ws = K.shape
+        dv = V.shape[1]
+        Nc, Ns = h * w, hs * ws
+        if (K.shape[1] != d or V.shape != (Nk, dv, hs, ws) or cn.shape != (Nq, dv, h, w) or Nq % Nk):
+            raise VstError(f"adaattn: Q{tuple(Q.shape)} K{tuple(K.shape)} V{tuple(V.shape)} c{tuple(cn.shape)}")
+        Q, K, V, cn = (ops._check(t, "adaattn operand", 4) for t in (Q, K, V, cn))
+        r = Nq // Nk
+        role = "attn_" + COSINE
+        Qm, Km = Q.view(Nq, d, Nc), K.view(Nk, d, Ns)
+        qn = channel_norm(Qm)
+        qs, ks = _recip(qn), _recip(channel_norm(Km))
+        Qh, Kh = _normalized(Qm, qs), _normalized(Km, ks)
+        U = _empty((Nk, 2 * dv, Ns), V)
+        lib.vst_square_concat(ptr(V), ptr(U), Nk, dv * Ns, stream())
+        G = gemm_abt(Kh, U, role=role)                       # [Nk][d][2dv]
+        ksum, us = plane_dot(Kh), plane_dot(U)              # [Nk][d], [Nk][2dv]
+        Gr, ksr, usr = _repeat(G, r), _repeat(ksum, r), _repeat(us, r)
+        qk = channel_dot(Qm, v=ksr)                         # q . ksum  [Nq][Nc]
+        rinv = _empty(qk.shape, qk)
+        lib.vst_attn_fwd_rows(ptr(qk), ptr(qn), ptr(_empty(qk.shape, qk)), ptr(rinv), qk.numel(), Ns,
+                              stream())                     # 1 / rs = 1 / (q . ksum / ||q|| + Ns)
+        MV = bmm_at_b(Gr, 2 * dv, d, False, Qh, Nc, role=role)  # G^T qh  [Nq][2dv][Nc]
+        _axpy(MV, u=usr, w=rinv)                            # (G^T qh + us) / rs
+        out = _empty((Nq, dv, h, w), V)
+        lib.vst_adaattn_out(ptr(MV), ptr(cn), ptr(out), Nq, dv * Nc, stream())
+        ctx.dims = (Nq, Nk, d, dv, Nc, Ns, (h, w), (hs, ws))
+        if any(ctx.needs_input_grad[:3]):
+            ctx.save_for_backward(V, cn, Qh, Kh, qs, ks, U, Gr, ksr, MV, rinv)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        V, cn, Qh, Kh, qs, ks, U, Gr, ksr, MV, rinv = ctx.saved_tensors
+        Nq, Nk, d, dv, Nc, Ns, hw, hws = ctx.dims
+        r = Nq // Nk
+        role = "attn_" + COSINE
+        if ctx.needs_input_grad[3]:
+            raise VstError("adaattn: gradient w.r.t. the content features (norm_v(c_x)) is not on the reference path")
+        dMV = _empty(MV.shape, MV)
+        lib.vst_adaattn_out_bwd(ptr(dout.contiguous()), ptr(MV), ptr(cn), ptr(dMV), Nq, dv * Nc, stream())
+        te = _axpy(channel_dot(dMV, y=MV).view(Nq, 1, Nc), w=rinv, out=_empty((Nq, 1, Nc), MV)).view(Nq, Nc)
+        dRh = _axpy(dMV, w=rinv)                            # dMV / rs (in place)
+        dG = _sum_repeats(gemm_abt(Qh, dRh, role=role), r)  # [Nk][d][2dv]
+        dQ = dK = dV = None
+        if ctx.needs_input_grad[0]:
+            dQh = bmm_at_b(Gr, d, 2 * dv, True, dRh, Nc, role=role)  # G dRh  [Nq][d][Nc]
+            _axpy(dQh, u=ksr, v=te, alpha=-1.0)
+            dQ = _normalize_bwd(Qh, dQh, qs).view(Nq, d, *hw)
+        if ctx.needs_input_grad[1]:
+            dks = _sum_repeats(plane_dot(Qh, te), r)       # -dksum
+            dKh = bmm_at_b(dG, d, 2 * dv, True, U, Ns, role=role)  # dG U  [Nk][d][Ns]
+            _axpy(dKh, u=dks, alpha=-1.0)
+            dK = _normalize_bwd(Kh, dKh, ks).view(Nk, d, *hws)
+        if ctx.needs_input_grad[2]:
+            dus = _sum_repeats(plane_dot(dRh), r)          # [Nk][2dv]
+            dU = bmm_at_b(dG, 2 * dv, d, False, Kh, Ns, role=role)  # dG^T Kh  [Nk][2dv][Ns]
+            _axpy(dU, u=dus)
+            dV = _empty(V.shape, V)
+            lib.vst_square_concat_bwd(ptr(dU), ptr(V), ptr(dV), Nk, dv * Ns, stream())
+        return dQ, dK, dV, None
+
+
 def adaattn(Q, K, V, cn, activation=COSINE):
+    """AdaAttN attention + modulation (AA/network.py:191-220 after the 1x1 convs).  Cosine: the
+    linear form (no Nc x Ns matrix; K / V may hold a divisor of Q's batch, broadcast over repeats);
+    softmax: the materialised-attention path."""
+    if activation == COSINE:
+        return LinearCosineAttnFn.apply(Q, K, V, cn)
+    if K.shape[0] != Q.shape[0]:
+        raise VstError("adaattn (softmax): Q and K/V batches must match")
     return AdaAttnFn.apply(Q, K, V, cn, activation)
 
 

@@ -58,6 +58,7 @@ class AdaAttNTrainer:
         self.model, self.vgg = model, vgg
         self.w = dict(LOSS_WEIGHTS if weights is None else weights)
         self.lr, self.betas, self.eps = lr, betas, eps
+        self.activation = activation
         self.flat = FlatParams(model)
         dev = self.flat.p.device
         self.noconv = [AdaAttnNoConv(v, q, activation).to(dev).eval()
@@ -84,7 +85,9 @@ class AdaAttNTrainer:
         fc1, fc2, fs = self.encode(c1, c2, s)
         B = next(iter(fc1.values())).shape[0]
         fc12 = _batch_pair(fc1, fc2)
-        fs2 = {k: _cat2(v, v) for k, v in fs.items()}
+        # cosine attention takes the style side once for both content frames (K / V broadcast over
+        # the two halves of the batch: the style 1x1 convs, down-sampling and K U^T run on B images)
+        fs2 = fs if self.activation == "cosine" else {k: _cat2(v, v) for k, v in fs.items()}
         fcs = self.vgg(self.model(fc12, fs2))  # cs1 ++ cs2
         fcs1 = {k: v[:B] for k, v in fcs.items()}
         fcs2 = {k: v[B:] for k, v in fcs.items()}

@@ -689,9 +689,9 @@ class GramFn(Function):
     def backward(ctx, gg):
         (y,) = ctx.saved_tensors
         N, C, H, W = y.shape
+        gemm_role("dgrad")  # before sizing S: the pack layout (and size) is the dgrad role's mode
         Mpad, Kpad = pack_dims(C, C)
         S = _empty((N * pack_floats(Mpad, Kpad),), y)
-        gemm_role("dgrad")
         lib.vst_symmetrize(ptr(gg.contiguous()), ptr(S), N, C, Kpad, Mpad, ctx.scale, gemm_mode(), stream())
         dy = conv_gemm(y.view(N, C, 1, H * W), S, C, 1, 1, H * W, GM_ZERO, 1, 0, 1, a_batch_stride=pack_floats(Mpad, Kpad))
         return dy.view(N, C, H, W), None
