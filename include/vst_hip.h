@@ -43,11 +43,15 @@ const char* vst_build_id(void);
  *   VST_GEMM_BF16X6  three-way hi + mid + lo split, the six products of order >= 2^-16 (per-product
  *                    error ~2^-24, fp32-class); packed operands are 1.5x the fp32 size
  *                    (Kpad*Mpad*3/2 floats).
+ * VST_GEMM_KBLOCK may be or-ed into the mode of a conv pack + GEMM pair (both must carry it):
+ * channel-block-major, tap-minor K order (16 channels x every tap, then the next 16 channels), which
+ * keeps each block's re-read source rows L2-resident; the sums then run in a different order.
  * An unknown mode returns VST_EINVAL (-1). */
 #define VST_GEMM_F32 0
 #define VST_GEMM_BF16X3 1
 #define VST_GEMM_BF16 2
 #define VST_GEMM_BF16X6 3
+#define VST_GEMM_KBLOCK 16
 
 /* ---- convolution (implicit GEMM on MFMA, arithmetic per the `mode` argument) ---------------
  * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv
@@ -368,6 +372,11 @@ int vst_flow_prep(const void* raw, float* out, int N, int Hs, int Ws, int Cr, in
 int vst_pfm_read_header(const char* path, int* width, int* height, int* channels, int* big_endian, int* offset,
                         float* scale);
 int vst_pfm_read(const char* path, void* dst, long bytes, int offset);
+
+/* ---- profiling ---------------------------------------------------------------------------
+ * an empty kernel (vst_marker_kernel) on `stream`: marks a region boundary in rocprofv3 traces
+ * (bench.py launches one before its timed steps; tools/pmc_traffic.py --after-marker) */
+int vst_marker(void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,8 @@ import json
 import sys
 
 FETCH_CORRECTION = 2.0
+PASS_ARGS = {"reconet": "bench.py --steps 2 --warmup 2 --prof-steps 0 (headline policy)",
+             "adaattn": "bench.py --model adaattn --steps 2 --warmup 2 --prof-steps 0"}
 
 
 def load(model, counter):
@@ -31,9 +33,22 @@ def instance(name):
     return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("::")[-1]
 
 
+def after_marker(rows):
+    """dispatches after the last vst_marker_kernel (bench.py's timed region)"""
+    ids = sorted(rows, key=int)
+    marks = [d for d in ids if "vst_marker_kernel" in rows[d]["Kernel_Name"]]
+    if not marks:
+        return rows
+    last = int(marks[-1])
+    return {d: r for d, r in rows.items() if int(d) > last}
+
+
 def main():
-    model = sys.argv[1] if len(sys.argv) > 1 else "reconet"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    model = args[0] if args else "reconet"
     F, W = load(model, "FETCH_SIZE"), load(model, "WRITE_SIZE")
+    if "--after-marker" in sys.argv:
+        F = after_marker(F)
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for d, r in F.items():
         name = r["Kernel_Name"]
@@ -48,12 +63,14 @@ def main():
     for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["bytes_per_launch"] * kv[1]["launches"])[:15]:
         print(f"{k[:36]:36s} n={v['launches']:4d} read={v['read_bytes_per_launch']/1e6:9.1f} MB "
               f"write={v['write_bytes_per_launch']/1e6:8.1f} MB per launch")
-    if len(sys.argv) > 2:
+    if len(args) > 1:
+        sel = ("dispatches of bench.py's timed steps only (after its vst_marker_kernel dispatch)"
+               if "--after-marker" in sys.argv else "every dispatch of the run")
         out = {"model": model, "fetch_correction": FETCH_CORRECTION,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (with --kernel-trace), "
-                         "bench.py --steps 1 --warmup 1; bytes = 2*FETCH + WRITE (calibrated, tools/calib)",
+                         f"{PASS_ARGS.get(model, 'bench.py')}; {sel}; bytes = 2*FETCH + WRITE (calibrated, tools/calib)",
                "families": fams}
-        json.dump(out, open(sys.argv[2], "w"), indent=1)
+        json.dump(out, open(args[1], "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -40,14 +40,17 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
   float v = 0.f;
   if (split_kh) {
     if (m < Cout * KH && k < KW * Cin) {
-      const int co = m / KH, kh = m % KH, kw = k / Cin, ci = k % Cin;
+      int kw, ci;
+      kdecode(k, Cin, KW, kw, ci, bsplit >> 4);
+      const int co = m / KH, kh = m % KH;
       v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
     }
   } else {
     int Ck = transposed ? Cout : Cin;  // channel count inside the k index
     int Mm = transposed ? Cin : Cout;
     if (m < Mm && k < KH * KW * Ck) {
-      const int tap = k / Ck, c = k % Ck;
+      int tap, c;
+      kdecode(k, Ck, KH * KW, tap, c, bsplit >> 4);
       int kh = tap / KW, kw = tap % KW;
       int co = transposed ? c : m, ci = transposed ? m : c;
       v = w[(((long)co * Cin + ci) * KH + kh) * KW + kw];
@@ -116,7 +119,9 @@ __global__ void pack_phase2_kernel(const float* __restrict__ w, float* __restric
   const int K2 = (KS + 1) / 2;
   float v = 0.f;
   if (m < 4 * Cin && k < K2 * K2 * Cout) {
-    const int tap = k / Cout, co = k % Cout, t = tap / K2, sx = tap % K2;
+    int tap, co;
+    kdecode(k, Cout, K2 * K2, tap, co, bsplit >> 4);
+    const int t = tap / K2, sx = tap % K2;
     const int ci = m >> 2, kh = ((m >> 1) & 1) + 2 * t, kw = (m & 1) + 2 * sx;
     if (kh < KS && kw < KS) v = w[(((long)co * Cin + ci) * KS + kh) * KS + kw];
   }
@@ -189,7 +194,9 @@ __global__ void pack_kwu_kernel(const float* __restrict__ w, float* __restrict__
   const int Mm = transposed ? Cin : Cout, Cc = transposed ? Cout : Cin;
   float v = 0.f;
   if (m < Mm && k < K * Cu) {
-    const int kh = k / Cu, cu = k - (k / Cu) * Cu, c = cu / K, kw = cu - (cu / K) * K;
+    int kh, cu;
+    kdecode(k, Cu, K, kh, cu, bsplit >> 4);
+    const int c = cu / K, kw = cu - (cu / K) * K;
     if (c < Cc) {
       const int co = transposed ? c : m, ci = transposed ? m : c;
       v = w[(((long)co * Cin + ci) * K + kh) * K + kw];
@@ -283,7 +290,7 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
 static long apack_floats(int M, int K, int mode) {
   const int bm = cfg_bm(select_cfg(M));
   const long f = (long)((M + bm - 1) / bm * bm) * ((K + BK - 1) / BK * BK);
-  return mode == VST_GEMM_BF16X6 ? f * 3 / 2 : f;
+  return vst_mode_arith(mode) == VST_GEMM_BF16X6 ? f * 3 / 2 : f;
 }
 
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
@@ -314,7 +321,8 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   {
     // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
     static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
-    if (t256 && cfg == T128 && M % 256 == 0 && (mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16)) cfg = T256;
+    const int am = vst_mode_arith(mode);
+    if (t256 && cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16)) cfg = T256;
   }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);
   P.Mpad = (M + bm - 1) / bm * bm;
@@ -337,10 +345,11 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   P.fd_Wo = make_fastdiv(Wo);
   P.fd_Cs = make_fastdiv(Cs);
   P.fd_KW = make_fastdiv(KW);
+  P.kb = (mode & VST_GEMM_KBLOCK) ? 1 : 0;
   dim3 grid(ceil_div((long)Ho * Wo, bn), P.Mpad / bm, N);
   const bool cfast = (Cs % 16) == 0, gm = gmask != nullptr;
   hipStream_t st = (hipStream_t)stream;
-  switch (mode) {
+  switch (vst_mode_arith(mode)) {
     case VST_GEMM_F32: launch_prec<0>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16: launch_prec<2>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16X6: launch_prec<3>(cfast, gm, cfg, grid, st, P); break;
@@ -545,7 +554,8 @@ __global__ void pack_upsum_kernel(const float* __restrict__ w, float* __restrict
   const int KU = KS + 1;
   float v = 0.f;
   if (m < Cin && k < KU * KU * Cout) {
-    const int tap = k / Cout, co = k % Cout;
+    int tap, co;
+    kdecode(k, Cout, KU * KU, tap, co, bsplit >> 4);
     const int jh = tap / KU, jw = tap % KU;
     const float* wp = w + ((long)co * Cin + m) * KS * KS;
     for (int a = 0; a < 2; ++a) {

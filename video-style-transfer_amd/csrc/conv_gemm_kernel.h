@@ -42,6 +42,7 @@ struct ConvParams {
   float* ph_border;
   int ph_H, ph_W, ph_pad;
   FastDiv fd_Wo, fd_Cs, fd_KW;
+  int kb;  // channel-blocked K order (VST_GEMM_KBLOCK, vst_common.h kdecode)
 };
 
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
@@ -170,9 +171,12 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     a_voff[i] = (A_F4 % NT == 0 || idx < A_F4) ? 16 * (AW == 16 ? a_slot(idx) : idx) : OOR;
   }
 
-  // CFAST tap walk: tiles are loaded in k order (tap-major), so the (tap, channel) position
-  // advances by 16 channels per tile and the gather offset is decoded once per tap (wave-uniform
-  // branch), not once per k-tile
+  // CFAST walk, tiles in k order: tap-major -- the (tap, channel) position advances by 16 channels
+  // per tile and the gather offset is decoded once per tap (wave-uniform branch); channel-blocked
+  // (P.kb) -- the tap advances every tile, its offset decoded per tile (the tap is a scalar, so the
+  // decode is a few VALU ops per thread), the channel block every KH*KW tiles
+  const bool blocked = CFAST && kblocked(P.Cs, P.kb);
+  const int ntap = P.KH * P.KW;
   int st_tap = 0, st_c0 = 0, st_vbase = 0;
   bool st_ok = false;
 
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
       // (Cs % 16 == 0, so K = taps * Cs is a whole number of tiles and every tile is in range)
       static_assert(BK == 16, "one tap per k-tile");
       (void)k0;
-      if (st_c0 == 0) {
+      if (blocked || st_c0 == 0) {
         const int kh = (int)fdiv((uint32_t)st_tap, P.fd_KW), kw = st_tap - kh * P.KW;
         const int off0 = gather_offset(P, oy, ox, kh, kw);
         st_ok = pvalid && off0 >= 0;
@@ -207,10 +211,17 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
         rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
         if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, i * sstep, 0));
       }
-      st_c0 += 16;
-      if (st_c0 == P.Cs) {
-        st_c0 = 0;
-        ++st_tap;
+      if (blocked) {
+        if (++st_tap == ntap) {
+          st_tap = 0;
+          st_c0 += 16;
+        }
+      } else {
+        st_c0 += 16;
+        if (st_c0 == P.Cs) {
+          st_c0 = 0;
+          ++st_tap;
+        }
       }
     } else {
 #pragma unroll

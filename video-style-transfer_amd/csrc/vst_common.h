@@ -63,13 +63,39 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
-// GEMM arithmetic mode: a per-call argument of every GEMM / pack entry (vst_hip.h VST_GEMM_*);
-// the library keeps no mode state
+// GEMM arithmetic mode: a per-call argument of every GEMM / pack entry (vst_hip.h VST_GEMM_*, plus
+// the VST_GEMM_KBLOCK K-order flag); the library keeps no mode state
+static inline int vst_mode_arith(int mode) { return mode & ~VST_GEMM_KBLOCK; }
 static inline bool vst_mode_ok(int mode) {
-  return mode == VST_GEMM_F32 || mode == VST_GEMM_BF16X3 || mode == VST_GEMM_BF16 || mode == VST_GEMM_BF16X6;
+  const int a = vst_mode_arith(mode);
+  return (mode & ~(VST_GEMM_KBLOCK | 3)) == 0 &&
+         (a == VST_GEMM_F32 || a == VST_GEMM_BF16X3 || a == VST_GEMM_BF16 || a == VST_GEMM_BF16X6);
 }
-// packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6)
-static inline int apack_split(int mode) { return mode == VST_GEMM_F32 ? 0 : (mode == VST_GEMM_BF16X6 ? 2 : 1); }
+// packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6); bit 4:
+// channel-blocked K order (kblocked)
+static inline int apack_split(int mode) {
+  const int a = vst_mode_arith(mode);
+  return (a == VST_GEMM_F32 ? 0 : (a == VST_GEMM_BF16X6 ? 2 : 1)) | ((mode & VST_GEMM_KBLOCK) ? 16 : 0);
+}
+
+// K order of a conv GEMM (the packed A rows and the kernel's B walk must agree).  With
+// VST_GEMM_KBLOCK and a channel count inside k that is a multiple of 16, k runs channel-block
+// major, tap minor -- k = (c/16)*(16*T) + tap*16 + c%16 -- so the T taps of one 16-channel block
+// are consecutive k-tiles and their B gathers re-read the same few source rows back to back
+// (L2-resident: ~3 rows x 16 channels per block) instead of one tap sweeping all channels before
+// the next (a reuse distance of Cs x 3 rows per block, past the XCD's 4 MB L2 at 64 blocks per
+// XCD).  Otherwise k is tap-major, k = tap*Ck + c.
+__host__ __device__ inline bool kblocked(int Ck, int kb) { return kb && Ck % 16 == 0; }
+__host__ __device__ inline void kdecode(int k, int Ck, int T, int& tap, int& c, int kb) {
+  if (kblocked(Ck, kb)) {
+    const int g = k / (16 * T), r = k - g * 16 * T;
+    tap = r >> 4;
+    c = g * 16 + (r & 15);
+  } else {
+    tap = k / Ck;
+    c = k - tap * Ck;
+  }
+}
 
 // Packed GEMM A operand ("weights"), k-tiles of 16: element (k, m) lives at
 //   ((k/16) * Mpad + m) * 16 + (k%2) * 8 + (k%16)/2
@@ -121,6 +147,7 @@ __device__ __forceinline__ void split3_bf16x2(float a, float b, uint32_t& hi, ui
 // 8h + j) reads its hi and lo fragments with one ds_read_b128 each.  split == 2 (bf16x6): 96-byte
 // blocks [hi][mid][lo] (the pack buffer is 1.5x the fp32 one).
 __device__ __forceinline__ void apack_store(float* out, int k, int m, int Mpad, float v, int split) {
+  split &= 3;
   if (!split) {
     out[apack_index(k, m, Mpad)] = v;
     return;

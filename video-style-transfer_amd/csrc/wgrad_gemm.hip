@@ -684,7 +684,7 @@ static void launch_wg(int c, bool tap, dim3 g, int mode, hipStream_t st, const W
   // float4 A loads need 4 consecutive pixels in one row segment (and, for the row-split gather,
   // in one output row)
   const bool av = (P.Ho * P.Wo) % 4 == 0 && (!P.asplit || P.Wo % 4 == 0);
-  switch (mode) {
+  switch (vst_mode_arith(mode)) {
     case VST_GEMM_F32: launch_wg_p<0>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg_p<2>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16X6: launch_wg_p<3>(av, tap, c, g, st, P); break;
@@ -734,7 +734,7 @@ static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
 
 template <int GMD>
 static void launch_wg2(int c, dim3 g, int mode, hipStream_t st, const Wg2Params& P) {
-  switch (mode) {
+  switch (vst_mode_arith(mode)) {
     case VST_GEMM_F32: launch_wg2_p<0, GMD>(c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg2_p<2, GMD>(c, g, st, P); break;
     case VST_GEMM_BF16X6: launch_wg2_p<3, GMD>(c, g, st, P); break;

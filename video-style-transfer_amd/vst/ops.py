@@ -35,6 +35,8 @@ def _check(t, name, ndim=None):
 
 
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
+KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
+KBLOCK_ON = os.environ.get("VST_KBLOCK", "1") != "0"  # A/B switch
 # The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
@@ -95,7 +97,7 @@ def gemm_mode():
 
 def gemm_mode_name(mode=None):
     mode = base_gemm_mode() if mode is None else mode
-    return {v: k for k, v in GEMM_MODES.items()}[mode]
+    return {v: k for k, v in GEMM_MODES.items()}[mode & ~KBLOCK]
 
 
 def use_policy(name):
@@ -153,13 +155,19 @@ def gemm_role(role):
         sc = sc.rpartition(".")[0] or None
     if m is None:
         m = GEMM_POLICY.get(role, _BASE_MODE[0])
+    # channel-blocked K order (VST_GEMM_KBLOCK) outside the stylizer: the frozen loss network's
+    # convs re-read their source rows from L2 instead of the Infinity Cache; the stylizer keeps the
+    # tap-major order its golden-gradient margins were measured in (tools/policy_check.py)
+    sc = _SCOPE[0]
+    if KBLOCK_ON and not (sc is not None and sc.split(".")[0] == "stylizer"):
+        m |= KBLOCK
     _CUR[0] = m
     return m
 
 
 def pack_floats(Mpad, Kpad):
     """Floats of one packed A operand in the current mode (bf16x6 blocks are 96 B, others 64 B)."""
-    return Kpad * Mpad * 3 // 2 if gemm_mode() == 3 else Kpad * Mpad
+    return Kpad * Mpad * 3 // 2 if (gemm_mode() & ~KBLOCK) == 3 else Kpad * Mpad
 
 
 def pack_dims(M, K):
