@@ -11,7 +11,8 @@ import sys
 import torch
 
 # GEMM arithmetic passed to every call (vst_hip.h VST_GEMM_*): 0 f32, 1 bf16x3, 2 bf16, 3 bf16x6
-MODE = int(os.environ.get("BENCH_GEMM_MODE", "3"))
+# (BENCH_GEMM_MODES="3,19": one column per mode and library; 19 = bf16x6 | VST_GEMM_KBLOCK)
+MODES = [int(m) for m in os.environ.get("BENCH_GEMM_MODES", os.environ.get("BENCH_GEMM_MODE", "3")).split(",")]
 
 sys.path.insert(0, "video-style-transfer_amd")
 from vst._lib import _CTYPES, parse_header  # noqa: E402
@@ -57,10 +58,11 @@ def load(path):
 def main():
     paths = sys.argv[1:]
     libs = [load(p) for p in paths]
+    cols = [(p, lib, m) for p, lib in zip(paths, libs) for m in MODES]
     dev = "cuda"
     st = torch.cuda.current_stream().cuda_stream
     only = None
-    results = {(p, s[0]): [] for p in paths for s in SHAPES}
+    results = {(p, m, s[0]): [] for p in paths for m in MODES for s in SHAPES}
     bufs = {}
     for s in SHAPES:
         name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
@@ -68,7 +70,7 @@ def main():
         out = torch.empty(N, M, Ho, Wo, device=dev)
         bufs[name] = (src, out)
     for rnd in range(3):
-        for p, lib in zip(paths, libs):
+        for p, lib, MODE in cols:
             for s in SHAPES:
                 name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
                 if only and only not in name:
@@ -76,7 +78,9 @@ def main():
                 src, out = bufs[name]
                 mp, kp = ctypes.c_int(), ctypes.c_int()
                 lib.vst_conv_pack_dims(M, KH * KW * Cs, ctypes.byref(mp), ctypes.byref(kp))
-                wp = torch.randn(kp.value * mp.value, device=dev) * 0.05
+                # packed A floats per mode (bf16x6 blocks are 96 B per 16 k, the others 64 B)
+                pf = kp.value * mp.value * 3 // 2 if (MODE & 15) == 3 else kp.value * mp.value
+                wp = torch.randn(pf, device=dev) * 0.05
                 args = (src.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cs, Hs, Ws, M, KH * KW * Cs, Ho, Wo,
                         KH, KW, gm, stride, pad, up, 0, 0, None, None, MODE, st)
                 for _ in range(2):
@@ -88,18 +92,19 @@ def main():
                     lib.vst_conv_gemm(*args)
                 e1.record()
                 torch.cuda.synchronize()
-                results[(p, name)].append(e0.elapsed_time(e1) / reps)
-    hdr = "shape".ljust(16) + "".join(p.split("/")[-1].replace("libvst_hip", "").replace(".so", "")[:14].rjust(16) for p in paths)
+                results[(p, MODE, name)].append(e0.elapsed_time(e1) / reps)
+    hdr = "shape".ljust(16) + "".join(
+        (p.split("/")[-1].replace("libvst_hip", "").replace(".so", "")[:10] + f" m{m}").rjust(16) for p, _, m in cols)
     print(hdr)
-    tot = {p: 0.0 for p in paths}
+    tot = {(p, m): 0.0 for p, _, m in cols}
     for s in SHAPES:
         line = s[0].ljust(16)
-        for p in paths:
-            ms = statistics.median(results[(p, s[0])])
-            tot[p] += ms
+        for p, _, m in cols:
+            ms = statistics.median(results[(p, m, s[0])])
+            tot[(p, m)] += ms
             line += f"{ms*1e3:8.0f}us{s[-1]/ms/1e9:5.0f}TF".rjust(16)
         print(line)
-    print("total".ljust(16) + "".join(f"{tot[p]:14.2f}ms" for p in paths))
+    print("total".ljust(16) + "".join(f"{tot[(p, m)]:14.2f}ms" for p, _, m in cols))
 
 
 if __name__ == "__main__":

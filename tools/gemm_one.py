@@ -1,6 +1,8 @@
 """Run a few GEMM launches of one layer shape (for rocprofv3 PMC passes on a single kernel).
 
-    python tools/gemm_one.py [fwd|dgrad|wgrad|attn] [reps]
+    python tools/gemm_one.py [fwd|dgrad|wgrad|attn|vgg1|vgg3|vgg3kb] [reps]
+
+The GEMM policy comes from VST_GEMM_POLICY (default f32); vgg3kb runs the channel-blocked K order.
 """
 import os
 import sys
@@ -18,13 +20,24 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     g = torch.Generator(device="cuda").manual_seed(0)
     N, C, H, W = 16, 192, 64, 128
+    if which.startswith("vgg"):
+        C, H, W = {"vgg1": (64, 256, 512), "vgg3": (256, 64, 128), "vgg3kb": (256, 64, 128)}[which]
+        N = 8
     x = torch.randn(N, C, H, W, device="cuda", generator=g)
     w = torch.randn(C, C, 3, 3, device="cuda", generator=g) * 0.05
     gy = torch.randn(N, C, H, W, device="cuda", generator=g)
     for _ in range(reps):
         if which == "fwd":
-            ops.conv_gemm(x, ops.packed_weight(w, False), C, 3, H, W, ops.GM_REFLECT, 1, 1, 1)
+            with ops.gemm_scope("stylizer"):
+                ops.gemm_role("fwd")
+                ops.conv_gemm(x, ops.packed_weight(w, False), C, 3, H, W, ops.GM_REFLECT, 1, 1, 1)
+        elif which.startswith("vgg"):
+            scope = "stylizer" if which != "vgg3kb" else "vgg"
+            with ops.gemm_scope(scope):
+                ops.gemm_role("fwd")
+                ops.conv_gemm(x, ops.packed_weight(w, False), C, 3, H, W, ops.GM_ZERO, 1, 1, 1)
         elif which == "dgrad":
+            ops.gemm_role("dgrad")
             ops.conv_gemm(gy, ops.packed_weight(w, True), C, 3, H, W, ops.GM_TRANSPOSED, 1, 1, 1)
         elif which == "wgrad":
             ops.conv_wgrad(gy, x, w.shape, 3, 1, 1, "reflect", 1)

@@ -15,6 +15,12 @@ __device__ __forceinline__ f32x4 mk4(float a, float b, float c, float d) {
 #define VST_CONV_BK 16
 #endif
 constexpr int BK = VST_CONV_BK;  // k-tile depth (multiple of 16)
+// timing ablations for variant builds only (results are wrong when set): 1 no B split, 2 no B
+// loads, 4 no A loads, 8 no LDS stores in the k loop, 16 no k-loop barrier, 32 no MFMA phase
+#ifndef VST_ABL
+#define VST_ABL 0
+#endif
+constexpr int ABL = VST_ABL;
 constexpr int NT = 256;
 
 struct ConvParams {
@@ -86,8 +92,15 @@ __device__ __forceinline__ int a_slot(int idx) {
   return row * 4 + quad;
 }
 
-template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC>
+// ADIR (bf16x6 only): the packed weights go straight from memory into each wave's MFMA A operand
+// registers (one buffer_load_b128 per 32-row fragment and piece, next tile prefetched a k-step
+// ahead) instead of through LDS: no A stores to LDS (the stores were the largest non-MFMA cost of
+// the k loop, tools/gemm_bench.py ablations) and no A reads from it.  With WN > 1 the waves of one
+// wave row fetch the same fragments (WN x the A bytes, from L2: the packed weights of a layer are
+// at most a few MB).
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false>
 __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
+  static_assert(!ADIR || PREC == 3, "A-direct: bf16x6");
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   // A block per (k-tile, row): 16 fp32 / 16 hi + 16 lo bf16 (64 B); bf16x6: + 16 mid bf16 (96 B)
@@ -106,7 +119,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
   // LDS row: the A block + 4 pad dwords (20 or 28 dwords: conflict-free ds_read_b128 / ds_write_b128)
   constexpr int LS = AW + 4;
-  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
+  __shared__ __attribute__((aligned(16))) float As[2][ADIR ? 1 : BM][LS];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
 
   const int tid = threadIdx.x;
@@ -149,9 +162,9 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x4 ra[A_PER];
-  float rb[B_PER];
-  float rg[GM ? B_PER : 1];
+  f32x4 ra0[A_PER];
+  float rb0[B_PER];
+  float rg0[GM ? B_PER : 1];
   // buffer descriptors over this image's source planes (wave-uniform inputs only)
   const int plane_i = P.Hs * P.Ws;
   const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane_i * 4u;
@@ -170,6 +183,12 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     const int idx = tid + i * NT;
     a_voff[i] = (A_F4 % NT == 0 || idx < A_F4) ? 16 * (AW == 16 ? a_slot(idx) : idx) : OOR;
   }
+  // A-direct: lane (r, h) of fragment i, piece p reads the 16 B at dword 8p + 4h of packed row
+  // m0 + (wm*TM + i)*32 + r (same layout the LDS path copies: [hi k0..15][mid][lo] per row)
+  int ad_voff[ADIR ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < (ADIR ? TM : 1); ++i) ad_voff[i] = (((wm * TM + i) * 32 + lo) * AW + 4 * hi) * 4;
+  bf16x8_t arN[ADIR ? TM : 1][3], arC[ADIR ? TM : 1][3];
 
   // CFAST walk, tiles in k order: tap-major -- the (tap, channel) position advances by 16 channels
   // per tile and the gather offset is decoded once per tap (wave-uniform branch); channel-blocked
@@ -182,12 +201,20 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
 
   // Issue every global load of tile t without branches (out-of-range taps read a clamped, valid
   // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
-  auto load_tile = [&](int t) {
+  auto load_tile = [&](int t, f32x4 (&ra)[A_PER], float (&rb)[B_PER], float (&rg)[GM ? B_PER : 1]) {
     const int k0 = t * BK;
     const int a_soff = __builtin_amdgcn_readfirstlane(((t * P.Mpad + m0) * AW) * 4);
+    if constexpr (ADIR) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+          arN[i][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff[i], a_soff + 32 * pc, 0));
+    } else
 #pragma unroll
     for (int i = 0; i < A_PER; ++i)
-      ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
+      ra[i] = (ABL & 4) ? f32x4{(float)t, 1.f, 2.f, (float)i}
+                        : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
     if (CFAST) {
       // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
       // offset per thread per group; out-of-range taps use an offset past the buffer end, which
@@ -208,21 +235,20 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
       const int sstep = __builtin_amdgcn_readfirstlane(KSTEP * plane_i * 4);
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
+        rb[i] = (ABL & 2) ? __int_as_float(vo + i)
+                          : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
         if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, i * sstep, 0));
       }
-      if (blocked) {
-        if (++st_tap == ntap) {
-          st_tap = 0;
-          st_c0 += 16;
-        }
-      } else {
-        st_c0 += 16;
-        if (st_c0 == P.Cs) {
-          st_c0 = 0;
-          ++st_tap;
-        }
-      }
+      // advance in select form: a branchy in-place update (`++st_tap` under one flag, `st_c0 += 16`
+      // under the other) was folded into a select of POINTERS to the two walk variables, which
+      // pushed them to scratch and put a flat load/store with vmcnt(0) -- a full drain of the tile
+      // prefetch -- into every k-step
+      const int tap1 = st_tap + 1, c1 = st_c0 + 16;
+      const bool wrap = blocked ? tap1 == ntap : c1 == P.Cs;
+      const int nt = blocked ? (wrap ? 0 : tap1) : (wrap ? tap1 : st_tap);
+      const int nc = blocked ? (wrap ? c1 : st_c0) : (wrap ? 0 : c1);
+      st_tap = nt;
+      st_c0 = nc;
     } else {
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
@@ -240,9 +266,10 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const f32x4 (&ra)[A_PER], const float (&rb)[B_PER],
+                        const float (&rg)[GM ? B_PER : 1]) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
+    for (int i = 0; i < (ADIR ? 0 : A_PER); ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
         if (AW == 16) {
@@ -259,7 +286,15 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     if constexpr (PREC == 3) {  // bf16x6 row: [hi k0..15][mid k0..15][lo k0..15]
       uint32_t h[B_PER / 2], m[B_PER / 2], l[B_PER / 2];
 #pragma unroll
-      for (int q = 0; q < B_PER / 2; ++q) split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
+      for (int q = 0; q < B_PER / 2; ++q) {
+        if (ABL & 1) {
+          h[q] = __float_as_uint(bv[2 * q]);
+          m[q] = __float_as_uint(bv[2 * q + 1]);
+          l[q] = h[q] ^ m[q];
+        } else {
+          split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
+        }
+      }
       uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
       if constexpr (ROWSTEP == 2) {
 #pragma unroll
@@ -304,14 +339,10 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     }
   };
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) load_tile(t + 1);
-    if constexpr (PREC == 3) {
+  auto compute_tile = [&](int buf) {
+    if constexpr (ADIR) {
+      mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC, Bs[buf], wn * TN * 32, lane);
+    } else if constexpr (PREC == 3) {
       mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
     } else if constexpr (PREC != 0) {
       mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
@@ -339,8 +370,31 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
             acc[i][j] =
                 __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < ntiles) store_tile(buf ^ 1);
-    __syncthreads();
+  };
+
+  // the loads of tile t+1 are in flight across the MFMAs of tile t (a second register set for
+  // tile t+2 measured no gain: the loop is not waiting on global latency)
+  // (A-direct: the A registers of tile t+1 land with the B loads the store waits for, then become
+  // the current set -- register moves after that wait, no extra drain)
+  auto rotate_a = [&]() {
+    if constexpr (ADIR) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) arC[i][pc] = arN[i][pc];
+    }
+  };
+  load_tile(0, ra0, rb0, rg0);
+  store_tile(0, ra0, rb0, rg0);
+  rotate_a();
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1, ra0, rb0, rg0);
+    if (!(ABL & 32)) compute_tile(buf);
+    if (t + 1 < ntiles && !(ABL & 8)) store_tile(buf ^ 1, ra0, rb0, rg0);
+    if (t + 1 < ntiles) rotate_a();
+    if (!(ABL & 16)) __syncthreads();
   }
 
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -465,6 +519,13 @@ inline int widen_cfg(int c, long HWo) {
 #ifndef VST_MINW_T128_BF
 #define VST_MINW_T128_BF 3
 #endif
+// bf16x6 128x128 tile with A-direct weights (WM=4 x TN=4 waves layout)
+#ifndef VST_ADIR
+#define VST_ADIR 1
+#endif
+#ifndef VST_MINW_ADIR
+#define VST_MINW_ADIR 3
+#endif
 
 template <bool CF, bool GMK, int PR>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
@@ -474,10 +535,17 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
     case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
     case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2, PR><<<grid, NT, 0, st>>>(P); break;
-    case T128: conv_gemm_kernel<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P); break;
+    case T128:
+      if constexpr (PR == 3 && VST_ADIR)
+        conv_gemm_kernel<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true><<<grid, NT, 0, st>>>(P);
+      else
+        conv_gemm_kernel<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P);
+      break;
     case T256:  // bf16x3 / bf16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
       if constexpr (PR == 1 || PR == 2) conv_gemm_kernel<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR><<<grid, NT, 0, st>>>(P);
       break;
+    // (A-direct measured slower on the 192-row and 64x256 tiles: with two or four waves per wave
+    // row the duplicated fragment loads cost more vector-memory time than the LDS stores they save)
     default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR><<<grid, NT, 0, st>>>(P); break;
   }
 }

@@ -240,6 +240,34 @@ __device__ __forceinline__ void mfma_bf16x6_ktile(f32x16 (&acc)[TM][TN], float (
     }
 }
 
+// bf16x6 k-tile with the A fragments already in registers (hi, mid, lo per 32-row fragment, loaded
+// straight from the packed weights) and B from LDS
+template <int TM, int TN, int LS>
+__device__ __forceinline__ void mfma_bf16x6_ktile_ra(f32x16 (&acc)[TM][TN], const bf16x8_t (&ar)[TM][3],
+                                                     float (*B)[LS], int b0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8_t bh[TN], bm[TN], bl[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float* p = &B[b0 + j * 32 + r][4 * h];
+    bh[j] = *reinterpret_cast<const bf16x8_t*>(p);
+    bm[j] = *reinterpret_cast<const bf16x8_t*>(p + 8);
+    bl[j] = *reinterpret_cast<const bf16x8_t*>(p + 16);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      f32x16 c = acc[i][j];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][2], bh[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][1], bm[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][0], bl[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][1], bh[j], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][0], bm[j], c, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][0], bh[j], c, 0, 0, 0);
+    }
+}
+
 // A wave-uniform pointer forced into SGPRs: a buffer descriptor built from a pointer the compiler
 // keeps in VGPRs (e.g. after a 64-bit VALU multiply) makes every buffer load a waterfall loop.
 __device__ __forceinline__ void* uniform_ptr(const void* p) {
