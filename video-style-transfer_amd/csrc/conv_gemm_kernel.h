@@ -98,23 +98,29 @@ __device__ __forceinline__ int a_slot(int idx) {
 // the k loop, tools/gemm_bench.py ablations) and no A reads from it.  With WN > 1 the waves of one
 // wave row fetch the same fragments (WN x the A bytes, from L2: the packed weights of a layer are
 // at most a few MB).
+// Block = WM x WN waves (4 on the LDS-A path; 2 or 6 with A-direct, where the first min(threads,
+// 256) threads gather and split the B tile and every wave reads it).
 template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false>
-__global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
+__global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(!ADIR || PREC == 3, "A-direct: bf16x6");
+  static_assert(ADIR || WM * WN == 4, "LDS-A path: 4 waves");
+  constexpr int NTT = WM * WN * 64;          // threads per block
+  constexpr int NBT = NTT < NT ? NTT : NT;   // threads that load and store the B tile
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   // A block per (k-tile, row): 16 fp32 / 16 hi + 16 lo bf16 (64 B); bf16x6: + 16 mid bf16 (96 B)
   constexpr int AW = PREC == 3 ? 24 : 16;    // dwords per (k-tile, row)
   constexpr int A_F4 = BM * AW / 4;          // float4 per A tile
   constexpr int A_PER = (A_F4 + NT - 1) / NT;
-  constexpr int ROWSTEP = NT / BN;           // B rows covered per pass
+  constexpr int ROWSTEP = NBT / BN;          // B rows covered per pass
   constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
   constexpr int KSTEPS = BK / 2;
   // k rows of this thread's B elements: fp32 MFMA (32x32x2: lane half h takes k = 2s + h) ->
   // k = brow0 + ROWSTEP*i; bf16 MFMA (32x32x16: lane half h takes k = 8h..8h+7) -> contiguous
   // k = brow0*B_PER + i, so each thread packs its own bf16 pairs
   constexpr int KSTEP = PREC ? 1 : ROWSTEP;
-  static_assert(NT % BN == 0 && BK % ROWSTEP == 0, "tile");
+  static_assert(NBT % BN == 0 && BK % ROWSTEP == 0, "tile");
+  const bool bthread = NTT == NBT || threadIdx.x < NBT;  // wave-uniform
 
   static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
   // LDS row: the A block + 4 pad dwords (20 or 28 dwords: conflict-free ds_read_b128 / ds_write_b128)
@@ -215,7 +221,8 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
     for (int i = 0; i < A_PER; ++i)
       ra[i] = (ABL & 4) ? f32x4{(float)t, 1.f, 2.f, (float)i}
                         : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
-    if (CFAST) {
+    if (!bthread) {
+    } else if (CFAST) {
       // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
       // offset per thread per group; out-of-range taps use an offset past the buffer end, which
       // the buffer-load range check turns into 0 (no branch, no select)
@@ -280,6 +287,7 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
         }
       }
     }
+    if (!bthread) return;
     float bv[B_PER];
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) bv[i] = GM ? (rg[i] > 0.f ? rb[i] : 0.f) : rb[i];
@@ -480,7 +488,8 @@ __global__ __launch_bounds__(NT, MINW) void conv_gemm_kernel(ConvParams P) {
 }
 
 // tile configurations (BM x BN)
-enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256 };
+// T64A / T192A: bf16x6 A-direct blocks of 2 / 6 waves (32 weight rows x 128 pixels per wave)
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256, T64A, T192A };
 
 inline int select_cfg(int M) {
   if (M <= 32) return T32;
@@ -490,7 +499,7 @@ inline int select_cfg(int M) {
   return T128;
 }
 inline int cfg_bm(int c) {
-  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256};
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256, 64, 192};
   return bm[c];
 }
 inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
@@ -519,7 +528,7 @@ inline int widen_cfg(int c, long HWo) {
 #ifndef VST_MINW_T128_BF
 #define VST_MINW_T128_BF 3
 #endif
-// bf16x6 128x128 tile with A-direct weights (WM=4 x TN=4 waves layout)
+// bf16x6 A-direct tiles (one wave per 32 weight rows, 128 pixels per block)
 #ifndef VST_ADIR
 #define VST_ADIR 1
 #endif
@@ -527,26 +536,34 @@ inline int widen_cfg(int c, long HWo) {
 #define VST_MINW_ADIR 3
 #endif
 
+template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false>
+static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
+  conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR><<<grid, WM * WN * 64, 0, st>>>(P);
+}
+
 template <bool CF, bool GMK, int PR>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
+  constexpr bool AD = PR == 3 && VST_ADIR;
   switch (cfg) {
-    case T32: conv_gemm_kernel<1, 1, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
-    case T64: conv_gemm_kernel<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
-    case T96: conv_gemm_kernel<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR><<<grid, NT, 0, st>>>(P); break;
-    case T64W: conv_gemm_kernel<1, 2, 4, 2, CF, GMK, 3, PR><<<grid, NT, 0, st>>>(P); break;
-    case T96W: conv_gemm_kernel<1, 3, 4, 2, CF, GMK, 2, PR><<<grid, NT, 0, st>>>(P); break;
-    case T128:
-      if constexpr (PR == 3 && VST_ADIR)
-        conv_gemm_kernel<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true><<<grid, NT, 0, st>>>(P);
-      else
-        conv_gemm_kernel<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR><<<grid, NT, 0, st>>>(P);
+    case T32: launch_k<1, 1, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
+    case T64: launch_k<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
+    case T64A:
+      if constexpr (AD) launch_k<2, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
+      break;
+    case T192A:
+      if constexpr (AD) launch_k<6, 1, 1, 4, CF, GMK, 3, PR, true>(grid, st, P);
+      break;
+    case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
+    case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
+    case T96W: launch_k<1, 3, 4, 2, CF, GMK, 2, PR>(grid, st, P); break;
+    case T128:  // bf16x6: four A-direct waves of 32 rows x 128 pixels
+      if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
+      else launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
-      if constexpr (PR == 1 || PR == 2) conv_gemm_kernel<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR><<<grid, NT, 0, st>>>(P);
+      if constexpr (PR == 1 || PR == 2) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR>(grid, st, P);
       break;
-    // (A-direct measured slower on the 192-row and 64x256 tiles: with two or four waves per wave
-    // row the duplicated fragment loads cost more vector-memory time than the LDS stores they save)
-    default: conv_gemm_kernel<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR><<<grid, NT, 0, st>>>(P); break;
+    default: launch_k<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR>(grid, st, P); break;
   }
 }
 

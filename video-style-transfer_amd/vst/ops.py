@@ -37,6 +37,7 @@ def _check(t, name, ndim=None):
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
 KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
 KBLOCK_ON = os.environ.get("VST_KBLOCK", "1") != "0"  # A/B switch
+KBLOCK_STYLIZER = os.environ.get("VST_KBLOCK", "1") == "2"  # also inside the stylizer scope
 # The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
@@ -159,7 +160,7 @@ def gemm_role(role):
     # convs re-read their source rows from L2 instead of the Infinity Cache; the stylizer keeps the
     # tap-major order its golden-gradient margins were measured in (tools/policy_check.py)
     sc = _SCOPE[0]
-    if KBLOCK_ON and not (sc is not None and sc.split(".")[0] == "stylizer"):
+    if KBLOCK_ON and (KBLOCK_STYLIZER or not (sc is not None and sc.split(".")[0] == "stylizer")):
         m |= KBLOCK
     _CUR[0] = m
     return m
