@@ -98,16 +98,17 @@ __device__ __forceinline__ int a_slot(int idx) {
 // the k loop, tools/gemm_bench.py ablations) and no A reads from it.  With WN > 1 the waves of one
 // wave row fetch the same fragments (WN x the A bytes, from L2: the packed weights of a layer are
 // at most a few MB).
-// Block = WM x WN waves (4 on the LDS-A path; 2 or 6 with A-direct, where the first min(threads,
-// 256) threads gather and split the B tile and every wave reads it).
+// Block = WM x WN waves (4 on the LDS-A path; 2, 6 or 8 with A-direct, where the threads that
+// divide the B tile evenly -- all of them for 2, 4 and 8 waves, the first 256 for 6 -- gather and
+// split it and every wave reads it).
 template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(!ADIR || PREC == 3, "A-direct: bf16x6");
   static_assert(ADIR || WM * WN == 4, "LDS-A path: 4 waves");
-  constexpr int NTT = WM * WN * 64;          // threads per block
-  constexpr int NBT = NTT < NT ? NTT : NT;   // threads that load and store the B tile
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
+  constexpr int NTT = WM * WN * 64;          // threads per block
+  constexpr int NBT = (NTT % BN == 0 && BK % (NTT / BN) == 0) ? NTT : NT;  // B-tile threads
   // A block per (k-tile, row): 16 fp32 / 16 hi + 16 lo bf16 (64 B); bf16x6: + 16 mid bf16 (96 B)
   constexpr int AW = PREC == 3 ? 24 : 16;    // dwords per (k-tile, row)
   constexpr int A_F4 = BM * AW / 4;          // float4 per A tile
@@ -304,7 +305,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
         }
       }
       uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
-      if constexpr (ROWSTEP == 2) {
+      if constexpr (ROWSTEP == 4) {  // k = 4*brow0 .. 4*brow0+3: one b64 per piece
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+          const uint32_t* v = part == 0 ? h : (part == 1 ? m : l);
+          *reinterpret_cast<u32x2*>(d + 8 * part + 2 * brow0) = u32x2{v[0], v[1]};
+        }
+      } else if constexpr (ROWSTEP == 2) {
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
           const uint32_t* v = part == 0 ? h : (part == 1 ? m : l);
@@ -488,8 +495,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 }
 
 // tile configurations (BM x BN)
-// T64A / T192A: bf16x6 A-direct blocks of 2 / 6 waves (32 weight rows x 128 pixels per wave)
-enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256, T64A, T192A };
+// T64A / T192A / T256A: bf16x6 A-direct blocks of 2 / 6 / 8 waves (32 weight rows x 128 pixels per
+// wave)
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256, T64A, T192A, T256A };
 
 inline int select_cfg(int M) {
   if (M <= 32) return T32;
@@ -499,7 +507,7 @@ inline int select_cfg(int M) {
   return T128;
 }
 inline int cfg_bm(int c) {
-  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256, 64, 192};
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256, 64, 192, 256};
   return bm[c];
 }
 inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
@@ -535,6 +543,9 @@ inline int widen_cfg(int c, long HWo) {
 #ifndef VST_MINW_ADIR
 #define VST_MINW_ADIR 3
 #endif
+#ifndef VST_MINW_A256
+#define VST_MINW_A256 4
+#endif
 
 template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false>
 static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
@@ -552,6 +563,9 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
       break;
     case T192A:
       if constexpr (AD) launch_k<6, 1, 1, 4, CF, GMK, 3, PR, true>(grid, st, P);
+      break;
+    case T256A:  // all eight waves gather the B tile (4 elements each)
+      if constexpr (AD) launch_k<8, 1, 1, 4, CF, GMK, VST_MINW_A256, PR, true>(grid, st, P);
       break;
     case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
     case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
