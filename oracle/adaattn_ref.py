@@ -2,7 +2,8 @@
 (see oracle/__init__.py).  Pinned by tests/golden/aa_*.npz produced from the reference itself.
 
 Follows AA/vgg19.py:43-63, AA/utilities.py:79-109, AA/network.py:11-251, AA/lossfn.py:5-53,
-AA/train_video.py:78-118.  Parameters are dicts keyed like the reference state_dicts.
+AA/train_video.py:78-118, AA/train_image.py:69-106.  Parameters are dicts keyed like the reference
+state_dicts.
 """
 import torch
 import torch.nn.functional as F
@@ -13,16 +14,17 @@ from .shapes import ADAATTN_LEVELS, DECODER
 FEATS = ("relu1_1", "relu2_1", "relu3_1", "relu4_1", "relu5_1")
 
 
-def vgg_normalize(x):
-    """AA/utilities.py:79-85 (out of place): (x/255 - mean)/std."""
-    mean = torch.tensor(R.IMAGENET_MEAN, dtype=torch.float32).view(-1, 1, 1)
-    std = torch.tensor(R.IMAGENET_STD, dtype=torch.float32).view(-1, 1, 1)
-    return (x.float() / 255.0 - mean) / std
+def vgg_normalize(x, dtype=torch.float32):
+    """AA/utilities.py:79-85 (out of place): (x/255 - mean)/std (dtype: float64 only for the exact
+    reference values the conditioning-aware tolerances are built from)."""
+    mean = torch.tensor(R.IMAGENET_MEAN, dtype=dtype).view(-1, 1, 1)
+    std = torch.tensor(R.IMAGENET_STD, dtype=dtype).view(-1, 1, 1)
+    return (x.to(dtype) / 255.0 - mean) / std
 
 
-def vgg19(VP, x):
+def vgg19(VP, x, dtype=torch.float32):
     """AA/vgg19.py:43-63 -> dict relu1_1..relu5_1."""
-    return dict(zip(FEATS, R.vgg_forward(VP, vgg_normalize(x), R.VGG19_PLAN)))
+    return dict(zip(FEATS, R.vgg_forward(VP, vgg_normalize(x, dtype), R.VGG19_PLAN)))
 
 
 def feature_down_sample(feat, last):
@@ -46,7 +48,12 @@ def cosine_attention(q, k):
     return s / s.sum(dim=-1, keepdim=True)
 
 
-def adaattn(P, prefix, c_x, s_x, c_1x, s_1x):
+def softmax_attention(q, k):
+    """AA/network.py:100-106: softmax(q k) over the style positions."""
+    return torch.softmax(torch.bmm(q, k), dim=-1)
+
+
+def adaattn(P, prefix, c_x, s_x, c_1x, s_1x, activation="cosine"):
     """AA/network.py:191-220 (prefix=None -> AdaAttnNoConv, AA/network.py:142-171)."""
     Q, K, V = instance_norm(c_1x), instance_norm(s_1x), s_x
     if prefix is not None:
@@ -58,7 +65,7 @@ def adaattn(P, prefix, c_x, s_x, c_1x, s_1x):
     b, _, hs, ws = K.shape
     Km = K.reshape(b, -1, hs * ws)
     Vt = V.reshape(b, -1, hs * ws).permute(0, 2, 1)
-    A = cosine_attention(Qt, Km)
+    A = cosine_attention(Qt, Km) if activation == "cosine" else softmax_attention(Qt, Km)
     M = torch.bmm(A, Vt)
     S = torch.sqrt((torch.bmm(A, Vt ** 2) - M ** 2).clamp(min=1e-6))
     b, _, h, w = c_x.shape
@@ -91,13 +98,14 @@ def decoder(P, x5, x4, x3):
     return conv(conv(x, "conv7"), "conv8")
 
 
-def stylize(P, fc, fs):
+def stylize(P, fc, fs, activation="cosine"):
     """StylizingNetwork.forward (AA/network.py:237-251)."""
     lc, ls = list(fc.values()), list(fs.values())
     outs = []
     for i in range(3):
         idx = i + 2
-        outs.append(adaattn(P, f"adaattn.{i}", lc[idx], ls[idx], feature_down_sample(lc, idx), feature_down_sample(ls, idx)))
+        outs.append(adaattn(P, f"adaattn.{i}", lc[idx], ls[idx], feature_down_sample(lc, idx), feature_down_sample(ls, idx),
+                            activation))
     return decoder(P, outs[2], outs[1], outs[0])
 
 
@@ -147,3 +155,24 @@ def adaattn_losses(P, VP, c1, c2, s, w=WEIGHTS):
     lf = lf * w["LAMBDA_L"]
     isl = sum(image_similarity_loss(fc1[k], fc2[k], fcs1[k], fcs2[k]) for k in FEATS[1:4]) * w["LAMBDA_IS"]
     return {"loss": gs + lf + isl, "loss_gs": gs, "loss_lf": lf, "loss_is": isl}
+
+
+IMAGE_WEIGHTS = dict(LAMBDA_G=10.0, LAMBDA_L=3.0)  # AA/train_image.py:20-21
+
+
+def adaattn_image_losses(P, VP, c, s, w=IMAGE_WEIGHTS, activation="softmax", dtype=torch.float32):
+    """Loss terms of one train_image step (AA/train_image.py:69-106): single content images, softmax
+    attention (ACTIAVTION = "softmax", :22), global-stylized + local-feature losses, no IS term.
+    dtype=float64 (with float64 P / VP) gives the exact values of the same step."""
+    fc = {k: v.detach() for k, v in vgg19(VP, c, dtype).items()}
+    fs = {k: v.detach() for k, v in vgg19(VP, s, dtype).items()}
+    fcs = vgg19(VP, stylize(P, fc, fs, activation), dtype)
+    gs = sum(global_stylized_loss(fcs[k], fs[k]) for k in FEATS[1:]) * w["LAMBDA_G"]
+    lc, ls = list(fc.values()), list(fs.values())
+    lf = 0
+    for i in range(3):
+        idx = i + 2
+        t = adaattn(None, None, lc[idx], ls[idx], feature_down_sample(lc, idx), feature_down_sample(ls, idx), activation)
+        lf = lf + F.mse_loss(fcs[FEATS[idx]], t)
+    lf = lf * w["LAMBDA_L"]
+    return {"loss": gs + lf, "loss_gs": gs, "loss_lf": lf}

@@ -502,6 +502,70 @@ def gen_adaattn():
     print("adaattn fixtures written")
 
 
+def gen_aa_image():
+    """One step of the reference's own AA/train_image.py train() (softmax attention, content + style
+    images, global-stylized + local-feature losses) -> aa_image_step.npz."""
+    _fresh_project(AA_DIR)
+    for n in ("utilities", "vgg19", "network", "lossfn"):
+        sys.modules[n] = _load(n, os.path.join(AA_DIR, n + ".py"))
+    aa_net, aa_vgg = sys.modules["network"], sys.modules["vgg19"]
+    step = {}
+    B, H, W, seeds = 2, 64, 96, (51, 52, 53)
+    rng = np.random.default_rng(seeds[2])
+    c = torch.from_numpy(rng.uniform(0, 255, (B, 3, H, W)).astype(f32))
+    st = torch.from_numpy(rng.uniform(0, 255, (B, 3, H, W)).astype(f32))
+    fake_ds = types.ModuleType("datasets")
+    fake_ds.CocoWikiArt = lambda *a, **k: None
+    sys.modules["datasets"] = fake_ds
+    ti = _load("aa_train_image", os.path.join(AA_DIR, "train_image.py"))
+
+    def net_factory(activation="softmax"):
+        m = aa_net.StylizingNetwork(activation)
+        seed_module(m, seeds[0])
+        ti.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(m.named_parameters())))
+        return m
+
+    def vgg_factory():
+        v = aa_vgg.VGG19()
+        seed_module(v, seeds[1])
+        return v
+
+    ti.EPOCH_START, ti.EPOCH_END = 1, 1
+    ti.DataLoader = lambda *a, **k: [(c.clone(), st.clone())]
+    ti.StylizingNetwork, ti.VGG19, ti.tqdm = net_factory, vgg_factory, _TqdmRecorder
+    _TqdmRecorder.records = []
+    save = torch.save
+    torch.save = lambda *a, **k: None
+    try:
+        ti.train()
+    finally:
+        torch.save = save
+    rec = _TqdmRecorder.records[-1]
+    step["content"], step["style"], step["seeds"] = _np(c), _np(st), np.array(seeds)
+    for k in ("loss", "loss_gs", "loss_lf"):
+        step[k] = np.array(rec[k], dtype=np.float64)
+    adam = ti.optim.Adam
+    _grad_summary("", adam.grads, adam.after, step, seed=seeds[0] + 1000)
+    # exact (float64) values of the same step from the oracle, whose float32 form the test pins to
+    # the reference: softmax attention over relu4_1/relu5_1 logits is ill-conditioned, and the
+    # reference's own fp32 gradients sit up to ~0.5 % from the exact ones (the key-conv biases,
+    # whose exact gradient is 0 -- softmax is shift-invariant -- are pure rounding noise there)
+    from oracle import adaattn_ref as A
+    from oracle import seeded_params, shapes
+    P = {k: v.double().requires_grad_(True) for k, v in seeded_params(shapes.stylizing_network(), seeds[0]).items()}
+    VP = {k: v.double() for k, v in seeded_params(shapes.vgg19(), seeds[1]).items()}
+    L = A.adaattn_image_losses(P, VP, c.double(), st.double(), dtype=torch.float64)
+    L["loss"].backward()
+    for k in ("loss", "loss_gs", "loss_lf"):
+        step[f"exact_{k}"] = np.array(float(L[k]))
+    for n in step["names"]:
+        g = P[str(n)].grad.reshape(-1)
+        step[f"exact_gnorm/{n}"] = np.array(float(g.norm()))
+        step[f"exact_gval/{n}"] = g[torch.from_numpy(step[f"gidx/{n}"])].numpy()
+    np.savez_compressed(os.path.join(HERE, "aa_image_step.npz"), **step)
+    print("adaattn image-step fixture written")
+
+
 # --------------------------------------------------------------------------------------------
 # ReCoNet inference (RC/utilities.py:108-235): the reference's own Inference / calculate_mse
 # --------------------------------------------------------------------------------------------
@@ -713,3 +777,5 @@ if __name__ == "__main__":
         gen_rtnstv()
     if "dataprep" in which:
         gen_dataprep()
+    if "aa_image" in which:
+        gen_aa_image()

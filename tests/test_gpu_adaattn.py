@@ -253,6 +253,52 @@ def test_train_video_step_golden(golden, step_policy):
         assert np.abs(got - s[f"phead/{n}"])[sel].max(initial=0) < 1e-5, n
 
 
+def test_train_image_step_golden(golden, step_policy):
+    """One full train_image step (softmax attention, content + style images, global-stylized +
+    local-feature losses, Adam) vs the reference's own AA/train_image.py train().
+
+    Softmax attention over the relu4_1 / relu5_1 logits is ill-conditioned: the reference's own fp32
+    gradients sit up to ~0.5 % from the exact (float64 oracle, recorded in the fixture) values, and
+    the key-conv bias gradients, exactly 0 (softmax is shift-invariant), are pure rounding noise.
+    Each gradient is therefore checked against the exact value with the usual bar (1e-3 of its norm
+    + 1e-4 of the largest norm) widened by twice the reference's own distance from it, and the
+    post-Adam check skips the noise-only tensors."""
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+
+    s = golden("aa_image_step")
+    seeds = s["seeds"]
+    model = _seeded(StylizingNetwork("softmax"), shapes.stylizing_network(), int(seeds[0])).to(DEV)
+    vgg = _seeded(VGG19(), shapes.vgg19(), int(seeds[1])).to(DEV)
+    tr = AdaAttNTrainer(model, vgg, activation="softmax")
+    out = tr.image_step(G(s["content"]), G(s["style"]))
+    for k in ("loss", "loss_gs", "loss_lf"):
+        assert rel_err(out[k].item(), s[k]) < 1e-3, k
+    names = list(s["names"])
+    named = dict(model.named_parameters())
+    gmax = max(float(s[f"gnorm/{n}"]) for n in names)
+    noise = set()
+    for n in names:
+        gr = C(named[n].grad).reshape(-1)  # views of the flat gradient the step reduced into
+        gn, ex = float(s[f"gnorm/{n}"]), float(s[f"exact_gnorm/{n}"])
+        tol = 1e-3 * gn + 1e-4 * gmax
+        if abs(gn - ex) > 0.5 * gn:
+            noise.add(n)
+        assert abs(float(gr.double().norm()) - ex) <= tol + 2 * abs(gn - ex), n
+        idx = s[f"gidx/{n}"]
+        ref_dev = np.abs(s[f"gval/{n}"] - s[f"exact_gval/{n}"]).max()
+        assert np.abs(gr[idx].numpy() - s[f"exact_gval/{n}"]).max() <= tol + 2 * ref_dev, n
+    assert noise <= {f"adaattn.{i}.g.bias" for i in range(3)}, noise
+    for n in names:
+        if n in noise:
+            continue
+        gh = s[f"ghead/{n}"]
+        sel = np.abs(gh) > 1e-6 * gmax + 1e-2 * np.abs(gh).max()
+        got = C(named[n]).reshape(-1)[:64].numpy()
+        assert np.abs(got - s[f"phead/{n}"])[sel].max(initial=0) < 1e-5, n
+
+
 # BASELINE config 5 runs AdaAttN on half-precision MFMA.  Here that is the "bf16" policy: every
 # GEMM a single bf16 product (8-bit significand, ~2^-8 = 3.9e-3 relative per product) with fp32
 # accumulation and fp32 everywhere else.  The reference has no half-precision path (AA/utilities.py:81

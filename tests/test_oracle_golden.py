@@ -199,6 +199,30 @@ def test_adaattn_train_step(golden):
         assert np.abs(g.reshape(-1)[idx].numpy() - s[f"gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
 
 
+def test_adaattn_image_step(golden):
+    """The oracle's train_image step (softmax attention, no IS term) vs the reference's own
+    AA/train_image.py train() (tests/golden/gen_golden.py gen_aa_image)."""
+    from oracle import adaattn_ref as A
+
+    s = golden("aa_image_step")
+    seeds = s["seeds"]
+    P = oracle.seeded_params(shapes.stylizing_network(), int(seeds[0]), requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg19(), int(seeds[1]))
+    L = A.adaattn_image_losses(P, VP, T(s["content"]), T(s["style"]))
+    for k in ("loss", "loss_gs", "loss_lf"):
+        assert rel_err(L[k].item(), s[k]) < 1e-3, k
+    L["loss"].backward()
+    names = list(s["names"])
+    assert sorted(names) == sorted(P)
+    gmax = max(float(s[f"gnorm/{n}"]) for n in names)
+    for n in names:
+        g = P[n].grad
+        gn = float(s[f"gnorm/{n}"])
+        assert abs(float(g.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
+        idx = s[f"gidx/{n}"]
+        assert np.abs(g.reshape(-1)[idx].numpy() - s[f"gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+
+
 # ----------------------------------------------------------------------------- distillation (SD2)
 SD_WEIGHTS = dict(ALPHA=1e5, BETA=1e10, GAMMA=1e-2, LAMBDA_F=1e11, LAMBDA_O=1e7)  # train_Flow_SD2.py:24-29
 

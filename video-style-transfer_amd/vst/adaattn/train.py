@@ -1,4 +1,5 @@
-"""AdaAttN video training step (AA/train_video.py:78-118) on MI355X, single- or multi-GPU.
+"""AdaAttN training steps on MI355X, single- or multi-GPU: the video step (AA/train_video.py:78-118)
+and the image step (AA/train_image.py:69-110, `image_step`).
 
 Per step, exactly the reference loop body:
   fc1, fc2, fs = VGG19(content1), VGG19(content2), VGG19(style)          (no gradient: data)
@@ -109,10 +110,39 @@ class AdaAttNTrainer:
             isl = t if isl is None else isl + t
         return {"loss": gs + lf + isl, "loss_gs": gs, "loss_lf": lf, "loss_is": isl}
 
+    def image_losses(self, c, s):
+        """Loss terms of one train_image step (AA/train_image.py:76-106): content / style images,
+        the trainer's activation (the reference script uses "softmax", :22), global-stylized and
+        local-feature losses only (no image-similarity term)."""
+        w = self.w
+        with torch.no_grad():
+            fc, fs = self.vgg(c), self.vgg(s)
+        fcs = self.vgg(self.model(fc, fs))
+        gs = None
+        for k in FEATURES[1:]:
+            t = global_stylized_loss(fcs[k], fs[k], weight=w["LAMBDA_G"])
+            gs = t if gs is None else gs + t
+        lc, ls = list(fc.values()), list(fs.values())
+        lf = None
+        for i in range(3):
+            idx = i + 2
+            with torch.no_grad():
+                target = self.noconv[i](lc[idx], ls[idx], feature_down_sample(lc, idx), feature_down_sample(ls, idx))
+            t = local_feature_loss(fcs[FEATURES[idx]], target, weight=w["LAMBDA_L"])
+            lf = t if lf is None else lf + t
+        return {"loss": gs + lf, "loss_gs": gs, "loss_lf": lf}
+
+    def image_step(self, c, s):
+        """backward + Adam of `image_losses` (AA/train_image.py:109-110)."""
+        return self._update(self.image_losses, c, s)
+
     def step(self, c1, c2=None, s=None):
+        return self._update(self.losses, c1, c2, s)
+
+    def _update(self, losses, *args):
         self.flat.zero_grad()
         self.dp.begin()
-        out = self.losses(c1, c2, s)
+        out = losses(*args)
         out["loss"].backward()
         gscale = self.dp.finish()
         self.step_count += 1
