@@ -44,13 +44,20 @@ def margin(tag):
     named = dict(model.named_parameters())
     gmax = max(float(s[f"{tag}_gnorm/{n}"]) for n in names)
     gm, worst = 0.0, None
+    detail = []
     for n in names:
         gr = named[n].grad.detach().cpu().reshape(-1)
         gn = float(s[f"{tag}_gnorm/{n}"])
         tol = 1e-3 * gn + 1e-4 * gmax
-        e = max(abs(float(gr.double().norm()) - gn), float(np.abs(gr[s[f"{tag}_gidx/{n}"]].numpy() - s[f"{tag}_gval/{n}"]).max()))
+        en = abs(float(gr.double().norm()) - gn)
+        es = float(np.abs(gr[s[f"{tag}_gidx/{n}"]].numpy() - s[f"{tag}_gval/{n}"]).max())
+        e = max(en, es)
+        detail.append((e / tol, n, en / tol, es / tol))
         if e / tol > gm:
             gm, worst = e / tol, n
+    if os.environ.get("POLICY_DETAIL"):
+        for m, n, a, b in sorted(detail, reverse=True)[:4]:
+            print(f"    {n:32s} margin {m:.3f} (norm {a:.3f}, samples {b:.3f})")
     return lm, gm, worst
 
 

@@ -323,13 +323,15 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
     const int am = vst_mode_arith(mode);
     if (t256 && cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16)) cfg = T256;
-    // bf16x6 A-direct blocks for 64- and 192-row layers (VST_AD64 / VST_AD192: 0 off, 1 on,
-    // 2 data gradients only)
+    // bf16x6 A-direct blocks (VST_AD64 / VST_AD128 / VST_AD192 / VST_AD256: 0 off, 1 on, 2 data
+    // gradients only)
     auto env_mode = [](const char* n, int dflt) { const char* v = getenv(n); return v ? atoi(v) : dflt; };
-    static const int ad64 = env_mode("VST_AD64", 1), ad192 = env_mode("VST_AD192", 2), ad256 = env_mode("VST_AD256", 1);
+    static const int ad64 = env_mode("VST_AD64", 1), ad192 = env_mode("VST_AD192", 2), ad256 = env_mode("VST_AD256", 1),
+                     ad128 = env_mode("VST_AD128", 1);
     const bool dg = gmode == GM_TRANSPOSED;
     if (VST_ADIR && am == VST_GEMM_BF16X6) {
       if (cfg == T128 && M % 256 == 0 && (ad256 == 1 || (ad256 == 2 && dg))) cfg = T256A;
+      if (cfg == T128 && (ad128 == 1 || (ad128 == 2 && dg))) cfg = T128A;
       if ((cfg == T64W || cfg == T64) && (ad64 == 1 || (ad64 == 2 && dg))) cfg = T64A;
       if (cfg == T192 && (ad192 == 1 || (ad192 == 2 && dg))) cfg = T192A;
     }

@@ -497,7 +497,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 // tile configurations (BM x BN)
 // T64A / T192A / T256A: bf16x6 A-direct blocks of 2 / 6 / 8 waves (32 weight rows x 128 pixels per
 // wave)
-enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256, T64A, T192A, T256A };
+enum TileCfg { T32 = 0, T64, T96, T128, T192, T64W, T96W, T256, T64A, T192A, T256A, T128A };
 
 inline int select_cfg(int M) {
   if (M <= 32) return T32;
@@ -507,7 +507,7 @@ inline int select_cfg(int M) {
   return T128;
 }
 inline int cfg_bm(int c) {
-  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256, 64, 192, 256};
+  const int bm[] = {32, 64, 96, 128, 192, 64, 96, 256, 64, 192, 256, 128};
   return bm[c];
 }
 inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
@@ -570,9 +570,9 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
     case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
     case T96W: launch_k<1, 3, 4, 2, CF, GMK, 2, PR>(grid, st, P); break;
-    case T128:  // bf16x6: four A-direct waves of 32 rows x 128 pixels
+    case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR>(grid, st, P); break;
+    case T128A:  // four A-direct waves of 32 rows x 128 pixels
       if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
-      else launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
       if constexpr (PR == 1 || PR == 2) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR>(grid, st, P);
