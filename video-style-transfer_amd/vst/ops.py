@@ -36,8 +36,13 @@ def _check(t, name, ndim=None):
 
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
 KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
-KBLOCK_ON = os.environ.get("VST_KBLOCK", "1") != "0"  # A/B switch
-KBLOCK_STYLIZER = os.environ.get("VST_KBLOCK", "1") == "2"  # also inside the stylizer scope
+# where the channel-blocked K order applies (VST_KBLOCK): "res" (default) the loss networks, every
+# data gradient and the stylizer's residual-block forwards; "1" not inside the stylizer forward at
+# all; "2" everywhere (diagnostic: fails the ragged golden step, tools/policy_check.py); "0" off
+_KB = os.environ.get("VST_KBLOCK", "res")
+KBLOCK_ON = _KB != "0"
+KBLOCK_STYLIZER = _KB == "2"
+KBLOCK_RES = _KB in ("2", "res")
 # The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
@@ -156,11 +161,14 @@ def gemm_role(role):
         sc = sc.rpartition(".")[0] or None
     if m is None:
         m = GEMM_POLICY.get(role, _BASE_MODE[0])
-    # channel-blocked K order (VST_GEMM_KBLOCK) outside the stylizer: the frozen loss network's
-    # convs re-read their source rows from L2 instead of the Infinity Cache; the stylizer keeps the
-    # tap-major order its golden-gradient margins were measured in (tools/policy_check.py)
+    # channel-blocked K order (VST_GEMM_KBLOCK): consecutive k-tiles revisit the same 16 source
+    # channels over all taps, so the gathered rows come from L2 instead of the Infinity Cache.  The
+    # stylizer's forward keeps the tap-major order outside its residual blocks: there the blocked
+    # order moves the ragged golden step's IN-parameter gradients past the bar under bf16x6
+    # (margin 2.7; residual blocks alone: 0.000 -- tools/policy_check.py, VST_KBLOCK=2 / res)
     sc = _SCOPE[0]
-    if KBLOCK_ON and (KBLOCK_STYLIZER or not (sc is not None and sc.split(".")[0] == "stylizer")):
+    in_stylizer = sc is not None and sc.split(".")[0] == "stylizer"
+    if KBLOCK_ON and (KBLOCK_STYLIZER or not in_stylizer or (KBLOCK_RES and sc.startswith("stylizer.res"))):
         m |= KBLOCK
     _CUR[0] = m
     return m
