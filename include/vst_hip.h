@@ -163,10 +163,12 @@ int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, f
  * stats: [N*C][2] (mean, rstd) saved for backward. */
 int vst_instnorm_fwd(const float* x, const float* w, const float* b, const float* res, float* y, float* stats, int N,
                      int C, int HW, float eps, int relu, void* stream);
-/* partial: N*C*3 floats; gw, gb, gbias_prev (sum of gx = grad of the feeding conv's bias) may be NULL */
-int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* stats, const float* w, float* gx,
-                     float* gw, float* gb, float* gbias_prev, float* partial, int N, int C, int HW, int relu,
-                     int accumulate, void* stream);
+/* partial: N*C*3 floats; gw, gb, gbias_prev (sum of gx = grad of the feeding conv's bias) may be NULL.
+ * relu: the ReLU mask is y > 0 when y is given, else the pre-activation recomputed from x and b
+ * (bit-identical to the forward's; valid only when the forward had no residual add). */
+int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* b, const float* stats,
+                     const float* w, float* gx, float* gw, float* gb, float* gbias_prev, float* partial, int N, int C,
+                     int HW, int relu, int accumulate, void* stream);
 /* out[c] (+)= sum_{n,i} x[n][c][i]; partial: N*C floats (conv bias gradient) */
 int vst_channel_sum(const float* x, float* out, float* partial, int N, int C, int HW, int accumulate, void* stream);
 

@@ -24,6 +24,13 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
   return s;
 }
 
+// The pre-activation (x - mean) * rstd * w + b with fixed rounding (no contraction left to the
+// compiler): the backward recomputes it from x to get the ReLU mask instead of reading y, and must
+// reproduce the forward's sign bit for bit.
+__device__ __forceinline__ float in_affine(float x, float mean, float rstd, float w, float b) {
+  return __fmaf_rn(__fmul_rn(__fsub_rn(x, mean), rstd), w, b);
+}
+
 // y = [relu]( (x - mean) * rstd * w + b ) [+ res]
 __global__ __launch_bounds__(NTN) void in_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, const float* __restrict__ res,
@@ -70,7 +77,7 @@ __global__ __launch_bounds__(NTN) void in_fwd_kernel(const float* __restrict__ x
       float o[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        o[k] = (o[k] - mean) * rstd * wc + bc;
+        o[k] = in_affine(o[k], mean, rstd, wc, bc);
         if (relu) o[k] = fmaxf(o[k], 0.f);
       }
       if (rp) {
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(NTN) void in_fwd_kernel(const float* __restrict__ x
     }
   } else {
     for (int i = threadIdx.x; i < HW; i += NTN) {
-      float o = (xp[i] - mean) * rstd * wc + bc;
+      float o = in_affine(xp[i], mean, rstd, wc, bc);
       if (relu) o = fmaxf(o, 0.f);
       if (rp) o += rp[i];
       yp[i] = o;
@@ -94,8 +101,10 @@ __global__ __launch_bounds__(NTN) void in_fwd_kernel(const float* __restrict__ x
 
 // g = gy * (relu ? y > 0 : 1); xhat = (x-mean)*rstd
 // gx = rstd*w*(g - mean(g) - xhat*mean(g*xhat));  partial[plane] = {sum g*xhat, sum g, sum gx}
+// y == nullptr with relu: the mask is in_affine(x, ...) > 0 (no residual), one tensor less to read
 __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                                                     const float* __restrict__ y, const float* __restrict__ stats,
+                                                     const float* __restrict__ y, const float* __restrict__ bias,
+                                                     const float* __restrict__ stats,
                                                      const float* __restrict__ w, float* __restrict__ gx,
                                                      float* __restrict__ partial, int C, int HW, int relu) {
   __shared__ double sh[3][NTN / 64];
@@ -106,29 +115,40 @@ __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ g
   const float* yp = y + plane * HW;
   const float mean = stats[2 * plane], rstd = stats[2 * plane + 1];
   const bool v4 = (HW & 3) == 0;
-  auto load_g = [&](int i) -> float4 {  // masked gradient, 4 consecutive elements
+  const bool ymask = relu && y, amask = relu && !y;
+  const float wc = w[c], bc = amask ? bias[c] : 0.f;
+  auto load_g = [&](int i, const float4& xv) -> float4 {  // masked gradient, 4 consecutive elements
     float4 g = reinterpret_cast<const float4*>(gp)[i];
-    if (relu) {
+    if (ymask) {
       const float4 yv = reinterpret_cast<const float4*>(yp)[i];
       g.x = yv.x > 0.f ? g.x : 0.f;
       g.y = yv.y > 0.f ? g.y : 0.f;
       g.z = yv.z > 0.f ? g.z : 0.f;
       g.w = yv.w > 0.f ? g.w : 0.f;
+    } else if (amask) {
+      g.x = in_affine(xv.x, mean, rstd, wc, bc) > 0.f ? g.x : 0.f;
+      g.y = in_affine(xv.y, mean, rstd, wc, bc) > 0.f ? g.y : 0.f;
+      g.z = in_affine(xv.z, mean, rstd, wc, bc) > 0.f ? g.z : 0.f;
+      g.w = in_affine(xv.w, mean, rstd, wc, bc) > 0.f ? g.w : 0.f;
     }
+    return g;
+  };
+  auto mask1 = [&](int i, float g, float xv) -> float {
+    if (ymask) return yp[i] > 0.f ? g : 0.f;
+    if (amask) return in_affine(xv, mean, rstd, wc, bc) > 0.f ? g : 0.f;
     return g;
   };
   double sg = 0.0, sgx = 0.0;
   if (v4) {
     for (int i = threadIdx.x; i < HW / 4; i += NTN) {
-      const float4 g = load_g(i), xv = reinterpret_cast<const float4*>(xp)[i];
+      const float4 xv = reinterpret_cast<const float4*>(xp)[i], g = load_g(i, xv);
       sg += (double)g.x + (double)g.y + (double)g.z + (double)g.w;
       sgx += (double)g.x * ((xv.x - mean) * rstd) + (double)g.y * ((xv.y - mean) * rstd) +
              (double)g.z * ((xv.z - mean) * rstd) + (double)g.w * ((xv.w - mean) * rstd);
     }
   } else {
     for (int i = threadIdx.x; i < HW; i += NTN) {
-      float g = gp[i];
-      if (relu && !(yp[i] > 0.f)) g = 0.f;
+      const float g = mask1(i, gp[i], xp[i]);
       float xh = (xp[i] - mean) * rstd;
       sg += g;
       sgx += (double)g * xh;
@@ -137,12 +157,12 @@ __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ g
   sg = block_sum(sg, sh[0]);
   sgx = block_sum(sgx, sh[1]);
   const float mg = (float)(sg / HW), mgx = (float)(sgx / HW);
-  const float k = rstd * w[c];
+  const float k = rstd * wc;
   float* gxp = gx + plane * HW;
   double sgo = 0.0;
   if (v4) {
     for (int i = threadIdx.x; i < HW / 4; i += NTN) {
-      const float4 g = load_g(i), xv = reinterpret_cast<const float4*>(xp)[i];
+      const float4 xv = reinterpret_cast<const float4*>(xp)[i], g = load_g(i, xv);
       const float4 o = make_float4(k * (g.x - mg - (xv.x - mean) * rstd * mgx), k * (g.y - mg - (xv.y - mean) * rstd * mgx),
                                    k * (g.z - mg - (xv.z - mean) * rstd * mgx), k * (g.w - mg - (xv.w - mean) * rstd * mgx));
       reinterpret_cast<float4*>(gxp)[i] = o;
@@ -150,8 +170,7 @@ __global__ __launch_bounds__(NTN) void in_bwd_kernel(const float* __restrict__ g
     }
   } else {
     for (int i = threadIdx.x; i < HW; i += NTN) {
-      float g = gp[i];
-      if (relu && !(yp[i] > 0.f)) g = 0.f;
+      const float g = mask1(i, gp[i], xp[i]);
       float xh = (xp[i] - mean) * rstd;
       float o = k * (g - mg - xh * mgx);
       gxp[i] = o;
@@ -206,8 +225,8 @@ __global__ __launch_bounds__(NT) void in_fwd_reg_kernel(const float* __restrict_
   for (int j = 0; j < V4; ++j) {
     const int i = threadIdx.x + j * NT;
     if (i >= n4) break;
-    float o0 = (v[j].x - mean) * rstd * wc + bc, o1 = (v[j].y - mean) * rstd * wc + bc;
-    float o2 = (v[j].z - mean) * rstd * wc + bc, o3 = (v[j].w - mean) * rstd * wc + bc;
+    float o0 = in_affine(v[j].x, mean, rstd, wc, bc), o1 = in_affine(v[j].y, mean, rstd, wc, bc);
+    float o2 = in_affine(v[j].z, mean, rstd, wc, bc), o3 = in_affine(v[j].w, mean, rstd, wc, bc);
     if (relu) {
       o0 = fmaxf(o0, 0.f);
       o1 = fmaxf(o1, 0.f);
@@ -227,7 +246,8 @@ __global__ __launch_bounds__(NT) void in_fwd_reg_kernel(const float* __restrict_
 
 template <int NT, int V4, bool KEEPX>
 __global__ __launch_bounds__(NT) void in_bwd_reg_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                                                         const float* __restrict__ y, const float* __restrict__ stats,
+                                                         const float* __restrict__ y, const float* __restrict__ bias,
+                                                         const float* __restrict__ stats,
                                                          const float* __restrict__ w, float* __restrict__ gx,
                                                          float* __restrict__ partial, int C, int HW, int relu) {
   __shared__ double sh[3][NT / 64];
@@ -238,6 +258,8 @@ __global__ __launch_bounds__(NT) void in_bwd_reg_kernel(const float* __restrict_
   const float4* x4 = reinterpret_cast<const float4*>(x + plane * HW);
   const float4* y4 = reinterpret_cast<const float4*>(y + plane * HW);
   const float mean = stats[2 * plane], rstd = stats[2 * plane + 1];
+  const bool ymask = relu && y, amask = relu && !y;
+  const float wc = w[c], bc = amask ? bias[c] : 0.f;
   float4 g[V4], xh[KEEPX ? V4 : 1];
   double sg = 0.0, sgx = 0.0;
 #pragma unroll
@@ -247,12 +269,17 @@ __global__ __launch_bounds__(NT) void in_bwd_reg_kernel(const float* __restrict_
     if (i < n4) {
       gv = g4[i];
       xv = x4[i];
-      if (relu) {
+      if (ymask) {
         const float4 yv = y4[i];
         gv.x = yv.x > 0.f ? gv.x : 0.f;
         gv.y = yv.y > 0.f ? gv.y : 0.f;
         gv.z = yv.z > 0.f ? gv.z : 0.f;
         gv.w = yv.w > 0.f ? gv.w : 0.f;
+      } else if (amask) {
+        gv.x = in_affine(xv.x, mean, rstd, wc, bc) > 0.f ? gv.x : 0.f;
+        gv.y = in_affine(xv.y, mean, rstd, wc, bc) > 0.f ? gv.y : 0.f;
+        gv.z = in_affine(xv.z, mean, rstd, wc, bc) > 0.f ? gv.z : 0.f;
+        gv.w = in_affine(xv.w, mean, rstd, wc, bc) > 0.f ? gv.w : 0.f;
       }
       xv = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
     }
@@ -264,7 +291,7 @@ __global__ __launch_bounds__(NT) void in_bwd_reg_kernel(const float* __restrict_
   sg = block_sum<double, NT>(sg, sh[0]);
   sgx = block_sum<double, NT>(sgx, sh[1]);
   const float mg = (float)(sg / HW), mgx = (float)(sgx / HW);
-  const float k = rstd * w[c];
+  const float k = rstd * wc;
   float4* o4 = reinterpret_cast<float4*>(gx + plane * HW);
   double sgo = 0.0;
 #pragma unroll
@@ -335,16 +362,18 @@ int vst_instnorm_fwd(const float* x, const float* w, const float* b, const float
 
 // partial: workspace of N*C*3 floats. gw/gb: [C] weight/bias grads (accumulated if accumulate);
 // gbias_prev: optional [C] grad of the bias of the conv feeding this norm (sum of gx).
-int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* stats, const float* w, float* gx,
-                     float* gw, float* gb, float* gbias_prev, float* partial, int N, int C, int HW, int relu,
-                     int accumulate, void* stream) {
+// relu: the mask comes from y when y is given, else from the recomputed pre-activation with b
+// (valid when the forward had no residual add).
+int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* b, const float* stats,
+                     const float* w, float* gx, float* gw, float* gb, float* gbias_prev, float* partial, int N, int C,
+                     int HW, int relu, int accumulate, void* stream) {
   VST_CHECK_ARG(gy && x && stats && w && gx && partial && N > 0 && C > 0 && HW > 0);
-  VST_CHECK_ARG(!relu || y);
+  VST_CHECK_ARG(!relu || y || b);
   hipStream_t st = (hipStream_t)stream;
   if ((HW & 3) == 0 && HW <= NTN * 4 * 4)
-    in_bwd_reg_kernel<512, 4, true><<<N * C, 512, 0, st>>>(gy, x, y, stats, w, gx, partial, C, HW, relu);
+    in_bwd_reg_kernel<512, 4, true><<<N * C, 512, 0, st>>>(gy, x, y, b, stats, w, gx, partial, C, HW, relu);
   else
-    in_bwd_kernel<<<N * C, NTN, 0, st>>>(gy, x, y, stats, w, gx, partial, C, HW, relu);
+    in_bwd_kernel<<<N * C, NTN, 0, st>>>(gy, x, y, b, stats, w, gx, partial, C, HW, relu);
   sum_over_n_kernel<<<ceil_div(C, 256), 256, 0, st>>>(partial, N, C, 3, gw, gb, gbias_prev, accumulate);
   return vst_launch_status();
 }

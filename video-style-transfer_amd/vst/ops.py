@@ -174,6 +174,9 @@ def gemm_role(role):
     return m
 
 
+_IN_YMASK = os.environ.get("VST_IN_YMASK", "0") != "0"  # A/B: InstanceNorm backward reads the ReLU mask from y
+
+
 def pack_floats(Mpad, Kpad):
     """Floats of one packed A operand in the current mode (bf16x6 blocks are 96 B, others 64 B)."""
     return Kpad * Mpad * 3 // 2 if (gemm_mode() & ~KBLOCK) == 3 else Kpad * Mpad
@@ -555,7 +558,9 @@ class InstanceNormFn(Function):
         ctx.relu = relu
         ctx.has_res = res is not None
         ctx.params = (w, b, conv_bias)
-        ctx.save_for_backward(x, y if relu else None, stats, w)
+        # the backward recomputes the ReLU mask from x and b unless a residual was added after it
+        keep_y = relu and (res is not None or _IN_YMASK)
+        ctx.save_for_backward(x, y if keep_y else None, stats, w)
         return y
 
     @staticmethod
@@ -572,8 +577,9 @@ class InstanceNormFn(Function):
         gb = sb if direct else _empty((C,), x)
         gc = (sc if direct else _empty((C,), x)) if need_c else None
         part = _empty((N * C * 3,), x)
-        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(stats), ptr(w.contiguous()), ptr(gx), ptr(gw), ptr(gb),
-                             ptr(gc), ptr(part), N, C, H * W, int(ctx.relu), int(direct), stream())
+        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(ctx.params[1].contiguous()), ptr(stats), ptr(w.contiguous()),
+                             ptr(gx), ptr(gw), ptr(gb), ptr(gc), ptr(part), N, C, H * W, int(ctx.relu), int(direct),
+                             stream())
         gres = gy if ctx.has_res else None
         if direct:
             gw = gb = gc = None
