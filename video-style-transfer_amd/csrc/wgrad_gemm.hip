@@ -361,6 +361,9 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
 //   * both operands are split (per PREC) in registers and stored with one ds_write_b128 per
 //     section; 8 consecutive lanes take 8 consecutive LDS rows, so the 28- / 20-dword row stride
 //     puts them on 8 distinct 4-bank groups (conflict-free).
+#ifndef VST_WG_VEC
+#define VST_WG_VEC 1
+#endif
 struct Wg2Params {
   const float* a;    // [N][M][HWo]
   const float* src;  // [N][Cs][Hs][Ws]
@@ -480,9 +483,21 @@ __global__ __launch_bounds__(NT, MINW) void wgrad2_kernel(Wg2Params P) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 8 * e, 0, 0));
         } else {
+          // stride 1: the 8 source elements are contiguous -> two 16-byte loads (dword-aligned;
+          // gfx950 buffer loads take unaligned addresses)
           const int vo = ok ? (rowoff + xv0) * 4 : OOR;
+          if (VST_WG_VEC) {
+            const f32x4 a0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo, 0, 0));
+            const f32x4 a1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo + 16, 0, 0));
 #pragma unroll
-          for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 4 * e, 0, 0));
+            for (int e = 0; e < 4; ++e) {
+              rb[i][e] = a0[e];
+              rb[i][4 + e] = a1[e];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 4 * e, 0, 0));
+          }
         }
       } else {  // border window: per element
 #pragma unroll
