@@ -20,6 +20,9 @@ constexpr int BK = VST_CONV_BK;  // k-tile depth (multiple of 16)
 #ifndef VST_ABL
 #define VST_ABL 0
 #endif
+#ifndef VST_B4_SWZ
+#define VST_B4_SWZ 1
+#endif
 constexpr int ABL = VST_ABL;
 constexpr int NT = 256;
 
@@ -150,8 +153,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   const float* A = P.wpack + (long)n * P.a_batch_stride;
 
   // this thread's B column (fixed for the whole k loop)
-  const int bcol = tid % BN;
-  const int brow0 = tid / BN;
+  // ROWSTEP 4 (8-wave blocks; one ds_write_b64 per piece): lanes 8j..8j+7 of a 32-lane chunk take
+  // 8 consecutive columns with row group j, so each 16-lane store group hits 16 distinct 2-bank
+  // pairs (the plain tid % BN order put columns r and r+8 on the same banks: 2-way conflicts).
+  // The gather then reads 8 consecutive pixels per 8 lanes instead of 64 per wave.
+  const int bcol = (ROWSTEP == 4 && VST_B4_SWZ) ? ((tid & 7) | ((tid >> 5) << 3)) % BN : tid % BN;
+  const int brow0 = (ROWSTEP == 4 && VST_B4_SWZ) ? (tid >> 3) & 3 : tid / BN;
   const int krow0 = PREC ? brow0 * B_PER : brow0;
   const int p = p0 + bcol;
   const bool pvalid = p < HWo;
