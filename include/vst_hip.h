@@ -102,6 +102,11 @@ int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int p
  *   dgrad (thin Cout, stride 1): vst_unfold_kw(dy, sgn=-1, off=0, Wout=W+2p, zero) then
  *             vst_conv_dgrad_padout_kwu with A from vst_pack_weight_kwu(transposed=1), then
  *             vst_fold_border. */
+/* Direct 3x3 conv of a 3-channel image, stride 1, pad 1 (reflect or zero), out = [relu](conv + b) in
+ * exact fp32 on the VALU (VGG conv1_1, RC/network.py:17 / AA/vgg19.py:19; b may be NULL).
+ * w: [Cout][3][3][3] (PyTorch layout).  The output-write-bound layer skips the unfold + K = 48 GEMM. */
+int vst_conv_cin3_k3(const float* x, const float* w, const float* b, float* out, int N, int H, int W, int Cout,
+                     int reflect, int relu, void* stream);
 int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int Wout, int K, int Cu, int sgn, int off,
                   int reflect, void* stream);
 int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K, int Cu, int transposed, int Mpad,

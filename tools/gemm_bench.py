@@ -42,6 +42,9 @@ conv("deconv1", 16, 192, 64, 128, 96, 3, up=2)
 conv("deconv2", 16, 96, 128, 256, 48, 3, up=2)
 conv("conv2", 16, 48, 256, 512, 96, 3, stride=2)
 conv("conv3", 16, 96, 128, 256, 192, 3, stride=2)
+# VGG conv1_1 over the kw-unfolded input (3 channels x 3 kw, padded to 16): K = 48, output-bound
+# (KW = 1 with pad 1 shifts the columns by one -- same cost as the real pad_x = 0 launch)
+SHAPES.append(("vgg1_1u.fwd", 16, 16, 256, 512, 64, 3, 1, 256, 512, 1, 1, 1, 1, 2.0 * 16 * 64 * 256 * 512 * 48))
 
 
 def load(path):

@@ -370,6 +370,49 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   return vst_launch_status();
 }
 
+// Direct 3x3 convolution of a 3-channel image (VGG conv1_1: Conv2d(3, Cout, 3, padding=1) [+ReLU],
+// RC/network.py:17, AA/vgg19.py:19), stride 1, zero or reflect pad 1.  27 MACs per output: the
+// layer is bound by its output write, so it runs on the VALU in exact fp32 (fmaf chain from the
+// bias over (ci, kh, kw)) instead of an unfold pass + a K = 48 GEMM.  One thread per pixel, all
+// output channels; the 27 inputs stay in registers, the weights are wave-uniform (scalar loads),
+// each output plane is written by consecutive lanes (coalesced rows).
+template <bool REFLECT>
+__global__ __launch_bounds__(256) void cin3_conv3_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* __restrict__ out, int H,
+                                                         int W, int Cout, int relu) {
+  const int n = blockIdx.z, y = blockIdx.y;
+  const int px = blockIdx.x * 256 + threadIdx.x;
+  if (px >= W) return;
+  const float* xn = x + (long)n * 3 * H * W;
+  float v[27];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    int yy = y + kh - 1;
+    bool oky = true;
+    if (REFLECT) yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+    else oky = yy >= 0 && yy < H;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      int xx = px + kw - 1;
+      bool ok = oky;
+      if (REFLECT) xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+      else ok = ok && xx >= 0 && xx < W;
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) v[ci * 9 + kh * 3 + kw] = ok ? xn[((long)ci * H + yy) * W + xx] : 0.f;
+    }
+  }
+  float* o = out + ((long)n * Cout * H + y) * W + px;
+  const long cstride = (long)H * W;
+  for (int co = 0; co < Cout; ++co) {
+    const float* wc = w + co * 27;
+    float a = b ? b[co] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 27; ++t) a = fmaf(wc[t], v[t], a);
+    if (relu) a = fmaxf(a, 0.f);
+    o[co * cstride] = a;
+  }
+}
+
 extern "C" {
 
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
@@ -428,6 +471,16 @@ int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, f
   return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, 4 * Cin, K2 * K2 * Cout, Hc, Wc, K2, K2,
                           GM_TRANSPOSED, 1, 0, 0, 1, EPI_PHASE2, 0, nullptr, gmask, mode, stream, nullptr, nullptr, nullptr,
                           nullptr, border, H, W, pad);
+}
+
+int vst_conv_cin3_k3(const float* x, const float* w, const float* b, float* out, int N, int H, int W, int Cout,
+                     int reflect, int relu, void* stream) {
+  VST_CHECK_ARG(x && w && out && N > 0 && H > 1 && W > 1 && Cout > 0);
+  dim3 grid(ceil_div(W, 256), H, N);
+  hipStream_t st = (hipStream_t)stream;
+  if (reflect) cin3_conv3_kernel<true><<<grid, 256, 0, st>>>(x, w, b, out, H, W, Cout, relu);
+  else cin3_conv3_kernel<false><<<grid, 256, 0, st>>>(x, w, b, out, H, W, Cout, relu);
+  return vst_launch_status();
 }
 
 int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int Wout, int K, int Cu, int sgn, int off,

@@ -174,6 +174,7 @@ def gemm_role(role):
     return m
 
 
+CIN3_DIRECT = os.environ.get("VST_CIN3_DIRECT", "1") != "0"  # A/B: direct VALU kernel for 3-channel 3x3 convs
 _IN_YMASK = os.environ.get("VST_IN_YMASK", "0") != "0"  # A/B: InstanceNorm backward reads the ReLU mask from y
 
 
@@ -487,6 +488,12 @@ class Conv2dFn(Function):
         gemm_role("fwd_img" if Cin == 3 else "fwd")
         if rowsplit_ok(Cout, ks, stride, pad_mode, up) and pad == ks // 2:
             out = conv_fwd_rowsplit(x, w, bias, epi, aux)
+        elif CIN3_DIRECT and Cin == 3 and ks == 3 and stride == 1 and up == 1 and pad == 1 and act in (None, "relu") \
+                and H > 1 and W > 1:
+            # VGG conv1_1: 27 MACs per output, bound by the output write -> direct fp32 VALU kernel
+            out = _empty((N, Cout, Ho, Wo), x)
+            lib.vst_conv_cin3_k3(ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, Cout, int(pad_mode == "reflect"),
+                                 int(act == "relu"), stream())
         elif kwu_ok(Cin, ks, stride, up, W) and 0 < pad < min(H, W) and Ho == H and Wo == W:
             # thin input (3-channel frames): kw-unfold, then a Kx1 conv on the 16-channel k-tile path
             xu = unfold_kw(x, ks, -pad, 1, W, pad_mode == "reflect")
