@@ -372,6 +372,7 @@ struct Wg2Params {
   int Cs, Hs, Ws, Ho, Wo;
   int KH, KW, stride, pad, up;
   int S, chunk;
+  int asplit, Ha;  // row-split A (vst_conv_wgrad_rowsplit): m = co*asplit + kh reads a[co][oy-kh][ox], a has Ha rows
 };
 
 template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE>
@@ -402,21 +403,32 @@ __global__ __launch_bounds__(NT, MINW) void wgrad2_kernel(Wg2Params P) {
   const int r_end = min(HWo, r_begin + P.chunk);
   const int ntiles = r_end > r_begin ? (r_end - r_begin) / BK : 0;
   const int plane = P.Hs * P.Ws;
-  const float* a_n = P.a + (long)n * P.M * HWo;
+  const long a_img = P.asplit ? (long)(P.M / P.asplit) * P.Ha * P.Wo : (long)P.M * HWo;
+  const float* a_n = P.a + (long)n * a_img;
   const float* src_n = P.src + (long)n * P.Cs * plane;
-  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)((long)P.M * HWo * 4));
+  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)(a_img * 4));
   const __amdgpu_buffer_rsrc_t bsrd = uniform_rsrc(src_n, (uint32_t)((long)P.Cs * plane * 4));
   const int Hv = P.Hs * P.up, Wv = P.Ws * P.up, sh = P.up - 1;
 
-  // A tasks: (row, half) with 8 consecutive lanes on 8 consecutive rows of one half
-  int a_voff[A_IT], a_row[A_IT], a_half[A_IT];
+  // A tasks: (row, half) with 8 consecutive lanes on 8 consecutive rows of one half.  Row-split A:
+  // a_voff is the (possibly negative) byte offset of a[co][-kh][8*half]; per tile the row oy - kh
+  // is checked and the tile offset added in the vector offset
+  int a_voff[A_IT], a_row[A_IT], a_half[A_IT], a_kh[A_IT];
 #pragma unroll
   for (int i = 0; i < A_IT; ++i) {
     const int q = tid + i * NT;
     a_row[i] = (q & 7) + 8 * (q >> 4);
     a_half[i] = (q >> 3) & 1;
     const int m = m0 + a_row[i];
-    a_voff[i] = (q < A_TASKS && m < P.M) ? (m * HWo + 8 * a_half[i]) * 4 : OOR;
+    const bool ok = q < A_TASKS && m < P.M;
+    if (P.asplit) {
+      const int co = m / P.asplit, kh = m - co * P.asplit;
+      a_kh[i] = ok ? kh : -(1 << 20);  // an invalid row never passes the per-tile row check
+      a_voff[i] = ((co * P.Ha - kh) * P.Wo + 8 * a_half[i]) * 4;
+    } else {
+      a_kh[i] = 0;
+      a_voff[i] = ok ? (m * HWo + 8 * a_half[i]) * 4 : OOR;
+    }
   }
   // B tasks: column c = q % BN (consecutive lanes -> consecutive columns), half = q / BN
   int b_col[B_IT], b_half[B_IT], b_kh[B_IT], b_kw[B_IT], b_cbase[B_IT];
@@ -453,8 +465,15 @@ __global__ __launch_bounds__(NT, MINW) void wgrad2_kernel(Wg2Params P) {
     const int soff = __builtin_amdgcn_readfirstlane((r_begin + t * BK) * 4);
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
-      ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], soff, 0));
-      ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i] + 16, soff, 0));
+      if (P.asplit) {  // wave-uniform branch
+        const int ya = t_oy - a_kh[i];
+        const int vo = (ya >= 0 && ya < P.Ha) ? a_voff[i] + soff : OOR;
+        ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo, 0, 0));
+        ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo + 16, 0, 0));
+      } else {
+        ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], soff, 0));
+        ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i] + 16, soff, 0));
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
@@ -757,11 +776,12 @@ static void launch_wg2(int c, dim3 g, int mode, hipStream_t st, const Wg2Params&
   }
 }
 
-// row-tiled kernel applies: plain (not row-split) gather, output rows a multiple of 16 wide, and
+// row-tiled kernel applies: output rows a multiple of 16 wide (plain or row-split A gather), and
 // every source offset within the 2^31 B buffer range
 static bool wg2_ok(int asplit, int Wo) {
   static const bool off = getenv("VST_WGRAD2") && atoi(getenv("VST_WGRAD2")) == 0;  // A/B switch
-  return !off && !asplit && Wo % BK == 0;
+  static const bool rs = !getenv("VST_WGRAD2_RS") || atoi(getenv("VST_WGRAD2_RS")) != 0;  // row-split A/B switch
+  return !off && (!asplit || rs) && Wo % BK == 0;
 }
 
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
@@ -788,6 +808,8 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     Q.pad = pad;
     Q.up = up;
     Q.S = S;
+    Q.asplit = asplit;
+    Q.Ha = Ha;
     Q.chunk = ((Ho * Wo + S - 1) / S + BK - 1) / BK * BK;
     dim3 g(Q.Jpad / WBN, Q.Mpad / wbm(c), N * S);
     if (gmode == 0) launch_wg2<0>(c, g, mode, st, Q);
