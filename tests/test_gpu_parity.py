@@ -74,6 +74,7 @@ CONV_CASES = [
     (2, 192, 9, 15, 192, 3, 1, "reflect", 1, None),   # residual conv, ragged
     (2, 192, 5, 8, 96, 3, 1, "reflect", 2, None),     # deconv1 (nearest x2 upsample)
     (1, 96, 9, 6, 48, 3, 1, "reflect", 2, None),      # deconv2
+    (1, 40, 7, 33, 24, 3, 1, "reflect", 2, None),     # upsample conv, (W+1) over two k-tiles, odd H
     (2, 48, 16, 20, 3, 9, 1, "reflect", 1, "tanh"),   # deconv3 ConvTanh (Cout=3)
     (2, 3, 12, 20, 64, 3, 1, "zero", 1, "relu"),      # VGG conv1_1
     (2, 64, 8, 12, 128, 3, 1, "zero", 1, "relu"),     # VGG conv

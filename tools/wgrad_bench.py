@@ -24,6 +24,9 @@ SHAPES = [
     ("conv2", 16, 48, 256, 512, 96, 3, 2, 0, 1, 1),
     ("conv3", 16, 96, 128, 256, 192, 3, 2, 0, 1, 1),
     ("conv1", 16, 3, 256, 512, 48, 9, 1, 0, 4, 1),
+    # the nearest-x2 layers through the phase-stacked source-grid GEMM (vst_conv_wgrad_up2)
+    ("deconv1_p", 16, 192, 64, 128, 96, 3, 1, 0, 1, 2),
+    ("deconv2_p", 16, 96, 128, 256, 48, 3, 1, 0, 1, 2),
 ]
 
 
@@ -50,7 +53,10 @@ def main():
         x = torch.randn(N, Cin, H, W, device="cuda")
         dy = torch.randn(N, Cout, Ho, Wo, device="cuda")
         dw = torch.empty(Cout, Cin, k, k, device="cuda")
-        ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout, k * k * Cin, Ho * Wo), device="cuda")
+        if name.endswith("_p"):
+            ws = torch.empty(libs[0].vst_conv_wgrad_up2_workspace(N, Cin, H, W, Cout), device="cuda")
+        else:
+            ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout, k * k * Cin, Ho * Wo), device="cuda")
         bufs[name] = (x, dy, dw, ws, Ho, Wo, 2.0 * N * Cout * Ho * Wo * Cin * k * k)
     for _ in range(5):
         for p, lib in zip(paths, libs):
@@ -59,11 +65,16 @@ def main():
                 x, dy, dw, ws, Ho, Wo, fl = bufs[name]
                 args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, Ho, Wo, k, k, gm,
                         stride, pad, up, 0, MODE, st)
-                lib.vst_conv_wgrad(*args)
+                if name.endswith("_p"):
+                    args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, 0, MODE, st)
+                    fn = lib.vst_conv_wgrad_up2
+                else:
+                    fn = lib.vst_conv_wgrad
+                assert fn(*args) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(5):
-                    lib.vst_conv_wgrad(*args)
+                    fn(*args)
                 e1.record()
                 torch.cuda.synchronize()
                 res[(p, name)].append(e0.elapsed_time(e1) / 5)

@@ -394,11 +394,16 @@ def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
     return dx
 
 
+_WGRAD_UP2 = os.environ.get("VST_WGRAD_UP2", "1") != "0"  # A/B switch for the phase-stacked up2 path
+
+
 def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     gemm_role("wgrad")
     N, Cin, H, W = x.shape
     Cout = w_shape[0]
     Ho, Wo = gz.shape[2:]
+    if _WGRAD_UP2 and up == 2 and ks == 3 and stride == 1 and pad == 1 and pad_mode == "reflect":
+        return conv_wgrad_up2(gz, x, w_shape, out)
     ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
@@ -406,6 +411,21 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
                       ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), gemm_mode())
     lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
                        GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), gemm_mode(), stream())
+    kprof.end(tok, family="wgrad")
+    return dw
+
+
+def conv_wgrad_up2(gz, x, w_shape, out=None):
+    """Weight gradient of UpsampleConvLayer (nearest x2, reflect pad 1, k3; RC/network.py:114-120)
+    as the phase-stacked source-grid GEMM (vst_conv_wgrad_up2)."""
+    N, Cin, H, W = x.shape
+    Cout = w_shape[0]
+    ws = _empty((lib.vst_conv_wgrad_up2_workspace(N, Cin, H, W, Cout),), x)
+    acc = out is not None
+    dw = _empty(w_shape, x) if out is None else out
+    tok = kprof.begin(2.0 * N * Cout * 4 * H * W * Cin * 9, 4.0 * (gz.numel() + x.numel() + dw.numel()),
+                      ("wgrad_up2", N, Cin, H, W, Cout), gemm_mode())
+    lib.vst_conv_wgrad_up2(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, int(acc), gemm_mode(), stream())
     kprof.end(tok, family="wgrad")
     return dw
 
