@@ -156,6 +156,14 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
 int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
                             int W, int Cout, int K, int accumulate, int mode, void* stream);
 
+/* forward of nearest-x2 upsample -> ReflectionPad2d(1) -> Conv2d(k3, stride 1) [+bias]
+ * (UpsampleConvLayer, RC/network.py:114-120; replaces F.interpolate + pad + conv2d): one
+ * phase-stacked 2x2 GEMM over the (H+1) x (W+1) source grid (2.25x fewer MACs).
+ * w2 [4*Cout][Cin][2][2] = vst_up2_phase_weights(w [Cout][Cin][3][3]); wpack = vst_pack_weight of
+ * w2 (Cout' = 4*Cout, KH = KW = 2, same mode); out [N][Cout][2H][2W] */
+int vst_up2_phase_weights(const float* w, float* w2, int Cout, int Cin, void* stream);
+int vst_conv_up2_fwd(const float* x, const float* wpack, const float* bias, float* out, int N, int Cin, int H, int W,
+                     int Cout, int mode, void* stream);
 /* weight gradient of nearest-x2 upsample -> ReflectionPad2d(1) -> Conv2d(k=3, stride 1)
  * (UpsampleConvLayer, RC/network.py:114-120; replaces autograd's conv2d weight backward of that
  * layer): one phase-stacked 2x2 GEMM on the source grid, 2.25x fewer MACs than the virtual-grid

@@ -473,6 +473,48 @@ int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, f
                           nullptr, border, H, W, pad);
 }
 
+// Forward of nearest-x2 upsample -> ReflectionPad2d(1) -> Conv2d(k3, stride 1) (UpsampleConvLayer,
+// RC/network.py:114-120) as ONE phase-stacked 2x2 GEMM on the source grid: output pixel (2i'-a, 2j'-b)
+// = sum_{eh,ew,ci} W2[(co, 1-a, 1-b)][ci][eh][ew] * x[ci][clamp(i'-1+eh)][clamp(j'-1+ew)] over the
+// (H+1) x (W+1) grid of (i', j'); the reflect border of the virtual grid is the edge clamp, W2 holds
+// the phase's tap sums (vst_up2_phase_weights).  16 instead of 36 MACs per (co, ci, source pixel);
+// the EPI_PHASE2 epilogue scatters the four phase rows of each channel to their output pixels (+bias).
+__global__ void up2_phase_weights_kernel(const float* __restrict__ w, float* __restrict__ w2, int Cout, int Cin) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over [Cout][4][Cin][2][2]
+  const long total = (long)Cout * 16 * Cin;
+  if (idx >= total) return;
+  const int ew = (int)(idx & 1), eh = (int)((idx >> 1) & 1);
+  long t = idx >> 2;
+  const int ci = (int)(t % Cin);
+  t /= Cin;
+  const int ph = (int)(t & 3), co = (int)(t >> 2);
+  const int a = 1 - (ph >> 1), b = 1 - (ph & 1);  // row phase (a', b') = (1-a, 1-b)
+  const float* wc = w + ((long)co * Cin + ci) * 9;
+  float s = 0.f;
+  for (int kh = 0; kh < 3; ++kh) {
+    if (((a + kh + 1) >> 1) - a != eh) continue;
+    for (int kw = 0; kw < 3; ++kw)
+      if (((b + kw + 1) >> 1) - b == ew) s += wc[kh * 3 + kw];
+  }
+  w2[idx] = s;
+}
+
+int vst_up2_phase_weights(const float* w, float* w2, int Cout, int Cin, void* stream) {
+  VST_CHECK_ARG(w && w2 && Cout > 0 && Cin > 0);
+  const long total = (long)Cout * 16 * Cin;
+  up2_phase_weights_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(w, w2, Cout, Cin);
+  return vst_launch_status();
+}
+
+int vst_conv_up2_fwd(const float* x, const float* wpack, const float* bias, float* out, int N, int Cin, int H, int W,
+                     int Cout, int mode, void* stream) {
+  VST_CHECK_ARG(vst_mode_ok(mode));
+  VST_CHECK_ARG(x && wpack && out && N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0);
+  return conv_gemm_launch(x, wpack, bias, nullptr, out, N, Cin, H, W, 4 * Cout, 4 * Cin, H + 1, W + 1, 2, 2, GM_CLAMP,
+                          1, 1, 1, 1, EPI_PHASE2 | (bias ? EPI_BIAS : 0), 0, nullptr, nullptr, mode, stream, nullptr,
+                          nullptr, nullptr, nullptr, nullptr, 2 * H, 2 * W, 1);
+}
+
 int vst_conv_cin3_k3(const float* x, const float* w, const float* b, float* out, int N, int H, int W, int Cout,
                      int reflect, int relu, void* stream) {
   VST_CHECK_ARG(x && w && out && N > 0 && H > 1 && W > 1 && Cout > 0);

@@ -46,6 +46,8 @@ struct ConvParams {
   // EPI_PHASE2 (stride-2 data gradient, all four parity phases in one GEMM): row m = ci*4 + 2a + b,
   // pixel (I, J) of the phase grid -> padded-grid position (2I + a, 2J + b); interior positions go
   // straight to dx [N][M/4][ph_H][ph_W], the reflect-pad border to ph_border [N][M/4][Hp][Wp].
+  // (The nearest-x2 forward, vst_conv_up2_fwd, uses the same map with ph_pad = 1, + bias, and no
+  // border buffer: its out-of-range phase positions are dropped.)
   // EPI_PADOUT (stride-1 data gradient over the padded grid): row m = ci, pixel (u, v) of the
   // padded grid, same interior / border split.
   float* ph_border;
@@ -54,7 +56,7 @@ struct ConvParams {
   int kb;  // channel-blocked K order (VST_GEMM_KBLOCK, vst_common.h kdecode)
 };
 
-enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2 };
+enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2, GM_CLAMP = 3 };
 enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32, EPI_PHASE2 = 64, EPI_PADOUT = 128 };
 
 // source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
@@ -79,6 +81,9 @@ __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox
     y = y >= Hv ? 2 * Hv - 2 - y : y;
     x = abs(x);
     x = x >= Wv ? 2 * Wv - 2 - x : x;
+  } else if (P.gmode == GM_CLAMP) {  // edge clamp (phase-stacked nearest-x2 forward, vst_conv_up2_fwd)
+    y = min(max(y, 0), Hv - 1);
+    x = min(max(x, 0), Wv - 1);
   } else {
     ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
   }
@@ -458,10 +463,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
             const int u = ph2 ? 2 * I + (r >> 1) : I, v = ph2 ? 2 * J + (r & 1) : J;
             if (ci >= Cx) continue;
             const int y = u - P.ph_pad, x = v - P.ph_pad;
-            const float val = acc[i][j][4 * g + r];
+            const float val = acc[i][j][4 * g + r] + ((P.epi & EPI_BIAS) ? P.bias[ci] : 0.f);
             if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W)
               dx_n[((long)ci * P.ph_H + y) * P.ph_W + x] = val;
-            else if (u < Hp && v < Wp)
+            else if (P.ph_border && u < Hp && v < Wp)
               bd_n[((long)ci * Hp + u) * Wp + v] = val;
           }
         }

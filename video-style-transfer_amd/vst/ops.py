@@ -174,6 +174,7 @@ def gemm_role(role):
     return m
 
 
+UP2_FWD = os.environ.get("VST_UP2_FWD", "1") != "0"  # A/B: phase-stacked nearest-x2 forward
 CIN3_DIRECT = os.environ.get("VST_CIN3_DIRECT", "1") != "0"  # A/B: direct VALU kernel for 3-channel 3x3 convs
 _IN_YMASK = os.environ.get("VST_IN_YMASK", "0") != "0"  # A/B: InstanceNorm backward reads the ReLU mask from y
 
@@ -514,6 +515,16 @@ class Conv2dFn(Function):
             out = _empty((N, Cout, Ho, Wo), x)
             lib.vst_conv_cin3_k3(ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, Cout, int(pad_mode == "reflect"),
                                  int(act == "relu"), stream())
+        elif UP2_FWD and up == 2 and ks == 3 and stride == 1 and pad == 1 and pad_mode == "reflect" and act is None:
+            # UpsampleConvLayer: phase-stacked 2x2 GEMM on the source grid (tap-summed weights)
+            w2 = _empty((4 * Cout, Cin, 2, 2), w)
+            lib.vst_up2_phase_weights(ptr(w), ptr(w2), Cout, Cin, stream())
+            out = _empty((N, Cout, Ho, Wo), x)
+            wp = packed_weight(w2, False)
+            tok = kprof.begin(2.0 * N * Cout * Ho * Wo * Cin * ks * ks, 4.0 * (x.numel() + wp.numel() + out.numel()),
+                              (N, Cin, H, W, 4 * Cout, H + 1, W + 1, 2, 2, 3, 1, 1, 1), gemm_mode())
+            lib.vst_conv_up2_fwd(ptr(x), ptr(wp), ptr(bias), ptr(out), N, Cin, H, W, Cout, gemm_mode(), stream())
+            kprof.end(tok)
         elif kwu_ok(Cin, ks, stride, up, W) and 0 < pad < min(H, W) and Ho == H and Wo == W:
             # thin input (3-channel frames): kw-unfold, then a Kx1 conv on the 16-channel k-tile path
             xu = unfold_kw(x, ks, -pad, 1, W, pad_mode == "reflect")
