@@ -21,5 +21,5 @@ for blk in notes.split("- .agpr_count")[1:]:
         continue
     g = lambda k: (re.search(r"\." + k + r":\s+(\S+)", blk) or [None, "?"])[1]  # noqa: E731
     dem = subprocess.check_output(["c++filt", name], text=True).strip().replace("(anonymous namespace)::", "")
-    print(f"vgpr {g('vgpr_count'):>4} spill {g('vgpr_spill_count'):>3} scratch {g('private_segment_fixed_size'):>4} "
+    print(f"vgpr {g('vgpr_count'):>4} agpr {blk.split(chr(10))[0].split(':')[-1].strip():>4} spill {g('vgpr_spill_count'):>3} scratch {g('private_segment_fixed_size'):>4} "
           f"lds {g('group_segment_fixed_size'):>6}  {dem[:100]}")

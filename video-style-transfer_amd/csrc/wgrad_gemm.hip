@@ -364,6 +364,9 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
 #ifndef VST_WG_VEC
 #define VST_WG_VEC 1
 #endif
+#ifndef VST_WABL
+#define VST_WABL 0  // timing-ablation builds: 1 no A split, 2 no B split, 3 neither (results wrong)
+#endif
 struct Wg2Params {
   const float* a;    // [N][M][HWo]
   const float* src;  // [N][Cs][Hs][Ws]
@@ -456,13 +459,15 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x4 ra[A_IT][2];
-  float rb[B_IT][8];
+  f32x4 RA[1][A_IT][2];  // the prefetched tile's registers
+  float RB[1][B_IT][8];
   // tile position (scalar): output row oy, first column ox0
   int t_oy = __builtin_amdgcn_readfirstlane(r_begin / P.Wo);
   int t_ox = __builtin_amdgcn_readfirstlane(r_begin - t_oy * P.Wo);
 
-  auto load_tile = [&](int t) {
+  auto load_tile = [&](int s, int t) {
+    auto& ra = RA[s];
+    auto& rb = RB[s];
     const int soff = __builtin_amdgcn_readfirstlane((r_begin + t * BK) * 4);
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
@@ -542,7 +547,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   };
 
   // 8 consecutive k (pixels 8*half .. 8*half+7) of one LDS row, in the layout of PREC
-  auto store8 = [&](float* row, int half, const float* v) {
+  auto store8 = [&](float* row, int half, const float* v, bool isA) {
+    if (VST_WABL && (VST_WABL == 3 || (VST_WABL == 1) == isA)) {  // timing ablation: no split (wrong results)
+      uint32_t* d = reinterpret_cast<uint32_t*>(row) + 4 * half;
+      const u32x4 x0 = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+      const u32x4 x1 = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
+      *reinterpret_cast<u32x4*>(d) = x0;
+      *reinterpret_cast<u32x4*>(d + 8) = x1;
+      if (PREC == 3) *reinterpret_cast<u32x4*>(d + 16) = x0;
+      return;
+    }
     if constexpr (PREC == 0) {  // fp32 [hi][s]: k = 2s + hi -> even k at dwords 4*half.., odd at 8 + 4*half..
       *reinterpret_cast<f32x4*>(row + 4 * half) = f32x4{v[0], v[2], v[4], v[6]};
       *reinterpret_cast<f32x4*>(row + 8 + 4 * half) = f32x4{v[1], v[3], v[5], v[7]};
@@ -563,18 +577,20 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int s) {
+    auto& ra = RA[s];
+    auto& rb = RB[s];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) {
         const float v[8] = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
                             ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
-        store8(&As[buf][a_row[i]][0], a_half[i], v);
+        store8(&As[buf][a_row[i]][0], a_half[i], v, true);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i)
-      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][b_col[i]][0], b_half[i], rb[i]);
+      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][b_col[i]][0], b_half[i], rb[i], false);
   };
   auto advance = [&]() {
     t_ox += BK;
@@ -584,19 +600,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     }
   };
 
-  if (ntiles > 0) {
-    load_tile(0);
-    advance();
-    store_tile(0);
-  }
-  __syncthreads();
   const int lo = lane & 31, hi = lane >> 5;
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) {
-      load_tile(t + 1);
-      advance();
-    }
+  auto mfma_tile = [&](int buf) {
     if constexpr (PREC == 3) {
       mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
     } else if constexpr (PREC != 0) {
@@ -624,7 +629,22 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
             acc[i][j] =
                 __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < ntiles) store_tile(buf ^ 1);
+  };
+
+  if (ntiles > 0) {
+    load_tile(0, 0);
+    advance();
+    store_tile(0, 0);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) {
+      load_tile(0, t + 1);
+      advance();
+    }
+    mfma_tile(buf);
+    if (t + 1 < ntiles) store_tile(buf ^ 1, 0);
     __syncthreads();
   }
 
@@ -883,21 +903,46 @@ static int splits_for(int N, int M, long J, int HWo) {
 // gives every (phase, tap) product: 16 (phase, e) pairs per (co, ci) instead of the 36 (phase, tap)
 // pairs of the virtual-grid GEMM (2.25x fewer MACs), with M = 4*Cout rows (48 -> 192, 96 -> 384)
 // filling whole tiles.  dW[co][ci][kh][kw] = sum_{a,b} P[(co,a,b)][(e(a,kh), e(b,kw), ci)].
+// one thread per (nc, a, i', 4-column group j'..j'+3): both b planes from the dy row 2i'-a
+// (two aligned float4 + one scalar load, two float4 stores)
 __global__ void up2_phase_planes_kernel(const float* __restrict__ dy, float* __restrict__ A, long NC, int H, int W,
                                         int Wp) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = NC * 4 * (H + 1) * Wp;
+  const int Wq = Wp >> 2;
+  const long total = NC * 2 * (H + 1) * Wq;
   if (idx >= total) return;
-  const int j = (int)(idx % Wp);
-  long t = idx / Wp;
+  const int jq = (int)(idx % Wq);
+  long t = idx / Wq;
   const int i = (int)(t % (H + 1));
   t /= H + 1;
-  const int ph = (int)(t & 3);
-  const long nc = t >> 2;
-  const int y = 2 * i - (ph >> 1), x = 2 * j - (ph & 1);
-  float v = 0.f;
-  if (y >= 0 && y < 2 * H && x >= 0 && x < 2 * W) v = dy[(nc * 2 * H + y) * 2 * W + x];
-  A[idx] = v;
+  const int a = (int)(t & 1);
+  const long nc = t >> 1;
+  const int y = 2 * i - a, j = 4 * jq, W2 = 2 * W;
+  float e[9];  // dy[y][2j - 1 .. 2j + 7]
+  if (y >= 0 && y < 2 * H) {
+    const float* row = dy + (nc * 2 * H + y) * W2;
+    if (2 * j + 8 <= W2) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(row + 2 * j);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(row + 2 * j + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        e[1 + q] = v0[q];
+        e[5 + q] = v1[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) e[1 + q] = 2 * j + q < W2 ? row[2 * j + q] : 0.f;
+    }
+    e[0] = (j > 0 && 2 * j - 1 < W2) ? row[2 * j - 1] : 0.f;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) e[q] = 0.f;
+  }
+  // plane (a, b) row i: element j' = dy[y][2j' - b]
+  float* p0 = A + (((nc * 4 + 2 * a) * (H + 1) + i) * Wp + j);
+  float* p1 = p0 + (long)(H + 1) * Wp;
+  *reinterpret_cast<f32x4*>(p0) = f32x4{e[1], e[3], e[5], e[7]};
+  *reinterpret_cast<f32x4*>(p1) = f32x4{e[0], e[2], e[4], e[6]};
 }
 
 __global__ void up2_wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int Cout,
@@ -952,7 +997,7 @@ int vst_conv_wgrad_up2(const float* dy, const float* x, float* dw, float* worksp
   float* slab = workspace;
   float* planes = workspace + (long)N * S * Mpad * Jpad;
   hipStream_t st = (hipStream_t)stream;
-  const long np = (long)N * M * Hq * Wp;
+  const long np = (long)N * Cout * 2 * Hq * (Wp / 4);
   up2_phase_planes_kernel<<<ceil_div(np, 256), 256, 0, st>>>(dy, planes, (long)N * Cout, H, W, Wp);
   int rc = vst_launch_status();
   if (rc) return rc;
