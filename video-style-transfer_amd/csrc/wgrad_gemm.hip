@@ -384,7 +384,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int LS = PREC == 3 ? 28 : 20;
-  constexpr int A_TASKS = 2 * BM, A_IT = (A_TASKS + NTH - 1) / NTH;
+  // A task = AQ consecutive pixels of one dY row.  8 (two float4) unless 2*BM tasks would leave
+  // some waves with one task more than others (the 192-row tile: 384 tasks on 256 threads): then 4,
+  // so every thread splits the same number of elements (3 x 4 A + 8 B) and no wave waits at the
+  // barrier for the others' extra split work
+  constexpr int AQ = ((2 * BM) % NTH != 0 && (4 * BM) % NTH == 0) ? 4 : 8;
+  constexpr int APARTS = BK / AQ;
+  constexpr int A_TASKS = APARTS * BM, A_IT = (A_TASKS + NTH - 1) / NTH;
   constexpr int B_TASKS = 2 * BN, B_IT = (B_TASKS + NTH - 1) / NTH;
   constexpr int OOR = 0x7ffffff0;
   static_assert(BK == 16, "16-pixel k-tiles");
@@ -421,17 +427,17 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
   for (int i = 0; i < A_IT; ++i) {
     const int q = tid + i * NTH;
-    a_row[i] = (q & 7) + 8 * (q >> 4);
-    a_half[i] = (q >> 3) & 1;
+    a_row[i] = (q & 7) + 8 * (q / (8 * APARTS));
+    a_half[i] = (q >> 3) % APARTS;  // part index (half for AQ = 8, quarter for AQ = 4)
     const int m = m0 + a_row[i];
     const bool ok = q < A_TASKS && m < P.M;
     if (P.asplit) {
       const int co = m / P.asplit, kh = m - co * P.asplit;
       a_kh[i] = ok ? kh : -(1 << 20);  // an invalid row never passes the per-tile row check
-      a_voff[i] = ((co * P.Ha - kh) * P.Wo + 8 * a_half[i]) * 4;
+      a_voff[i] = ((co * P.Ha - kh) * P.Wo + AQ * a_half[i]) * 4;
     } else {
       a_kh[i] = 0;
-      a_voff[i] = ok ? (m * HWo + 8 * a_half[i]) * 4 : OOR;
+      a_voff[i] = ok ? (m * HWo + AQ * a_half[i]) * 4 : OOR;
     }
   }
   // B tasks: column c = q % BN (consecutive lanes -> consecutive columns), half = q / BN
@@ -475,10 +481,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
         const int ya = t_oy - a_kh[i];
         const int vo = (ya >= 0 && ya < P.Ha) ? a_voff[i] + soff : OOR;
         ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo, 0, 0));
-        ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo + 16, 0, 0));
+        if (AQ == 8) ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo + 16, 0, 0));
       } else {
         ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], soff, 0));
-        ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i] + 16, soff, 0));
+        if (AQ == 8)
+          ra[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i] + 16, soff, 0));
       }
     }
 #pragma unroll
@@ -577,12 +584,36 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
     }
   };
+  // 4 consecutive k (pixels 4*part .. 4*part+3) of one LDS row: one ds_write_b64 per section
+  // (8 consecutive lanes on 8 rows 28 / 20 dwords apart, two parts per 16-lane group: distinct banks)
+  auto store4 = [&](float* row, int part, const f32x4& v) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(row) + 2 * part;
+    if constexpr (PREC == 0) {
+      *reinterpret_cast<f32x2*>(row + 2 * part) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(row + 8 + 2 * part) = f32x2{v[1], v[3]};
+    } else if constexpr (PREC == 3) {
+      uint32_t h0, m0, l0, h1, m1, l1;
+      split3_bf16x2(v[0], v[1], h0, m0, l0);
+      split3_bf16x2(v[2], v[3], h1, m1, l1);
+      *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(d + 8) = u32x2{m0, m1};
+      *reinterpret_cast<u32x2*>(d + 16) = u32x2{l0, l1};
+    } else {
+      uint32_t h0, l0, h1, l1;
+      split_bf16x2(v[0], v[1], h0, l0);
+      split_bf16x2(v[2], v[3], h1, l1);
+      *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
+      if (PREC == 1) *reinterpret_cast<u32x2*>(d + 8) = u32x2{l0, l1};
+    }
+  };
   auto store_tile = [&](int buf, int s) {
     auto& ra = RA[s];
     auto& rb = RB[s];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
-      if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) {
+      if (AQ == 4) {
+        if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) store4(&As[buf][a_row[i]][0], a_half[i], ra[i][0]);
+      } else if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) {
         const float v[8] = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
                             ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
         store8(&As[buf][a_row[i]][0], a_half[i], v, true);
