@@ -693,7 +693,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   }
 }
 
-enum { W32 = 0, W64, W96, W128, W192 };
+enum { W32 = 0, W64, W96, W128, W192, W64N, W96N };  // *N: 256-column variants (row-tiled kernel only)
 static int wsel(int M) {
   if (M <= 32) return W32;
   if (M <= 64) return W64;
@@ -818,6 +818,8 @@ static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
     case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
     case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
     case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
+    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
     default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
   }
 }
@@ -867,10 +869,17 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     Q.asplit = asplit;
     Q.Ha = Ha;
     Q.chunk = ((Ho * Wo + S - 1) / S + BK - 1) / BK * BK;
-    dim3 g(Q.Jpad / WBN, Q.Mpad / wbm(c), N * S);
-    if (gmode == 0) launch_wg2<0>(c, g, mode, st, Q);
-    else if (gmode == 2) launch_wg2<2>(c, g, mode, st, Q);
-    else launch_wg2<1>(c, g, mode, st, Q);
+    // 64- / 96-row tiles over more than 128 columns: 256-column blocks when that pads J no further
+    // (ReCoNet conv1 J = 243, conv2 J = 432): the dY rows are split once per 256 columns instead of
+    // per 128, and each wave runs twice the MFMAs per k-tile.  Same Mpad / Jpad / split count, so
+    // the slab layout and the workspace size do not change.
+    static const bool wide = !getenv("VST_WG_WIDE") || atoi(getenv("VST_WG_WIDE")) != 0;  // A/B switch
+    int cw = c;
+    if (wide && (c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
+    dim3 g(Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
+    if (gmode == 0) launch_wg2<0>(cw, g, mode, st, Q);
+    else if (gmode == 2) launch_wg2<2>(cw, g, mode, st, Q);
+    else launch_wg2<1>(cw, g, mode, st, Q);
     return vst_launch_status();
   }
   WgParams P;
