@@ -5,7 +5,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/pmc_r02.sh reconet > gpurun_out/fin_pmc.log 2>&1 || exit 3
-python tools/pmc_traffic.py reconet gpurun_out/r02_traffic_reconet.json > gpurun_out/fin_traffic.log 2>&1 || exit 3
+python tools/pmc_traffic.py reconet gpurun_out/r02_traffic_reconet.json --after-marker > gpurun_out/fin_traffic.log 2>&1 || exit 3
 cp gpurun_out/r02_traffic_reconet.json profiles/r02_traffic_reconet.json || exit 3
 bash tools/pmc_busy_r02.sh reconet > gpurun_out/fin_busy.log 2>&1 || exit 4
 python tools/pmc_busy.py reconet gpurun_out/r02_mfma_busy_reconet.json > gpurun_out/fin_busy2.log 2>&1 || exit 4
