@@ -100,6 +100,13 @@ __device__ __forceinline__ int a_slot(int idx) {
   return row * 4 + quad;
 }
 
+// hi-half A slots (PREC 2: two float4 per row): slot = row*2 + quad, 8 consecutive lanes on 8
+// consecutive rows of one quad (rows 20 dwords apart: distinct 4-bank groups per 8-lane store)
+__device__ __forceinline__ int a_slot2(int idx) {
+  const int row = (idx & 7) | ((idx >> 4) << 3), quad = (idx >> 3) & 1;
+  return row * 2 + quad;
+}
+
 // ADIR (bf16x6 only): the packed weights go straight from memory into each wave's MFMA A operand
 // registers (one buffer_load_b128 per 32-row fragment and piece, next tile prefetched a k-step
 // ahead) instead of through LDS: no A stores to LDS (the stores were the largest non-MFMA cost of
@@ -119,7 +126,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   constexpr int NBT = (NTT % BN == 0 && BK % (NTT / BN) == 0) ? NTT : NT;  // B-tile threads
   // A block per (k-tile, row): 16 fp32 / 16 hi + 16 lo bf16 (64 B); bf16x6: + 16 mid bf16 (96 B)
   constexpr int AW = PREC == 3 ? 24 : 16;    // dwords per (k-tile, row)
-  constexpr int A_F4 = BM * AW / 4;          // float4 per A tile
+  // single bf16 (PREC 2) reads only the hi half of each packed 64-B block: the lo half is never an
+  // MFMA operand, so it is neither loaded nor stored to LDS (half the A bytes of the bf16 path)
+  constexpr int AWL = PREC == 2 ? 8 : AW;    // dwords per (k-tile, row) actually staged
+  constexpr int A_F4 = BM * AWL / 4;         // float4 per A tile
   constexpr int A_PER = (A_F4 + NT - 1) / NT;
   constexpr int ROWSTEP = NBT / BN;          // B rows covered per pass
   constexpr int B_PER = BK / ROWSTEP;        // B elements per thread per tile
@@ -200,7 +210,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int idx = tid + i * NT;
-    a_voff[i] = (A_F4 % NT == 0 || idx < A_F4) ? 16 * (AW == 16 ? a_slot(idx) : idx) : OOR;
+    a_voff[i] = (A_F4 % NT == 0 || idx < A_F4)
+                    ? (AWL == 8 ? (a_slot2(idx) >> 1) * AW * 4 + (a_slot2(idx) & 1) * 16
+                                : 16 * (AW == 16 ? a_slot(idx) : idx))
+                    : OOR;
   }
   // A-direct: lane (r, h) of fragment i, piece p reads the 16 B at dword 8p + 4h of packed row
   // m0 + (wm*TM + i)*32 + r (same layout the LDS path copies: [hi k0..15][mid][lo] per row)
@@ -292,7 +305,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     for (int i = 0; i < (ADIR ? 0 : A_PER); ++i) {
       int idx = tid + i * NT;
       if (A_F4 % NT == 0 || idx < A_F4) {
-        if (AW == 16) {
+        if (AWL == 8) {
+          const int sl = a_slot2(idx);
+          *reinterpret_cast<f32x4*>(&As[buf][sl >> 1][(sl & 1) * 4]) = ra[i];
+        } else if (AW == 16) {
           const int sl = a_slot(idx);
           *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
         } else {
