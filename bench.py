@@ -87,13 +87,16 @@ def oracle_ref_ratio(kind):
 
 
 def _median_rate(one, warmup, steps):
-    for _ in range(warmup):
+    for i in range(warmup):
+        t0 = time.perf_counter()
         one()
+        print(f"[bench] cpu warm-up step {i}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     ts = []
-    for _ in range(steps):
+    for i in range(steps):
         t0 = time.perf_counter()
         one()
         ts.append(time.perf_counter() - t0)
+        print(f"[bench] cpu step {i}: {ts[-1]:.2f} s", file=sys.stderr, flush=True)
     ts.sort()
     return ts[len(ts) // 2], ts
 
@@ -133,6 +136,18 @@ def cpu_baseline(args):
             R.adam_step({k: p for k, p in P.items()}, {k: p.grad for k, p in P.items()}, state)
 
     med, ts = _median_rate(one, args.cpu_warmup, args.cpu_steps)
+    # the same first step in float64 (exact up to float64 rounding): the yardstick the full-size gate
+    # holds both the HIP step and the fp32 oracle step to
+    P64 = {k: v.double().requires_grad_(True) for k, v in first["P0"].items()}
+    VP64 = {k: v.double() for k, v in VP.items()}
+    g64 = R.style_grams(VP64, style_image(3, H, W).double())
+    if args.config == 2:
+        L = R.reconet_single_losses(P64, VP64, torch.cat([img1, img2]).double(), g64, w)
+    else:
+        L = R.reconet_losses(P64, VP64, img1.double(), img2.double(), flow.double(), mask.double(), g64)
+    L["loss"].backward()
+    first["terms64"] = {k: float(v.detach()) for k, v in L.items()}
+    first["grads64"] = {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach() for k, p in P64.items()}
     res = {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": nt, "kind": "port",
            "os_cpu_count": os.cpu_count(),
            "sample": f"median of {args.cpu_steps} timed steps (+{args.cpu_warmup} warm-up) of a B=1 synthetic "
@@ -158,21 +173,124 @@ def cpu_baseline_adaattn(args):
     from oracle import reconet_ref as R
 
     state = {}
+    first = {"P0": {k: p.detach().clone() for k, p in P.items()}, "VP": VP, "inputs": (c1, c2, s)}
 
     def one():
         L = A.adaattn_losses(P, VP, c1, c2, s)
         for p in P.values():
             p.grad = None
         L["loss"].backward()
+        if "terms" not in first:
+            first.update(terms={k: float(v) for k, v in L.items()}, grads={k: p.grad.clone() for k, p in P.items()})
         with torch.no_grad():
             R.adam_step(P, {k: p.grad for k, p in P.items()}, state, lr=1e-4)
 
-    steps, warm = max(1, args.cpu_steps // 2), 1
+    steps, warm = max(1, args.cpu_steps // 2), min(1, args.cpu_warmup)
     med, ts = _median_rate(one, warm, steps)
     return {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": nt, "kind": "port", "os_cpu_count": os.cpu_count(),
             "sample": f"median of {steps} timed step(s) (+{warm} warm-up) of a B=1 synthetic 3x{H}x{W} (content1, "
                       f"content2, style) triple, oracle/adaattn_ref.py on torch-CPU fp32, {nt} threads",
-            "step_s": ts, "oracle_to_reference_time_ratio": oracle_ref_ratio("adaattn")}
+            "step_s": ts, "oracle_to_reference_time_ratio": oracle_ref_ratio("adaattn")}, first
+
+
+# config-5 policy (single bf16 products): the bar tests/test_gpu_adaattn.py states for it
+BF16_BAR = {"loss_rel": 2e-2, "gnorm_rel_of_gn_plus_0.1gmax": 5e-2, "sampled_cosine_min": 0.99}
+
+
+def adaattn_level_parity(model, vgg, c, s, ref_form=True):
+    """Each AdaAttN level's two attention moments M (AA/network.py:208) and S = sqrt(clamp(E2 - M^2))
+    (:209-213) from the HIP path (the current GEMM policy, linear form) vs the float64 exact value
+    (oracle.adaattn_ref.cosine_moments_exact) on the SAME Q, K, V (the HIP 1x1 convs of the HIP VGG19
+    features), so only the attention arithmetic is measured; `ref_form`: the reference's own
+    materialised fp32 form (oracle.adaattn_ref.attention_moments) on the same Q, K, V beside it.
+    S is read through the product's output kernel: out = S * cn + M with cn = 0 gives M, with
+    cn = 2^20 gives S = (out - M) / 2^20 (exact scaling; the add rounds at 2^-24 of S * 2^20)."""
+    from oracle import adaattn_ref as A
+    from vst import ops
+    from vst.adaattn.attention import COSINE, adaattn, instance_norm_plain
+    from vst.adaattn.utilities import feature_down_sample
+
+    def rel(x, e):
+        x, e = x.double().cpu(), e.double().cpu()
+        return {"max": float((x - e).abs().max() / e.abs().max()), "norm": float((x - e).norm() / e.norm())}
+
+    out = []
+    with torch.no_grad():
+        fc, fs = list(vgg(c).values()), list(vgg(s).values())
+        for i in range(3):
+            idx, mod = i + 2, model.adaattn[i]
+            with ops.gemm_scope("stylizer"):
+                Q = ops.conv2d(instance_norm_plain(feature_down_sample(fc, idx)), mod.f.weight, mod.f.bias)
+                K = ops.conv2d(instance_norm_plain(feature_down_sample(fs, idx)), mod.g.weight, mod.g.bias)
+                V = ops.conv2d(fs[idx], mod.h.weight, mod.h.bias)
+                shp = (Q.shape[0], V.shape[1]) + tuple(Q.shape[2:])
+                M = adaattn(Q, K, V, torch.zeros(shp, device=Q.device), COSINE)
+                S = (adaattn(Q, K, V, torch.full(shp, 2.0 ** 20, device=Q.device), COSINE) - M) * 2.0 ** -20
+            Qc, Kc, Vc = Q.cpu(), K.cpu(), V.cpu()
+            Me, Se = A.cosine_moments_exact(Qc, Kc, Vc)
+            e = {"level": FEATS_AA[idx], "Nc": Q.shape[2] * Q.shape[3], "Ns": K.shape[2] * K.shape[3],
+                 "d": Q.shape[1], "dv": V.shape[1], "hip": {"M": rel(M, Me), "S": rel(S, Se)}}
+            if ref_form:
+                Mr, Sr = A.attention_moments(Qc, Kc, Vc)
+                e["reference_form_fp32"] = {"M": rel(Mr, Me), "S": rel(Sr, Se)}
+                del Mr, Sr
+            out.append(e)
+    return out
+
+
+FEATS_AA = ("relu1_1", "relu2_1", "relu3_1", "relu4_1", "relu5_1")
+
+
+def full_size_parity_adaattn(args, dev, first):
+    """The HIP train_video step (current GEMM policy) vs the oracle step on the SAME B=1 full-size
+    triple and initial weights (cpu_baseline_adaattn's first step): loss terms, per-tensor gradient
+    norms, sampled-gradient cosine, and each attention level's M / S vs float64."""
+    from vst import ops
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+
+    c1, c2, s = first["inputs"]
+    model = StylizingNetwork("cosine")
+    model.load_state_dict(first["P0"])
+    vgg = VGG19()
+    vgg.load_state_dict(first["VP"])
+    model, vgg = model.to(dev), vgg.to(dev)
+    tr = AdaAttNTrainer(model, vgg, activation="cosine")
+    tr.flat.zero_grad()
+    out = tr.losses(torch.stack([c1, c2, s]).to(dev))
+    out["loss"].backward()
+    torch.cuda.synchronize()
+    ref = first["terms"]
+    terms = {k: abs(float(out[k]) - ref[k]) / abs(ref[k]) for k in ref}
+    g = {n: p.grad.detach().double().cpu().reshape(-1) for n, p in model.named_parameters()}
+    gr = {n: first["grads"][n].double().reshape(-1) for n in g}
+    gmax = max(float(v.norm()) for v in gr.values())
+    gerr = {n: abs(float(g[n].norm()) - float(gr[n].norm())) / (float(gr[n].norm()) + 0.1 * gmax) for n in g}
+    margin = max((abs(float(g[n].norm()) - float(gr[n].norm())) / (1e-3 * float(gr[n].norm()) + 1e-4 * gmax), n)
+                 for n in g)
+    a = torch.cat([g[n] / (gr[n].norm() + 1e-30) for n in g])
+    b = torch.cat([gr[n] / (gr[n].norm() + 1e-30) for n in g])
+    cos = float(a @ b / (a.norm() * b.norm()))
+    flat = float(torch.cat([g[n] - gr[n] for n in g]).norm() / torch.cat(list(gr.values())).norm())
+    levels = adaattn_level_parity(model, vgg, c1.to(dev), s.to(dev))
+    single_bf16 = ops.policy_modes() == ["bf16"]
+    res = {"workload": f"B=1 3x{args.height}x{args.width} (content1, content2, style) triple, same seeded weights/inputs",
+           "gemm_policy": args.gemm, "loss_rel_err": terms,
+           "grad_norm_margin_worst": {"tensor": margin[1], "margin": margin[0],
+                                      "bar": "1e-3 norm + 1e-4 largest norm (fp32-class golden bar)"},
+           "grad_norm_err_worst": {"tensor": max(gerr, key=gerr.get), "err": max(gerr.values()),
+                                   "bar": "|norm - ref| / (ref + 0.1 largest)"},
+           "grad_cosine_whole": cos, "grad_rel_err_flat": flat, "attention_levels": levels}
+    if single_bf16:
+        res["bar"] = BF16_BAR
+        res["pass"] = bool(max(terms.values()) <= BF16_BAR["loss_rel"]
+                           and max(gerr.values()) <= BF16_BAR["gnorm_rel_of_gn_plus_0.1gmax"]
+                           and cos >= BF16_BAR["sampled_cosine_min"])
+    else:
+        res["bar"] = {"loss_rel": 1e-3, "grad_norm_margin": 1.0}
+        res["pass"] = bool(max(terms.values()) < 1e-3 and margin[0] <= 1.0)
+    return res
 
 
 def pmc_traffic(model, family="conv_gemm_kernel"):
@@ -280,26 +398,36 @@ def full_size_parity(args, dev, first):
     tr.flat.zero_grad()
     out["loss"].backward()
     torch.cuda.synchronize()
-    ref = first["terms"]
+    ref, ref64 = first["terms"], first["terms64"]
     terms = {k: abs(float(out[k]) - ref[k]) / abs(ref[k]) for k in ref}
+    terms64 = {k: abs(float(out[k]) - ref64[k]) / abs(ref64[k]) for k in ref64}
     g = {n: p.grad.detach().double().cpu().reshape(-1) for n, p in model.named_parameters()}
     gr = {n: first["grads"][n].double().reshape(-1) for n in g}
-    flat = float(torch.cat([g[n] - gr[n] for n in g]).norm() / torch.cat(list(gr.values())).norm())
+    ge = {n: first["grads64"][n].reshape(-1) for n in g}
+
+    def flat_err(a, b):
+        return float(torch.cat([a[n] - b[n] for n in g]).norm() / torch.cat([b[n] for n in g]).norm())
+
+    flat, flat64, oracle64 = flat_err(g, gr), flat_err(g, ge), flat_err(gr, ge)
     gmax = max(float(v.norm()) for v in gr.values())
     # per tensor: |norm - ref norm| / (1e-3 ref norm + 1e-4 largest ref norm) -- the golden-step bar of
     # tests/test_gpu_parity.py, <= 1 passes
     margin = max((abs(float(g[n].norm()) - float(gr[n].norm())) / (1e-3 * float(gr[n].norm()) + 1e-4 * gmax), n)
                  for n in g)
     tol = 1e-3
+    # flat gradient gate: the HIP step's distance from the float64 step within 2x the fp32 oracle's own
+    # distance from it (single gradient elements are conditioned by ReLU / InstanceNorm decisions, so
+    # the bar is what fp32 itself achieves on this input, not a fixed number)
+    flat_bar = 2.0 * oracle64
     return {"workload": f"B=1 3x{args.height}x{args.width} frame pair, config {args.config}, same seeded weights/inputs",
-            "tolerance": tol, "loss_rel_err": terms,
+            "tolerance": tol, "loss_rel_err": terms, "loss_rel_err_vs_float64": terms64,
             "grad_norm_margin_worst": {"tensor": margin[1], "margin": margin[0]},
             "grad_rel_err_flat": flat,
-            "grad_rel_err_flat_note": "element-wise over all 3.76M gradients: ReLU / InstanceNorm decisions make "
-                                      "single elements sensitive to fp32 summation order -- the exact-f32-MFMA policy "
-                                      "shows the same level (1.4e-3, profiles/r02_bench_f32.json), so it is reported, "
-                                      "not gated",
-            "pass": bool(max(terms.values()) < tol and margin[0] <= 1.0)}
+            "grad_rel_err_flat_vs_float64": flat64,
+            "oracle_fp32_grad_rel_err_flat_vs_float64": oracle64,
+            "grad_flat_gate": {"bar": flat_bar, "rule": "HIP vs float64 <= 2 x (fp32 oracle vs float64)",
+                               "pass": bool(flat64 <= flat_bar)},
+            "pass": bool(max(terms.values()) < tol and margin[0] <= 1.0 and flat64 <= flat_bar)}
 
 
 def build_adaattn(args, dev, rank):
@@ -625,9 +753,11 @@ def main():
             if args.model == "reconet":
                 result["cpu_baseline"], first = cpu_baseline(args)
                 result["full_size_parity"] = full_size_parity(args, dev, first)
+            elif args.model == "adaattn":
+                result["cpu_baseline"], first = cpu_baseline_adaattn(args)
+                result["full_size_parity"] = full_size_parity_adaattn(args, dev, first)
             else:
-                result["cpu_baseline"] = {"adaattn": cpu_baseline_adaattn, "reconet_infer": cpu_baseline_infer}[
-                    args.model](args)
+                result["cpu_baseline"] = cpu_baseline_infer(args)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

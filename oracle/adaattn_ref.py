@@ -74,6 +74,46 @@ def adaattn(P, prefix, c_x, s_x, c_1x, s_1x, activation="cosine"):
     return S * instance_norm(c_x) + M
 
 
+def attention_moments(Q, K, V, activation="cosine"):
+    """The two moments AdaAttN reads from its attention (AA/network.py:205-213), materialised as the
+    reference computes them: A = activation(Q^T K) (b, Nc, Ns), M = A V^T, S = sqrt(clamp(A (V^2)^T
+    - M^2, 1e-6)).  Q (b, d, h, w), K (b, d, hs, ws), V (b, dv, hs, ws); returns M, S as (b, dv, h, w)."""
+    b, d, h, w = Q.shape
+    Qt = Q.reshape(b, d, h * w).permute(0, 2, 1)
+    Km = K.reshape(b, d, -1)
+    Vt = V.reshape(b, V.shape[1], -1).permute(0, 2, 1)
+    A = cosine_attention(Qt, Km) if activation == "cosine" else softmax_attention(Qt, Km)
+    M = torch.bmm(A, Vt)
+    S = torch.sqrt((torch.bmm(A, Vt ** 2) - M ** 2).clamp(min=1e-6))
+    return (M.reshape(b, h, w, -1).permute(0, 3, 1, 2), S.reshape(b, h, w, -1).permute(0, 3, 1, 2))
+
+
+def cosine_moments_exact(Q, K, V):
+    """EXACT evaluator of `attention_moments(..., "cosine")` for sizes whose Nc x Ns matrix is too
+    large for the CPU (config 5 level 3: 32768^2 per image): the same quantity re-associated, in
+    float64.  With q^ = q/|q|, k^ = k/|k|, A_ij = (q^_i.k^_j + 1) / sum_j (q^_i.k^_j + 1), so
+      [M; E2]_i = (G^T q^_i + sum_j u_j) / (q^_i . sum_j k^_j + Ns),  G = K^ U^T,  U = [V; V^2],
+    an identity of real arithmetic (not an approximation); in float64 its rounding is ~1e-13, far
+    below any fp32 path's error, so it is the yardstick both the reference's fp32 form and the HIP
+    path are measured against.  Checked against the materialised form in float64 by
+    tests/test_oracle_golden.py::test_cosine_moments_exact."""
+    b, d, h, w = Q.shape
+    dv = V.shape[1]
+    q = Q.double().reshape(b, d, -1)
+    k = K.double().reshape(b, d, -1)
+    v = V.double().reshape(b, dv, -1)
+    qh = q / torch.sqrt((q * q).sum(1, keepdim=True))
+    kh = k / torch.sqrt((k * k).sum(1, keepdim=True))
+    U = torch.cat([v, v * v], 1)                                  # (b, 2dv, Ns)
+    G = torch.bmm(kh, U.transpose(1, 2))                          # (b, d, 2dv)
+    num = torch.bmm(G.transpose(1, 2), qh) + U.sum(2, keepdim=True)  # (b, 2dv, Nc)
+    den = (qh * kh.sum(2, keepdim=True)).sum(1, keepdim=True) + k.shape[2]  # (b, 1, Nc)
+    mom = num / den
+    M, E2 = mom[:, :dv], mom[:, dv:]
+    S = torch.sqrt((E2 - M * M).clamp(min=1e-6))
+    return M.reshape(b, dv, h, w), S.reshape(b, dv, h, w)
+
+
 def upsample2(x):
     """F.interpolate(scale_factor=2, mode='bilinear', align_corners=False)."""
     return R.resize_bilinear(x, (2 * x.shape[2], 2 * x.shape[3]))

@@ -238,6 +238,108 @@ def gen_reconet():
 
 
 # --------------------------------------------------------------------------------------------
+# Per-loss-term gradients of the train_candy step: the reference's own train() run once per term
+# with every other weight constant (LAMBDA_F, LAMBDA_O, ALPHA, BETA, GAMMA; train_candy.py:23-28)
+# set to 0, so the recorded gradient is that term's alone (at the seeded init FTL is >99.99 % of
+# every stylizer gradient of the full step, which hides the other four terms' backward).  The
+# exact (float64) gradient of the same term from the oracle is stored beside it, so the GPU test
+# can hold the HIP gradient to the reference's own fp32 distance from the exact one.
+# --------------------------------------------------------------------------------------------
+TERM_CONST = {"FTL": "LAMBDA_F", "OTL": "LAMBDA_O", "CL": "ALPHA", "SL": "BETA", "RL": "GAMMA"}
+TERM_CASES = {"b2": (2, 32, 64, (11, 12, 13, 14)), "b1r": (1, 36, 60, (21, 22, 23, 24))}
+
+
+def gen_terms():
+    from oracle import reconet_ref as R
+    from oracle import seeded_params, shapes
+
+    _fresh_project(RC_DIR)
+    rc_util = _load("utilities", os.path.join(RC_DIR, "utilities.py"))
+    sys.modules["utilities"] = rc_util
+    rc_net = _load("network", os.path.join(RC_DIR, "network.py"))
+    sys.modules["network"] = rc_net
+    out = {}
+    for tag, (B, H, W, seeds) in TERM_CASES.items():
+        style = style_image(seeds[3], H, W)
+        img1, img2, flow, mask = frame_pair_batch(seeds[2], B, H, W, mask_fn=rc_util.flow_warp_mask)
+        out[f"{tag}_img1"], out[f"{tag}_img2"] = _np(img1), _np(img2)
+        out[f"{tag}_flow"], out[f"{tag}_mask"], out[f"{tag}_style"] = _np(flow), _np(mask), _np(style)
+        out[f"{tag}_seeds"] = np.array(seeds)
+        for term, const in TERM_CONST.items():
+            fake_ds = types.ModuleType("datasets")
+            fake_ds.FlyingThings3D_Monkaa = lambda *a, **k: None
+            fake_ds.toTensor255 = lambda _img, _s=style: _s[0].clone()
+            sys.modules["datasets"] = fake_ds
+            tc = _load(f"rc_terms_{tag}_{term}", os.path.join(RC_DIR, "train_single", "train_candy.py"))
+            for c in TERM_CONST.values():
+                if c != const:
+                    setattr(tc, c, 0.0)
+
+            def reconet_factory(n=1, _s=seeds[0], _tc=tc):
+                net = rc_net.ReCoNet(n)
+                seed_module(net, _s)
+                _tc.optim = types.SimpleNamespace(Adam=_make_recording_adam(list(net.named_parameters())))
+                return net
+
+            def vgg_factory(device="cpu", _s=seeds[1]):
+                v = rc_net.Vgg16(device)
+                seed_module(v, _s)
+                return v
+
+            class _Img:
+                BILINEAR = 2
+
+                @staticmethod
+                def open(_p):
+                    class _O:
+                        def convert(self, *_):
+                            return self
+
+                        def resize(self, *_):
+                            return self
+
+                    return _O()
+
+            tc.device, tc.batch_size, tc.IMG_SIZE, tc.epoch_start, tc.epoch_end = "cpu", B, (W, H), 1, 1
+            tc.DataLoader = lambda *a, **k: [(img1.clone(), img2.clone(), flow.clone(), mask.clone())]
+            tc.ReCoNet, tc.Vgg16, tc.Image, tc.tqdm = reconet_factory, vgg_factory, _Img, _TqdmRecorder
+            _TqdmRecorder.records = []
+            save = torch.save
+            torch.save = lambda *a, **k: None
+            try:
+                tc.train()
+            finally:
+                torch.save = save
+            rec = _TqdmRecorder.records[-1]
+            p = f"{tag}_{term}_"
+            out[p + "loss"] = np.array(rec["loss"], dtype=np.float64)
+            out[p + "term"] = np.array(rec[term], dtype=np.float64)
+            grads = tc.optim.Adam.grads
+            names = sorted(grads)
+            out[p + "names"] = np.array(names)
+            # the same term in float64 through the oracle (exact up to float64 rounding)
+            P = {k: v.double().requires_grad_(True) for k, v in seeded_params(shapes.reconet(), seeds[0]).items()}
+            VP = {k: v.double() for k, v in seeded_params(shapes.vgg16(), seeds[1]).items()}
+            L = R.reconet_losses(P, VP, img1.double(), img2.double(), flow.double(), mask.double(),
+                                 R.style_grams(VP, style.double()), terms=(term,))
+            L["loss"].backward()
+            out[p + "exact_loss"] = np.array(float(L["loss"].detach()))
+            rng = np.random.default_rng(seeds[0] + 2000)
+            for n in names:
+                g = grads[n].reshape(-1).double()
+                ge = P[n].grad.reshape(-1) if P[n].grad is not None else torch.zeros(g.numel(), dtype=torch.float64)
+                out[f"{p}gnorm/{n}"] = np.array(float(g.norm()))
+                out[f"{p}exact_gnorm/{n}"] = np.array(float(ge.norm()))
+                idx = rng.integers(0, g.numel(), size=min(256, g.numel()))
+                out[f"{p}gidx/{n}"] = idx.astype(np.int64)
+                out[f"{p}gval/{n}"] = _np(g[idx])
+                out[f"{p}exact_gval/{n}"] = _np(ge[idx])
+            print(tag, term, rec[term], float(L["loss"].detach()))
+    np.savez_compressed(os.path.join(HERE, "rc_terms.npz"), **out)
+    print("per-term fixtures written")
+
+
+# --------------------------------------------------------------------------------------------
 # ReCoNet loop-body clones: train_coco2014 (config 2: single images, content + style only),
 # train_Flow_noFTL (no FTL) and train_multiple/train_Flow (input_frame_num = 4)
 # --------------------------------------------------------------------------------------------
@@ -771,6 +873,8 @@ if __name__ == "__main__":
         gen_sd()
     if "clones" in which:
         gen_clones()
+    if "terms" in which:
+        gen_terms()
     if "infer" in which:
         gen_infer()
     if "rtnstv" in which:

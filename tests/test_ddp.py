@@ -249,7 +249,7 @@ def test_product_bucketed_dp_equals_mean_of_shard_gradients(tmp_path, kind):
     assert np.array_equal(p0, p1), "replicas diverged (broadcast or all-reduce)"
     st = np.load(tmp_path / "stats0.npy")
     assert st[0] > 1, "expected several gradient buckets"
-    assert 0 < st[1] <= st[0], "no bucket was launched from backward (no overlap)"
+    assert st[1] == st[0], f"only {st[1]} of {st[0]} buckets were all-reduced during backward (overlap)"
     nt = torch.get_num_threads()
     torch.set_num_threads(2)
     try:
@@ -261,3 +261,73 @@ def test_product_bucketed_dp_equals_mean_of_shard_gradients(tmp_path, kind):
     assert np.abs(gsum - (g0 + g1).numpy()).max() <= 1e-5 * np.abs((g0 + g1).numpy()).max()
     expect = _adam_flat(params, names, (g0 + g1) / 2, 1.0).numpy()
     assert np.abs(p0 - expect).max() < 1e-6
+
+
+# ----------------------------------------------------------------------------- bucket readiness
+# GradBuckets launches a bucket once every parameter in it has had its AccumulateGrad run (post-
+# accumulate hook), i.e. after the backward of EVERY op that used it.  A block that takes a
+# gradient-carrying skip input first and consumes it last, a parameter used twice, and a parameter
+# the graph never reaches (its bucket must wait for finish()) are the cases an input-hook scheme
+# gets wrong.
+class _Toy(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 16)
+        self.b = torch.nn.Linear(16, 16)
+        self.c = torch.nn.Linear(16, 16)
+        self.unused = torch.nn.Linear(16, 16)
+
+    def block(self, skip, x):
+        h = torch.tanh(self.b(x))      # the skip input (first argument) is used last
+        return self.c(h) + self.a(skip)
+
+    def forward(self, x):
+        s = torch.relu(self.a(x))      # `a` is used twice
+        return self.block(s, s * 2)
+
+
+def _toy_grads(rank, buckets):
+    from vst.reconet._flat import FlatParams
+    from vst.reconet.dist import GradBuckets, broadcast_params
+
+    torch.manual_seed(11)
+    model = _Toy()
+    flat = FlatParams(model)
+    broadcast_params(flat.p)
+    dp = GradBuckets(model, flat, bucket_bytes=buckets) if buckets else None
+    x = torch.from_numpy(np.random.default_rng(rank).standard_normal((4, 16)).astype(np.float32))
+    flat.zero_grad()
+    if dp:
+        dp.begin()
+    (model(x) ** 2).sum().backward()
+    return flat, dp
+
+
+def _toy_worker(rank, world, port, outdir):
+    import sys
+
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "video-style-transfer_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flat, dp = _toy_grads(rank, 4 * 200)  # one Linear per bucket
+    in_bwd = sum(dp.launched)
+    dp.finish()
+    np.save(os.path.join(outdir, f"g{rank}.npy"), flat.g.numpy())
+    np.save(os.path.join(outdir, f"s{rank}.npy"), np.array([len(dp.buckets), in_bwd]))
+    dist.destroy_process_group()
+
+
+def test_bucket_readiness_skip_input_and_unused_param(tmp_path):
+    world = 2
+    mp.spawn(_toy_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    import sys
+
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "video-style-transfer_amd")]
+    expect = sum(_toy_grads(r, 0)[0].g for r in range(world)).numpy()
+    for r in range(world):
+        g = np.load(tmp_path / f"g{r}.npy")
+        assert np.abs(g - expect).max() <= 1e-6 * np.abs(expect).max(), r
+    nb, in_bwd = np.load(tmp_path / "s0.npy")
+    assert nb >= 4
+    assert in_bwd == nb - 1, (nb, in_bwd)  # every bucket but the unused parameter's, during backward

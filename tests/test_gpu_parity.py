@@ -393,6 +393,151 @@ def test_train_step_golden(golden, tag, step_policy):
         assert np.abs(got - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
 
 
+@pytest.mark.parametrize("term", ["FTL", "OTL", "CL", "SL", "RL"])
+@pytest.mark.parametrize("tag", ["b2", "b1r"])
+def test_train_step_per_term_golden(golden, tag, term, step_policy):
+    """Each train_candy loss term ALONE through the HIP trainer (`terms=(term,)`) vs the reference's
+    own train() with the other four weight constants zeroed and vs the float64 gradient of the same
+    term (tests/golden/rc_terms.npz).  At the seeded init FTL is >99.99 % of every stylizer gradient
+    of the full step, so this is the check that pins the OTL, content, Gram-style and TV backward.
+    Bar (conftest.term_grad_margins): term value 1e-4 relative; every gradient tensor's norm and 256
+    sampled elements within TERM_REL = 2e-3 of that tensor's OWN exact norm (or 4x the reference's own
+    fp32 error, where that is larger -- the ConvTanh bias under OTL / TV); tensors whose exact gradient
+    is zero (conv biases feeding InstanceNorm; the decoder under FTL) below 1e-5 of the largest norm.
+    (Why 2e-3 and not fp32 rounding: conftest.TERM_REL; the decision-independent 2e-5 check of every
+    block's backward under each term is test_stylizer_block_chain_per_term.)"""
+    import conftest
+    from vst.reconet import network as N
+    from vst.reconet.train import ReCoNetTrainer
+
+    d = golden("rc_terms")
+    seeds = d[f"{tag}_seeds"]
+    model = _seeded(N.ReCoNet(), shapes.reconet(), int(seeds[0])).to(DEV)
+    vgg = _seeded(N.Vgg16(), shapes.vgg16(), int(seeds[1])).to(DEV)
+    tr = ReCoNetTrainer(model, vgg, G(d[f"{tag}_style"]), terms=(term,))
+    frames = torch.stack([G(d[f"{tag}_img1"]), G(d[f"{tag}_img2"])])
+    out = tr.losses(frames, G(d[f"{tag}_flow"]), G(d[f"{tag}_mask"]))
+    p = f"{tag}_{term}_"
+    assert rel_err(out["loss"].item(), d[p + "term"]) < 1e-4, (out["loss"].item(), float(d[p + "term"]))
+    tr.flat.zero_grad()
+    out["loss"].backward()
+    grads = {n: C(v.grad if v.grad is not None else torch.zeros_like(v)).numpy()
+             for n, v in model.named_parameters()}
+    m = conftest.term_grad_margins(d, p, grads)
+    worst = sorted(m, key=m.get)[-3:]
+    print(f"per-term {tag} {term} {step_policy}: worst margins", {n: round(m[n], 3) for n in worst})
+    assert m[worst[-1]] <= 1.0, (worst[-1], m[worst[-1]])
+
+
+# Block chain: every stylizer block's backward, driven by each loss term's own EXACT gradient signal.
+# The float64 oracle runs the one-term step (rc_terms case) and records each block's input and the
+# exact gradient at its output; the HIP block then gets that input (rounded to fp32) and that
+# gradient, and its input gradient and parameter gradients are compared with the float64 backward of
+# the same block on the same rounded input.  Unlike the whole-step check, an fp32 ReLU / InstanceNorm
+# decision that flips far upstream cannot move these numbers, so the bar is near fp32 rounding.
+BLOCK_TOL = 2e-5
+BLOCKS = (("conv1", 9, 1, False), ("conv2", 3, 2, False), ("conv3", 3, 2, False), ("res1",), ("res2",), ("res3",),
+          ("res4",), ("res5",), ("deconv1", 3, 1, True), ("deconv2", 3, 1, True), ("deconv3", 9))
+
+
+def _oracle_block(P, name, spec, x):
+    if name.startswith("res"):
+        return R.residual_block(x, P, name)
+    if name == "deconv3":
+        return R.conv_tanh(x, P, name, 9)
+    _, k, s, up = spec
+    return R.conv_in_relu(x, P, name, k, s, upsample=up)
+
+
+def _exact_block_io(d, tag, term):
+    """float64 one-term step: {block: (input, gradient at output)}."""
+    seeds = d[f"{tag}_seeds"]
+    P = {k: v.double().requires_grad_(True) for k, v in oracle.seeded_params(shapes.reconet(), int(seeds[0])).items()}
+    VP = {k: v.double() for k, v in oracle.seeded_params(shapes.vgg16(), int(seeds[1])).items()}
+    io = {b[0]: ([], []) for b in BLOCKS}
+
+    def fwd(P_, x):
+        outs = {}
+        for spec in BLOCKS:
+            io[spec[0]][0].append(x.detach())
+            y = _oracle_block(P_, spec[0], spec, x)
+            y.retain_grad()
+            io[spec[0]][1].append(y)
+            outs[spec[0]] = y
+            x = y
+        # vgg_normalize_ divides the styled output in place: hand it a copy
+        return outs["deconv1"], outs["res5"], outs["deconv3"] * 1.0
+
+    T = lambda k: torch.from_numpy(d[f"{tag}_{k}"]).double()  # noqa: E731
+    L = R.reconet_losses(P, VP, T("img1").clone(), T("img2").clone(), T("flow"), T("mask"),
+                         R.style_grams(VP, T("style")), forward=fwd, terms=(term,))
+    L["loss"].backward()
+    return P, {b: (torch.cat(xs), torch.cat([y.grad if y.grad is not None else torch.zeros_like(y) for y in ys]))
+               for b, (xs, ys) in io.items()}
+
+
+@pytest.mark.parametrize("term", ["FTL", "OTL", "CL", "SL", "RL"])
+@pytest.mark.parametrize("tag", ["b2", "b1r"])
+def test_stylizer_block_chain_per_term(golden, tag, term, step_policy):
+    """Each ReCoNet block (conv1..3, res1..5, deconv1..3) backward on HIP under each loss term's exact
+    gradient signal: input gradient and every parameter gradient within BLOCK_TOL (norm-wise, of the
+    tensor's own float64 norm; conv biases feeding InstanceNorm, whose exact gradient is 0, below
+    BLOCK_TOL of the block's largest parameter-gradient norm; the ConvTanh bias gradient, a plain sum
+    over every pixel with heavy cancellation under OTL / TV, additionally gets the fp32 summation bound
+    64 ulp x the sum of magnitudes -- the reference's own fp32 value sits 2.5e-4..6e-4 from exact
+    there).  Parameter gradients go through the in-place .grad sinks as in the trainer."""
+    from vst import ops
+    from vst.reconet import network as N
+
+    d = golden("rc_terms")
+    P64, io = _exact_block_io(d, tag, term)
+    model = _seeded(N.ReCoNet(), shapes.reconet(), int(d[f"{tag}_seeds"][0])).to(DEV)
+    worst = (0.0, None)
+    for spec in BLOCKS:
+        name = spec[0]
+        x64, gy64 = io[name]
+        if float(gy64.norm()) == 0.0:
+            continue  # the term does not reach this block (FTL: the decoder)
+        need_dx = name != "conv1"
+        xr = x64.float().double().requires_grad_(need_dx)
+        Pb = {k: v.detach().clone().requires_grad_(True) for k, v in P64.items() if k.startswith(name + ".")}
+        if name == "deconv3":  # ConvTanh: keep the pre-tanh gradient, whose plain sum is the bias gradient
+            z = R.conv_layer(xr, Pb, name, 9, 1)
+            z.retain_grad()
+            (torch.tanh(z / 255) * 150 + 255 / 2).backward(gy64)
+            # fp32 summation bound of a sum with cancellation: 64 ulp of the sum of magnitudes
+            bias_l1 = 64 * 2.0 ** -24 * float(z.grad.abs().sum(dim=(0, 2, 3)).norm())
+        else:
+            _oracle_block(Pb, name, spec, xr).backward(gy64)
+            bias_l1 = 0.0
+        mod = getattr(model, name)
+        for p in mod.parameters():
+            p.grad = torch.zeros_like(p)
+        xg = G(xr.detach().float()).requires_grad_(need_dx)
+        with ops.gemm_scope("stylizer"):
+            yg = mod(xg)
+        yg.backward(G(gy64.float()))
+        errs = {}
+        if need_dx:
+            errs["dx"] = _norm_err(C(xg.grad), xr.grad)
+        named = dict(mod.named_parameters())
+        pmax = max(float(v.grad.norm()) for v in Pb.values())
+        for k, v in Pb.items():
+            got = C(named[k[len(name) + 1:]].grad).double()
+            e = float(v.grad.norm())
+            if e < 1e-6 * pmax:
+                errs[k] = float(got.norm()) / pmax
+            elif k.endswith("conv2d.bias") and bias_l1:
+                errs[k] = float((got - v.grad).norm()) / (e + bias_l1 / BLOCK_TOL)
+            else:
+                errs[k] = float((got - v.grad).norm()) / e
+        k = max(errs, key=errs.get)
+        if errs[k] > worst[0]:
+            worst = (errs[k], f"{name}:{k}")
+        assert errs[k] <= BLOCK_TOL, (name, k, errs[k])
+    print(f"block chain {tag} {term} {step_policy}: worst {worst[0]:.2e} ({worst[1]})")
+
+
 CLONE_SCRIPTS = {"coco": ("train_coco2014", 1), "cocor": ("train_coco2014", 1), "noftl": ("train_Flow_noFTL", 1),
                  "multi": ("train_Flow", 4)}
 

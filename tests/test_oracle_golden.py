@@ -11,6 +11,7 @@ import oracle
 from oracle import reconet_ref as R
 from oracle import shapes
 
+import conftest
 from conftest import rel_err
 
 
@@ -95,6 +96,30 @@ def test_train_step(golden, tag):
         assert np.abs(params[n].reshape(-1)[:64].numpy() - s[f"{tag}_phead/{n}"])[sel].max(initial=0) < 1e-5, n
 
 
+@pytest.mark.parametrize("term", R.ALL_TERMS)
+@pytest.mark.parametrize("tag", ["b2", "b1r"])
+def test_train_step_per_term(golden, tag, term):
+    """Each train_candy loss term ALONE (the reference's own train() with the other four weight
+    constants zeroed, gen_golden.gen_terms): the oracle's term value and its gradient, tensor by
+    tensor, at the per-term bar of conftest.term_grad_margins (TERM_REL of the tensor's own exact norm;
+    the oracle itself sits ~1e-6 from the exact gradient on these cases)."""
+    d = golden("rc_terms")
+    seeds = d[f"{tag}_seeds"]
+    P = oracle.seeded_params(shapes.reconet(), int(seeds[0]), requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg16(), int(seeds[1]))
+    grams = R.style_grams(VP, T(d[f"{tag}_style"]))
+    L = R.reconet_losses(P, VP, T(d[f"{tag}_img1"]).clone(), T(d[f"{tag}_img2"]).clone(),
+                         T(d[f"{tag}_flow"]), T(d[f"{tag}_mask"]), grams, terms=(term,))
+    p = f"{tag}_{term}_"
+    assert rel_err(L["loss"].item(), d[p + "term"]) < 1e-5
+    assert rel_err(d[p + "term"], d[p + "exact_loss"]) < 1e-5
+    L["loss"].backward()
+    grads = {n: (v.grad if v.grad is not None else torch.zeros_like(v)).numpy() for n, v in P.items()}
+    m = conftest.term_grad_margins(d, p, grads)
+    worst = max(m, key=m.get)
+    assert m[worst] <= 1.0, (worst, m[worst])
+
+
 CLONES = {  # tag: (single, input_frame_num, weights, terms) -- the reference script each golden ran
     "coco": (True, 1, dict(R.LOSS_WEIGHTS, BETA=1e10), ("CL", "SL")),        # train_coco2014.py
     "cocor": (True, 1, dict(R.LOSS_WEIGHTS, BETA=1e10), ("CL", "SL")),
@@ -147,6 +172,21 @@ def test_clone_train_steps(golden, tag):
 
 
 # ----------------------------------------------------------------------------- AdaAttN
+def test_cosine_moments_exact():
+    """oracle.adaattn_ref.cosine_moments_exact (the float64 re-associated yardstick for the config-4/5
+    attention sizes) equals the materialised attention_moments in float64, ragged shapes included."""
+    from oracle import adaattn_ref as A
+
+    g = torch.Generator().manual_seed(3)
+    for b, d, dv, (h, w), (hs, ws) in ((2, 16, 8, (6, 10), (5, 7)), (1, 40, 24, (9, 4), (12, 11))):
+        Q = torch.randn(b, d, h, w, generator=g, dtype=torch.float64)
+        K = torch.randn(b, d, hs, ws, generator=g, dtype=torch.float64)
+        V = torch.randn(b, dv, hs, ws, generator=g, dtype=torch.float64) * 2 + 0.5
+        M, S = A.attention_moments(Q, K, V)
+        Me, Se = A.cosine_moments_exact(Q, K, V)
+        assert rel_err(Me, M) < 1e-12 and rel_err(Se, S) < 1e-12
+
+
 def test_adaattn_units(golden):
     from oracle import adaattn_ref as A
 

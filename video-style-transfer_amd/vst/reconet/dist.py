@@ -6,20 +6,22 @@ runs on gloo/CPU, which is how tests/test_ddp.py covers it).
 
 Bucket readiness.  The trainers keep every parameter as a view into one flat buffer
 (`FlatParams`), in `module.parameters()` order, and the HIP backward writes weight gradients
-straight into it.  The model's top-level blocks ("units": its children, with ModuleList /
-ModuleDict expanded) are called once per forward; a forward pre-hook attaches a gradient hook to
-each call's input.  That hook fires once the input's gradient is complete, i.e. after the block's
-backward -- which wrote all of the block's parameter gradients -- has run.  A bucket (a contiguous
-range of the flat gradient, cut at parameter boundaries, built from the end of the buffer because
-backward reaches the last layers first) is launched as an async all-reduce when every unit owning
-one of its parameters has had all its calls' input hooks fire.  Units whose input does not require
-grad (the first conv on the images, AdaAttN levels fed by frozen VGG features) and parameters
-outside any unit are reduced by `finish()` after backward returns.  Hooks fire in the same order
-on every rank (same graph), so the collectives are issued in the same order everywhere.
+straight into it (the Function then returns None for the parameter).  Every parameter carries a
+post-accumulate-grad hook.  Autograd runs a leaf's AccumulateGrad node exactly once per backward,
+after EVERY edge into it has delivered -- i.e. after the backward of every op that used the
+parameter has run, and so after each of those ops has enqueued its write into the flat gradient on
+the stream (whether it wrote in place and returned None, or returned the gradient to autograd).
+A bucket (a contiguous range of the flat gradient, cut at parameter boundaries, built from the
+end of the buffer because backward reaches the last layers first) is launched as an async
+all-reduce when the hooks of all its parameters have fired.  No assumption about which input of a
+module is consumed first is needed, and a parameter the graph never reaches (unused this step)
+keeps its bucket back for `finish()`.  A hook that fires for a parameter whose bucket was already
+launched (a second backward in the same step) raises instead of reducing a half-written slice.
+Hooks fire in the same order on every rank (same graph), so the collectives are issued in the same
+order everywhere.
 """
 import torch
 import torch.distributed as dist
-from torch import nn
 
 BUCKET_BYTES = 8 << 20
 
@@ -53,26 +55,6 @@ def broadcast_params(flat_p, group=None):
         dist.broadcast(flat_p, src=src, group=group)
 
 
-def _units(model):
-    out = []
-    for name, m in model.named_children():
-        if isinstance(m, (nn.ModuleList, nn.ModuleDict)):
-            out += [(f"{name}.{n}", c) for n, c in _units_of_container(m)]
-        else:
-            out.append((name, m))
-    return out
-
-
-def _units_of_container(c):
-    out = []
-    for n, m in c.named_children():
-        if isinstance(m, (nn.ModuleList, nn.ModuleDict)):
-            out += [(f"{n}.{k}", x) for k, x in _units_of_container(m)]
-        else:
-            out.append((n, m))
-    return out
-
-
 class GradBuckets:
     """Bucketed, backward-overlapped all-reduce of a FlatParams gradient (see module docstring).
 
@@ -81,15 +63,14 @@ class GradBuckets:
     def __init__(self, model, flat, group=None, bucket_bytes=BUCKET_BYTES):
         self.flat, self.group = flat, group
         _, self.world = world_info(group)
-        spans, off = {}, 0
+        spans, off = [], 0
         for p in flat.params:
-            spans[id(p)] = (off, p.numel())
+            spans.append((off, p.numel()))
             off += p.numel()
         # buckets: contiguous [lo, hi) ranges, cut at parameter boundaries, from the end
         cap = max(1, bucket_bytes // 4)
         bounds, hi, size = [], off, 0
-        for p in reversed(flat.params):
-            o, k = spans[id(p)]
+        for o, k in reversed(spans):
             size += k
             if size >= cap:
                 bounds.append((o, hi))
@@ -97,62 +78,34 @@ class GradBuckets:
         if hi > 0:
             bounds.append((0, hi))
         self.buckets = bounds  # backward order: last parameters first
-        owner = {}
-        self.units = []
-        for name, m in _units(model):
-            ps = [p for p in m.parameters() if id(p) in spans]
-            if not ps:
-                continue
-            self.units.append((name, m))
-            u = len(self.units) - 1
-            for p in ps:
-                owner[id(p)] = u
-            m.register_forward_pre_hook(self._make_pre_hook(u))
-        # bucket -> the units owning its parameters (None = a parameter outside every unit)
-        self.bucket_units = []
-        for lo, hi in self.buckets:
-            us = set()
-            for p in flat.params:
-                o, k = spans[id(p)]
-                if o < hi and o + k > lo:
-                    us.add(owner.get(id(p)))
-            self.bucket_units.append(us)
-        self.unit_buckets = [[b for b, us in enumerate(self.bucket_units) if u in us] for u in range(len(self.units))]
+        self.bucket_of = [next(b for b, (lo, h) in enumerate(bounds) if lo <= o < h) for o, _ in spans]
+        self.bucket_nparams = [self.bucket_of.count(b) for b in range(len(bounds))]
+        self.names = {id(p): n for n, p in model.named_parameters()}
         self.active = False
         self.works = []
         self.launched = []
+        if self.world > 1:
+            for i, p in enumerate(flat.params):
+                p.register_post_accumulate_grad_hook(self._make_hook(i))
 
-    def _make_pre_hook(self, u):
-        def pre_hook(_module, inputs):
-            if not self.active or not torch.is_grad_enabled():
+    def _make_hook(self, i):
+        def hook(p):
+            if not self.active:
                 return
-            t = next((x for x in inputs if isinstance(x, torch.Tensor) and x.requires_grad), None)
-            if t is None:
-                self.blocked[u] = True
-                return
-            self.calls[u] += 1
-            t.register_hook(lambda g, u=u: self._unit_done(u))
+            b = self.bucket_of[i]
+            if self.launched[b]:
+                raise RuntimeError(f"gradient of {self.names.get(id(p), '?')} accumulated after its bucket's "
+                                   f"all-reduce was launched (a second backward before finish()?)")
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch(b)
 
-        return pre_hook
+        return hook
 
     def begin(self):
-        n = len(self.units)
-        self.calls, self.done, self.blocked = [0] * n, [0] * n, [False] * n
+        self.pending = list(self.bucket_nparams)
         self.works, self.launched = [], [False] * len(self.buckets)
         self.active = self.world > 1
-
-    def _unit_complete(self, u):
-        return u is not None and not self.blocked[u] and self.done[u] == self.calls[u]
-
-    def _unit_done(self, u):
-        if not self.active:
-            return None
-        self.done[u] += 1
-        if self.done[u] == self.calls[u]:
-            for b in self.unit_buckets[u]:
-                if not self.launched[b] and all(self._unit_complete(x) for x in self.bucket_units[b]):
-                    self._launch(b)
-        return None
 
     def _launch(self, b):
         lo, hi = self.buckets[b]
