@@ -28,8 +28,10 @@ extern "C" {
 /* ---- library ------------------------------------------------------------------------------ */
 int vst_version(void);
 const char* vst_strerror(int code);
-/* Build provenance: "<fnv1a-64 hex of csrc/* and include/vst_hip.h at build time>" (the Python
- * loader and the GPU tests compare it with the tree they run from). */
+/* Build provenance: the first 16 hex digits of the sha256 of the sorted csrc/ *.hip, *.h and Makefile
+ * followed by include/vst_hip.h, taken at build time (csrc/Makefile BUILD_ID; vst/_lib.py
+ * source_build_id() computes the same digest over the tree it runs from and refuses a library whose
+ * id differs). */
 const char* vst_build_id(void);
 
 /* GEMM arithmetic: a per-call argument `mode` of every conv / Gram / attention GEMM entry and of
@@ -247,10 +249,12 @@ int vst_tv_bwd(const float* s, long NC, int H, int W, const float* gout, const f
 int vst_sum_scaled(const float* x, long n, float weight, float* ws, float* out, void* stream);
 
 /* ---- AdaAttN (AA/network.py:102-251, AA/lossfn.py:5-53) --------------------------------------
- * Attention matrices are materialised per image ([N][Nc][Ns] fp32); the products run on the GEMM
- * kernels: S = Q^T K and dA = [dM;dE2]^T [V;V^2] and dK = Q dS and d[V;V^2] = [dM;dE2] A as
- * vst_conv_gemm 1x1 products with a per-image packed A, [M;E2] = A [V;V^2]^T-style and dQ = K dS^T
- * as vst_gemm_abt. */
+ * Cosine attention (CosineSimilarity, the train_video path) is never materialised: its two moments
+ * [M; E2] = (G^T q^ + sum u) / (q^ . sum k^ + Ns), G = K^ [V; V^2]^T, are formed in linear form
+ *  from vst_gemm_abt / vst_attn_gemm products, vst_outer_axpy, vst_attn_fwd_rows and
+ * vst_square_concat, with the transposed algebra in the backward.  The softmax activation (the image
+ * trainer) keeps the materialised path: S = Q^T K per image ([N][Nc][Ns] fp32), vst_softmax_rows,
+ * [M;E2] and the backward products on the same GEMM entries. */
 /* out[n][m][j] = scale * sum_r a[n][m][r] b[n][j][r]; workspace = vst_wgrad_workspace(N, M, J, R) */
 int vst_gemm_abt(const float* a, const float* b, float* out, float* workspace, int N, int M, int J, int R, float scale,
                  int mode, void* stream);

@@ -944,7 +944,8 @@ static int splits_for(int N, int M, long J, int HWo) {
 // pairs of the virtual-grid GEMM (2.25x fewer MACs), with M = 4*Cout rows (48 -> 192, 96 -> 384)
 // filling whole tiles.  dW[co][ci][kh][kw] = sum_{a,b} P[(co,a,b)][(e(a,kh), e(b,kw), ci)].
 // one thread per (nc, a, i', 4-column group j'..j'+3): both b planes from the dy row 2i'-a
-// (two aligned float4 + one scalar load, two float4 stores)
+// (two aligned float4 + one scalar load, two float4 stores; odd W, whose rows start only 8-B
+// aligned, takes the per-element loads)
 __global__ void up2_phase_planes_kernel(const float* __restrict__ dy, float* __restrict__ A, long NC, int H, int W,
                                         int Wp) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -961,7 +962,7 @@ __global__ void up2_phase_planes_kernel(const float* __restrict__ dy, float* __r
   float e[9];  // dy[y][2j - 1 .. 2j + 7]
   if (y >= 0 && y < 2 * H) {
     const float* row = dy + (nc * 2 * H + y) * W2;
-    if (2 * j + 8 <= W2) {
+    if ((W & 1) == 0 && 2 * j + 8 <= W2) {  // even W: the row starts 16-B aligned (2W % 4 == 0)
       const f32x4 v0 = *reinterpret_cast<const f32x4*>(row + 2 * j);
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(row + 2 * j + 4);
 #pragma unroll

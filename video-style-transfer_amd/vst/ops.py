@@ -5,6 +5,7 @@ device memory).  Reference call sites each operator replaces are cited per class
 import contextlib
 import ctypes
 import os
+import threading
 import weakref
 
 import torch
@@ -47,8 +48,24 @@ KBLOCK_RES = _KB in ("2", "res")
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
 # the pack and GEMM calls that follow it pass to the library.
-_BASE_MODE = [None]  # base mode of the selected policy
-_CUR = [None]        # mode of the GEMM being set up (gemm_role)
+class _ThreadSlot(threading.local):
+    """One value per host thread, indexed like the one-element lists it replaces (slot[0])."""
+
+    def __init__(self, value=None):
+        self.value = value
+
+    def __getitem__(self, _i):
+        return self.value
+
+    def __setitem__(self, _i, v):
+        self.value = v
+
+
+_BASE_MODE = [None]  # base mode of the selected policy (process-wide)
+# mode of the GEMM being set up (gemm_role) and the model scope: per host thread, so two threads
+# issuing ops (trainers on separate streams, autograd's device thread) never pack under one mode and
+# launch under another
+_CUR = _ThreadSlot()
 # per-role overrides of the base mode; roles: "fwd" (forward products), "fwd_img" (Cin = 3),
 # "dgrad" (data gradients, Gram backward), "wgrad" (weight gradients, Gram), "attn_cosine" /
 # "attn_softmax" (AdaAttN attention products, fwd + bwd)
@@ -98,7 +115,7 @@ def base_gemm_mode():
 def gemm_mode():
     """The mode passed to the library by the pack / GEMM calls being issued (set by gemm_role)."""
     _ensure_policy()
-    return _CUR[0]
+    return _BASE_MODE[0] if _CUR[0] is None else _CUR[0]
 
 
 def gemm_mode_name(mode=None):
@@ -134,7 +151,7 @@ def policy_modes():
     return sorted({gemm_mode_name(m) for m in [_BASE_MODE[0], *GEMM_POLICY.values()]})
 
 
-_SCOPE = [None]
+_SCOPE = _ThreadSlot()
 
 
 @contextlib.contextmanager
@@ -598,12 +615,15 @@ class InstanceNormFn(Function):
         ctx.params = (w, b, conv_bias)
         # the backward recomputes the ReLU mask from x and b unless a residual was added after it
         keep_y = relu and (res is not None or _IN_YMASK)
-        ctx.save_for_backward(x, y if keep_y else None, stats, w)
+        # b is saved (not read live from ctx.params) so an in-place update of it before this
+        # backward -- the recomputed ReLU mask depends on it -- trips autograd's version check
+        # (FlatParams.adam bumps the flat buffer's version after its kernel)
+        ctx.save_for_backward(x, y if keep_y else None, stats, w, b)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, y, stats, w = ctx.saved_tensors
+        x, y, stats, w, b = ctx.saved_tensors
         gy = gy.contiguous()
         N, C, H, W = x.shape
         gx = _empty(x.shape, x)
@@ -615,7 +635,7 @@ class InstanceNormFn(Function):
         gb = sb if direct else _empty((C,), x)
         gc = (sc if direct else _empty((C,), x)) if need_c else None
         part = _empty((N * C * 3,), x)
-        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(ctx.params[1].contiguous()), ptr(stats), ptr(w.contiguous()),
+        lib.vst_instnorm_bwd(ptr(gy), ptr(x), ptr(y), ptr(b.contiguous()), ptr(stats), ptr(w.contiguous()),
                              ptr(gx), ptr(gw), ptr(gb), ptr(gc), ptr(part), N, C, H * W, int(ctx.relu), int(direct),
                              stream())
         gres = gy if ctx.has_res else None

@@ -6,6 +6,7 @@ place into an existing .grad), the DDP all-reduce is ONE RCCL call and Adam is O
 (`vst_adam`) over the whole model (62 tensors / 3,763,011 floats for ReCoNet).
 """
 import torch
+from torch.autograd.graph import increment_version
 
 from .._lib import lib, ptr, stream
 
@@ -45,3 +46,6 @@ class FlatParams:
     def adam(self, step, lr, betas, eps, gscale=1.0):
         lib.vst_adam(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), self.numel, float(lr), float(betas[0]),
                      float(betas[1]), float(eps), int(step), float(gscale), stream())
+        # the kernel updated every parameter in place: bump the version counter the parameter views
+        # share with the flat buffer, so a graph saved before this step refuses to run backward
+        increment_version(self.p)
