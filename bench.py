@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed oracle steps (median)")
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--gemm", default=os.environ.get("VST_GEMM_POLICY"),
-                    choices=("bf16x6", "f32", "parity", "bf16x3", "bf16"),
+                    choices=("bf16x6", "f32", "parity", "bf16x3", "bf16", "f16"),
                     help="GEMM arithmetic policy (vst.ops.POLICIES); default bf16x6 (fp32-class split products), "
                          "bf16 for the config-5 AdaAttN shape (BASELINE's half-precision path)")
     return ap.parse_args()
@@ -259,11 +259,11 @@ def full_size_parity_adaattn(args, dev, first):
     tr = AdaAttNTrainer(model, vgg, activation="cosine")
     tr.flat.zero_grad()
     out = tr.losses(torch.stack([c1, c2, s]).to(dev))
-    out["loss"].backward()
+    unscale = tr.backward(out["loss"])
     torch.cuda.synchronize()
     ref = first["terms"]
     terms = {k: abs(float(out[k]) - ref[k]) / abs(ref[k]) for k in ref}
-    g = {n: p.grad.detach().double().cpu().reshape(-1) for n, p in model.named_parameters()}
+    g = {n: p.grad.detach().double().cpu().reshape(-1) * unscale for n, p in model.named_parameters()}
     gr = {n: first["grads"][n].double().reshape(-1) for n in g}
     gmax = max(float(v.norm()) for v in gr.values())
     gerr = {n: abs(float(g[n].norm()) - float(gr[n].norm())) / (float(gr[n].norm()) + 0.1 * gmax) for n in g}
@@ -274,7 +274,7 @@ def full_size_parity_adaattn(args, dev, first):
     cos = float(a @ b / (a.norm() * b.norm()))
     flat = float(torch.cat([g[n] - gr[n] for n in g]).norm() / torch.cat(list(gr.values())).norm())
     levels = adaattn_level_parity(model, vgg, c1.to(dev), s.to(dev))
-    single_bf16 = ops.policy_modes() == ["bf16"]
+    single_bf16 = ops.policy_modes() in (["bf16"], ["f16"])
     res = {"workload": f"B=1 3x{args.height}x{args.width} (content1, content2, style) triple, same seeded weights/inputs",
            "gemm_policy": args.gemm, "loss_rel_err": terms,
            "grad_norm_margin_worst": {"tensor": margin[1], "margin": margin[0],
@@ -601,7 +601,7 @@ def default_policy(args):
     if args.gemm:
         return args.gemm
     if args.model == "adaattn" and (args.height, args.width) == (512, 1024):
-        return "bf16"  # config 5: BASELINE's reduced-precision MFMA path
+        return "bf16"  # config 5: BASELINE's half-precision MFMA path
     return "bf16x6"
 
 
@@ -609,8 +609,8 @@ def arithmetic_label(ops, ks):
     """dtype string: fp32 operands/accumulation + the product arithmetic actually launched."""
     names = sorted({ops.gemm_mode_name(m) for m in ks["by_mode"]}) or ops.policy_modes()
     desc = {"f32": "f32 MFMA", "bf16x6": "bf16x6 split MFMA (~2^-24/product)", "bf16x3": "bf16x3 split MFMA (~2^-16)",
-            "bf16": "bf16 MFMA (~2^-8)"}
-    base = "bf16" if names == ["bf16"] else "f32"
+            "bf16": "bf16 MFMA (~2^-8)", "f16": f"fp16 MFMA (~2^-11, static loss scale {ops.loss_scale():g})"}
+    base = names[0] if names in (["bf16"], ["f16"]) else "f32"
     return f"{base} ({' + '.join(desc[n] for n in names)})"
 
 

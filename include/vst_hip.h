@@ -45,6 +45,11 @@ const char* vst_build_id(void);
  *   VST_GEMM_BF16X6  three-way hi + mid + lo split, the six products of order >= 2^-16 (per-product
  *                    error ~2^-24, fp32-class); packed operands are 1.5x the fp32 size
  *                    (Kpad*Mpad*3/2 floats).
+ *   VST_GEMM_F16     one fp16 product per fp32 product (v_mfma_f32_32x32x16_f16, 11-bit significand,
+ *                    ~2^-11 per operand rounding, fp32 accumulate): BASELINE config 5's fp16 MFMA
+ *                    path.  fp16's range ends at 65504 and its normal range at 6.1e-5, so the caller
+ *                    keeps operands inside it (the AdaAttN trainer scales the loss, hence every
+ *                    backward operand, by a static power of two and unscales in Adam).
  * VST_GEMM_KBLOCK may be or-ed into the mode of a conv pack + GEMM pair (both must carry it):
  * channel-block-major, tap-minor K order (16 channels x every tap, then the next 16 channels), which
  * keeps each block's re-read source rows L2-resident; the sums then run in a different order.
@@ -53,6 +58,7 @@ const char* vst_build_id(void);
 #define VST_GEMM_BF16X3 1
 #define VST_GEMM_BF16 2
 #define VST_GEMM_BF16X6 3
+#define VST_GEMM_F16 4
 #define VST_GEMM_KBLOCK 16
 
 /* ---- convolution (implicit GEMM on MFMA, arithmetic per the `mode` argument) ---------------

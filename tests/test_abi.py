@@ -51,7 +51,7 @@ def test_host_side_argument_validation_without_gpu():
     assert (mp.value, kp.value) == (192, 1728)
     assert lib.vst_wgrad_workspace(16, 192, 1728, 8192) > 0
     # GEMM arithmetic is a validated per-call argument: an unknown mode fails before any launch
-    for bad in (-1, 4, 7):
+    for bad in (-1, 5, 7, 8):
         assert lib.vst_pack_weight(1, 1, 4, 3, 3, 3, 0, 0, 64, 32, bad, None) == -1
         assert lib.vst_gemm_abt(1, 1, 1, 1, 1, 4, 4, 16, 1.0, bad, None) == -1
         assert lib.vst_conv_wgrad(1, 1, 1, 1, 1, 3, 8, 8, 4, 8, 8, 3, 3, 0, 1, 1, 1, 0, bad, None) == -1

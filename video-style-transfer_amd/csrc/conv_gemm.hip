@@ -322,7 +322,8 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
     static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
     const int am = vst_mode_arith(mode);
-    if (t256 && cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16)) cfg = T256;
+    if (t256 && cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16))
+      cfg = T256;
     // bf16x6 A-direct blocks (VST_AD64 / VST_AD128 / VST_AD192 / VST_AD256: 0 off, 1 on, 2 data
     // gradients only)
     auto env_mode = [](const char* n, int dflt) { const char* v = getenv(n); return v ? atoi(v) : dflt; };
@@ -365,6 +366,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     case VST_GEMM_F32: launch_prec<0>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16: launch_prec<2>(cfast, gm, cfg, grid, st, P); break;
     case VST_GEMM_BF16X6: launch_prec<3>(cfast, gm, cfg, grid, st, P); break;
+    case VST_GEMM_F16: launch_prec<4>(cfast, gm, cfg, grid, st, P); break;
     default: launch_prec<1>(cfast, gm, cfg, grid, st, P); break;
   }
   return vst_launch_status();

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   constexpr int AW = PREC == 3 ? 24 : 16;    // dwords per (k-tile, row)
   // single bf16 (PREC 2) reads only the hi half of each packed 64-B block: the lo half is never an
   // MFMA operand, so it is neither loaded nor stored to LDS (half the A bytes of the bf16 path)
-  constexpr int AWL = PREC == 2 ? 8 : AW;    // dwords per (k-tile, row) actually staged
+  constexpr int AWL = (PREC == 2 || PREC == 4) ? 8 : AW;  // dwords per (k-tile, row) actually staged
   constexpr int A_F4 = BM * AWL / 4;         // float4 per A tile
   constexpr int A_PER = (A_F4 + NT - 1) / NT;
   constexpr int ROWSTEP = NBT / BN;          // B rows covered per pass
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     } else if constexpr (PREC != 0) {  // bf16 row: [hi k0..15][lo k0..15], this thread's k contiguous
       uint32_t h[B_PER / 2], l[B_PER / 2];
 #pragma unroll
-      for (int q = 0; q < B_PER / 2; ++q) split_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
+      for (int q = 0; q < B_PER / 2; ++q) split2<PREC>(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
       uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
       if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
         *reinterpret_cast<u32x4*>(d + 4 * brow0) = u32x4{h[0], h[1], h[2], h[3]};
@@ -602,8 +602,8 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T128A:  // four A-direct waves of 32 rows x 128 pixels
       if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
       break;
-    case T256:  // bf16x3 / bf16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
-      if constexpr (PR == 1 || PR == 2) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR>(grid, st, P);
+    case T256:  // bf16x3 / bf16 / fp16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
+      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR>(grid, st, P);
       break;
     default: launch_k<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR>(grid, st, P); break;
   }
@@ -622,5 +622,6 @@ extern template void launch_prec<0>(bool, bool, int, dim3, hipStream_t, const Co
 extern template void launch_prec<1>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 extern template void launch_prec<2>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 extern template void launch_prec<3>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_prec<4>(bool, bool, int, dim3, hipStream_t, const ConvParams&);
 
 }  // namespace vstk

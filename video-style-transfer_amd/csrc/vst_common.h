@@ -68,14 +68,16 @@ static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int vst_mode_arith(int mode) { return mode & ~VST_GEMM_KBLOCK; }
 static inline bool vst_mode_ok(int mode) {
   const int a = vst_mode_arith(mode);
-  return (mode & ~(VST_GEMM_KBLOCK | 3)) == 0 &&
-         (a == VST_GEMM_F32 || a == VST_GEMM_BF16X3 || a == VST_GEMM_BF16 || a == VST_GEMM_BF16X6);
+  return (mode & ~(VST_GEMM_KBLOCK | 7)) == 0 &&
+         (a == VST_GEMM_F32 || a == VST_GEMM_BF16X3 || a == VST_GEMM_BF16 || a == VST_GEMM_BF16X6 ||
+          a == VST_GEMM_F16);
 }
-// packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6); bit 4:
-// channel-blocked K order (kblocked)
+// packed-A layout of a mode: 0 fp32, 1 hi+lo bf16 (bf16x3, bf16), 2 hi+mid+lo bf16 (bf16x6), 3 fp16
+// (hi slot only, same 64-B blocks as 1); bit 4: channel-blocked K order (kblocked)
 static inline int apack_split(int mode) {
   const int a = vst_mode_arith(mode);
-  return (a == VST_GEMM_F32 ? 0 : (a == VST_GEMM_BF16X6 ? 2 : 1)) | ((mode & VST_GEMM_KBLOCK) ? 16 : 0);
+  const int s = a == VST_GEMM_F32 ? 0 : (a == VST_GEMM_BF16X6 ? 2 : (a == VST_GEMM_F16 ? 3 : 1));
+  return s | ((mode & VST_GEMM_KBLOCK) ? 16 : 0);
 }
 
 // K order of a conv GEMM (the packed A rows and the kernel's B walk must agree).  With
@@ -118,6 +120,8 @@ __host__ __device__ inline long apack_index(int k, int m, int Mpad) {
 // is only valid for GEMM calls with that same mode.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -127,11 +131,29 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
+// two floats -> packed fp16 pair (round to nearest even; |x| > 65504 -> inf), element 0 low
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+  f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
+}
+
 // split (a, b) into packed hi and lo bf16 pairs: a = hi_a + lo_a (+ ~2^-17 relative)
 __device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pack_bf16x2(a, b);
   const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xffff0000u);
   lo = pack_bf16x2(a - ha, b - hb);
+}
+
+// the two-slot operand pair of a GEMM precision: PREC 1 / 2 bf16 hi + lo (2 uses only hi), PREC 4
+// the fp16 value in the hi slot (no lo term)
+template <int PREC>
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  if constexpr (PREC == 4) {
+    hi = pack_f16x2(a, b);
+    lo = 0u;
+  } else {
+    split_bf16x2(a, b, hi, lo);
+  }
 }
 
 // three-way split: a = hi + mid + lo, residual ~2^-25 relative (bf16x6 mode)
@@ -154,6 +176,11 @@ __device__ __forceinline__ void apack_store(float* out, int k, int m, int Mpad, 
   }
   const int aw = split == 2 ? 24 : 16;
   unsigned short* u = reinterpret_cast<unsigned short*>(out + ((long)(k >> 4) * Mpad + m) * aw);
+  if (split == 3) {  // fp16: [f16 k0..15][unused]
+    u[k & 15] = (unsigned short)(pack_f16x2(v, 0.f) & 0xffffu);
+    u[16 + (k & 15)] = 0;
+    return;
+  }
   const uint32_t h = pack_bf16x2(v, 0.f) & 0xffffu;
   const float r = v - __uint_as_float(h << 16);
   const uint32_t md = pack_bf16x2(r, 0.f) & 0xffffu;
@@ -172,6 +199,19 @@ template <int TM, int TN, int PREC, int LS>
 __device__ __forceinline__ void mfma_bf16_ktile(f32x16 (&acc)[TM][TN], float (*A)[LS], float (*B)[LS], int a0,
                                                 int b0, int lane) {
   const int r = lane & 31, h = lane >> 5;
+  if constexpr (PREC == 4) {  // fp16 rows: [f16 k0..15][unused]
+    f16x8_t af[TM], bf[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8_t*>(&A[a0 + i * 32 + r][4 * h]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8_t*>(&B[b0 + j * 32 + r][4 * h]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    return;
+  }
   bf16x8_t ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {

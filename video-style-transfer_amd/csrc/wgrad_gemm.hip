@@ -233,7 +233,7 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
       row[8 + (rr >> 1)] = md;
       row[16 + (rr >> 1)] = l;
     } else {
-      split_bf16x2(a, b, h, l);
+      split2<PREC>(a, b, h, l);
       if (PREC == 1) row[8 + (rr >> 1)] = l;
     }
     row[rr >> 1] = h;
@@ -273,8 +273,8 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
               *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{m0, m1};
               *reinterpret_cast<u32x2*>(row + 16 + 2 * q) = u32x2{l0, l1};
             } else {
-              split_bf16x2(rav[i][0], rav[i][1], h0, l0);
-              split_bf16x2(rav[i][2], rav[i][3], h1, l1);
+              split2<PREC>(rav[i][0], rav[i][1], h0, l0);
+              split2<PREC>(rav[i][2], rav[i][3], h1, l1);
               if (PREC == 1) *reinterpret_cast<u32x2*>(row + 8 + 2 * q) = u32x2{l0, l1};
             }
             *reinterpret_cast<u32x2*>(row + 2 * q) = u32x2{h0, h1};
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     } else {
       uint32_t h[4], l[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) split_bf16x2(v[2 * q], v[2 * q + 1], h[q], l[q]);
+      for (int q = 0; q < 4; ++q) split2<PREC>(v[2 * q], v[2 * q + 1], h[q], l[q]);
       uint32_t* d = reinterpret_cast<uint32_t*>(row) + 4 * half;
       *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
       if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
@@ -600,8 +600,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       *reinterpret_cast<u32x2*>(d + 16) = u32x2{l0, l1};
     } else {
       uint32_t h0, l0, h1, l1;
-      split_bf16x2(v[0], v[1], h0, l0);
-      split_bf16x2(v[2], v[3], h1, l1);
+      split2<PREC>(v[0], v[1], h0, l0);
+      split2<PREC>(v[2], v[3], h1, l1);
       *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
       if (PREC == 1) *reinterpret_cast<u32x2*>(d + 8) = u32x2{l0, l1};
     }
@@ -778,6 +778,7 @@ static void launch_wg(int c, bool tap, dim3 g, int mode, hipStream_t st, const W
     case VST_GEMM_F32: launch_wg_p<0>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg_p<2>(av, tap, c, g, st, P); break;
     case VST_GEMM_BF16X6: launch_wg_p<3>(av, tap, c, g, st, P); break;
+    case VST_GEMM_F16: launch_wg_p<4>(av, tap, c, g, st, P); break;
     default: launch_wg_p<1>(av, tap, c, g, st, P); break;
   }
 }
@@ -830,6 +831,7 @@ static void launch_wg2(int c, dim3 g, int mode, hipStream_t st, const Wg2Params&
     case VST_GEMM_F32: launch_wg2_p<0, GMD>(c, g, st, P); break;
     case VST_GEMM_BF16: launch_wg2_p<2, GMD>(c, g, st, P); break;
     case VST_GEMM_BF16X6: launch_wg2_p<3, GMD>(c, g, st, P); break;
+    case VST_GEMM_F16: launch_wg2_p<4, GMD>(c, g, st, P); break;
     default: launch_wg2_p<1, GMD>(c, g, st, P); break;
   }
 }

@@ -71,6 +71,7 @@ class AdaAttNTrainer:
         # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
         broadcast_params(self.flat.p, process_group)
         self.dp = GradBuckets(model, self.flat, process_group)
+        self._seed = None
 
     def encode(self, c1, c2=None, s=None):
         """VGG19 features of the data images (no gradient).  c1 may be a [3, B, 3, H, W] buffer."""
@@ -139,12 +140,24 @@ class AdaAttNTrainer:
     def step(self, c1, c2=None, s=None):
         return self._update(self.losses, c1, c2, s)
 
+    def backward(self, loss):
+        """loss.backward() under the policy's static loss scale (ops.loss_scale: every gradient,
+        the flat buffer included, comes out scaled); returns the factor that unscales them."""
+        s = ops.loss_scale()
+        if s == 1.0:
+            loss.backward()
+            return 1.0
+        if self._seed is None or self._seed[0] != s:
+            self._seed = (s, torch.full((), s, device=loss.device))
+        loss.backward(self._seed[1])
+        return 1.0 / s
+
     def _update(self, losses, *args):
         self.flat.zero_grad()
         self.dp.begin()
         out = losses(*args)
-        out["loss"].backward()
-        gscale = self.dp.finish()
+        unscale = self.backward(out["loss"])
+        gscale = self.dp.finish() * unscale
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}

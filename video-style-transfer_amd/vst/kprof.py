@@ -11,8 +11,9 @@ _active = None
 
 # MFMA peak per GEMM arithmetic mode (vst_set_gemm_mode), in algorithmic fp32-operand TFLOP/s:
 # f32 = v_mfma_f32_32x32x2_f32 (157.3 TF); bf16x3 = 3 bf16 MFMAs per product (2500 / 3);
-# bf16 = 2500 (dense bf16 MFMA, MI355X_MICROARCH.md); bf16x6 = 6 bf16 MFMAs per product
-MODE_PEAK_TFLOPS = {0: 157.3, 1: 2500.0 / 3.0, 2: 2500.0, 3: 2500.0 / 6.0}
+# bf16 = 2500 (dense bf16 MFMA, MI355X_MICROARCH.md); bf16x6 = 6 bf16 MFMAs per product;
+# f16 = 2500 (dense fp16 MFMA)
+MODE_PEAK_TFLOPS = {0: 157.3, 1: 2500.0 / 3.0, 2: 2500.0, 3: 2500.0 / 6.0, 4: 2500.0}
 
 
 class KernelTimer:

@@ -35,7 +35,7 @@ def _check(t, name, ndim=None):
     return t.contiguous()
 
 
-GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3}
+GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3, "f16": 4}
 KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
 # where the channel-blocked K order applies (VST_KBLOCK): "res" (default) the loss networks, every
 # data gradient and the stylizer's residual-block forwards; "1" not inside the stylizer forward at
@@ -91,14 +91,32 @@ def _mode_id(mode):
 #     (tools/policy_check.py: all stylizer forwards bf16x3 -> 1.07 of the gradient tolerance on the
 #     ragged golden step; none -> 0.002); the softmax attention stays exact fp32.
 #   "bf16x3": every GEMM split in two (fails the ragged golden step's gradient tolerance, 1.07).
-#   "bf16": single bf16 products (~2^-8): the reduced-precision path of BASELINE config 5.
+#   "bf16": single bf16 products (~2^-8): a reduced-precision option for BASELINE config 5.
+#   "f16": single fp16 products (~2^-11 per operand) with a static loss scale (LOSS_SCALE): the
+#     fp16 MFMA path BASELINE config 5 names.
 POLICIES = {
     "f32": ("f32", {}),
     "bf16x6": ("bf16x6", {"attn_softmax": "f32"}),
     "parity": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6", "attn_softmax": "f32"}),
     "bf16x3": ("bf16x3", {}),
     "bf16": ("bf16", {}),
+    # the linear-form cosine attention's intermediates (G = K^ [V; V^2]^T sums over every style
+    # position) leave fp16's range at 2^12-scaled gradients: its products stay on bf16x3 (fp32
+    # exponent range, ~2^-16; a small share of the step's FLOPs)
+    "f16": ("f16", {"attn_cosine": "bf16x3", "attn_softmax": "f32"}),
 }
+# Static loss scale of a policy: the trainers run backward from loss * scale and Adam unscales.
+# fp16 operands must lie in [6.1e-5, 65504] to keep their 11-bit significand: the step's
+# backward GEMM operands (gradients) reach at most ~0.85 and go down to ~1e-11
+# (profiles/r02_fp16_range.json), so 2^12 lifts all but the smallest into the normal range while
+# leaving 16x headroom below the fp16 maximum; forward operands (|x| <= ~3.5e3) are not scaled.
+LOSS_SCALE = {"f16": 2.0 ** 12}
+
+
+def loss_scale():
+    """The static loss scale of the selected policy (1.0 unless the policy computes in fp16)."""
+    _ensure_policy()
+    return LOSS_SCALE.get(POLICY_NAME[0], 1.0)
 
 
 def _ensure_policy():

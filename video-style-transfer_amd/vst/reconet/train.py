@@ -80,6 +80,7 @@ class ReCoNetTrainer:
         # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
         broadcast_params(self.flat.p, process_group)
         self.dp = GradBuckets(model, self.flat, process_group)
+        self._seed = None
         dev = self.flat.p.device
         self.chscale_cache = {}
         with torch.no_grad():
@@ -161,12 +162,24 @@ class ReCoNetTrainer:
                 out["SDL"] = ops.mse(self.teacher(x)[ti], mout[si].detach(), nf * 0.01 * w["BETA"])
         return out
 
+    def backward(self, loss):
+        """loss.backward() under the policy's static loss scale (ops.loss_scale); returns the factor
+        that unscales the gradients."""
+        s = ops.loss_scale()
+        if s == 1.0:
+            loss.backward()
+            return 1.0
+        if self._seed is None or self._seed[0] != s:
+            self._seed = (s, torch.full((), s, device=loss.device))
+        loss.backward(self._seed[1])
+        return 1.0 / s
+
     def step(self, frames, flow=None, mask=None):
         self.flat.zero_grad()
         self.dp.begin()
         out = self.losses(frames, flow, mask)
-        out["loss"].backward()
-        gscale = self.dp.finish()
+        unscale = self.backward(out["loss"])
+        gscale = self.dp.finish() * unscale
         self.step_count += 1
         self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
         return {k: v.detach() for k, v in out.items()}
