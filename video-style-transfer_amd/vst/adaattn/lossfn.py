@@ -81,7 +81,7 @@ def cosine_distance(fu, fv):
     if u.shape != v.shape:
         raise VstError("cosine_distance: shape mismatch")
     N, C, _ = u.shape
-    G = gemm_abt(u, v, role="fwd")
+    G = gemm_abt(u, v, role="loss_fwd")
     un, vn = plane_norm(u), plane_norm(v)
     D = _empty((N, C, C), u)
     lib.vst_cosdist(ptr(G), ptr(un), ptr(vn), ptr(D), N, C, stream())
@@ -98,7 +98,7 @@ class ImageSimilarityFn(Function):
         if not (c1.shape == c2.shape == s1.shape == s2.shape):
             raise VstError("image_similarity_loss: all four feature maps must share a shape")
         N, C, P = c1.shape
-        Gc, Gs = gemm_abt(c1, c2, role="fwd"), gemm_abt(s1, s2, role="fwd")
+        Gc, Gs = gemm_abt(c1, c2, role="loss_fwd"), gemm_abt(s1, s2, role="loss_fwd")
         unc, vnc, uns, vns = plane_norm(c1), plane_norm(c2), plane_norm(s1), plane_norm(s2)
         colc, cols = _empty((N, C), c1), _empty((N, C), c1)
         partial = _empty((N * C,), c1)
@@ -126,12 +126,12 @@ class ImageSimilarityFn(Function):
         d1 = d2 = None
         if ctx.needs_input_grad[2]:
             # d s1[i] = sum_j dG[i][j] s2[j]  -> A op [k=j][m=i] = dG[i][j] (transpose)
-            d1 = bmm_at_b(dG, C, C, True, s2, P, role="dgrad")
+            d1 = bmm_at_b(dG, C, C, True, s2, P, role="loss_dgrad")
             lib.vst_plane_norm_grad(ptr(d1), ptr(dun), ptr(uns), ptr(s1), N * C, P, stream())
             d1 = d1.view(ctx.shape)
         if ctx.needs_input_grad[3]:
             # d s2[j] = sum_i dG[i][j] s1[i]  -> A op [k=i][m=j] = dG[i][j]
-            d2 = bmm_at_b(dG, C, C, False, s1, P, role="dgrad")
+            d2 = bmm_at_b(dG, C, C, False, s1, P, role="loss_dgrad")
             lib.vst_plane_norm_grad(ptr(d2), ptr(dvn), ptr(vns), ptr(s2), N * C, P, stream())
             d2 = d2.view(ctx.shape)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:

@@ -164,9 +164,10 @@ class AdaAttN(nn.Module):
             return self._forward(c_x, s_x, c_1x, s_1x)
 
     def _forward(self, c_x, s_x, c_1x, s_1x):
-        Q = ops.conv2d(instance_norm_plain(c_1x), self.f.weight, self.f.bias)
-        K = ops.conv2d(instance_norm_plain(s_1x), self.g.weight, self.g.bias)
-        V = ops.conv2d(s_x, self.h.weight, self.h.bias)
+        with ops.gemm_scope("attn"):  # policy key "stylizer.attn.<role>" (fp16 policy: bf16x3 here)
+            Q = ops.conv2d(instance_norm_plain(c_1x), self.f.weight, self.f.bias)
+            K = ops.conv2d(instance_norm_plain(s_1x), self.g.weight, self.g.bias)
+            V = ops.conv2d(s_x, self.h.weight, self.h.bias)
         return adaattn(Q, K, V, instance_norm_plain(c_x), self.activation.kind)
 
 

@@ -68,7 +68,8 @@ _BASE_MODE = [None]  # base mode of the selected policy (process-wide)
 _CUR = _ThreadSlot()
 # per-role overrides of the base mode; roles: "fwd" (forward products), "fwd_img" (Cin = 3),
 # "dgrad" (data gradients, Gram backward), "wgrad" (weight gradients, Gram), "attn_cosine" /
-# "attn_softmax" (AdaAttN attention products, fwd + bwd)
+# "attn_softmax" (AdaAttN attention products, fwd + bwd), "loss_fwd" / "loss_dgrad" (the AdaAttN
+# cosine-distance products of the image-similarity loss)
 GEMM_POLICY = {}
 DEFAULT_POLICY = "f32"
 
@@ -100,10 +101,13 @@ POLICIES = {
     "parity": ("bf16x3", {"stylizer.fwd": "bf16x6", "stylizer.fwd_img": "bf16x6", "attn_softmax": "f32"}),
     "bf16x3": ("bf16x3", {}),
     "bf16": ("bf16", {}),
-    # the linear-form cosine attention's intermediates (G = K^ [V; V^2]^T sums over every style
-    # position) leave fp16's range at 2^12-scaled gradients: its products stay on bf16x3 (fp32
-    # exponent range, ~2^-16; a small share of the step's FLOPs)
-    "f16": ("f16", {"attn_cosine": "bf16x3", "attn_softmax": "f32"}),
+    # inside the AdaAttN modules (the 1x1 f / g / h projections and the linear-form cosine
+    # attention, whose intermediates G = K^ [V; V^2]^T sum over every style position) and in the
+    # image-similarity loss (the C x C cosine-distance matrix gradient) the 2^12-scaled gradients
+    # leave fp16's range (tools/nan_diag.py): those products stay on bf16x3 (fp32 exponent range,
+    # ~2^-16; a small share of the step's FLOPs)
+    "f16": ("f16", {"stylizer.attn.fwd": "bf16x3", "stylizer.attn.dgrad": "bf16x3", "stylizer.attn.wgrad": "bf16x3",
+                    "attn_cosine": "bf16x3", "attn_softmax": "f32", "loss_fwd": "bf16x3", "loss_dgrad": "bf16x3"}),
 }
 # Static loss scale of a policy: the trainers run backward from loss * scale and Adam unscales.
 # fp16 operands must lie in [6.1e-5, 65504] to keep their 11-bit significand: the step's
@@ -170,6 +174,7 @@ def policy_modes():
 
 
 _SCOPE = _ThreadSlot()
+_PSCOPE = _ThreadSlot()  # forward scope re-entered by a backward (policy_scope)
 
 
 @contextlib.contextmanager
@@ -185,12 +190,25 @@ def gemm_scope(name):
         _SCOPE[0] = old
 
 
+@contextlib.contextmanager
+def policy_scope(name):
+    """Backward passes run after their forward's gemm_scope has closed (and on autograd's thread):
+    a Function that recorded its forward scope re-enters it here, for the POLICY lookup of its
+    backward GEMMs only (the channel-blocked K-order choice keeps using the live scope)."""
+    old = _PSCOPE[0]
+    _PSCOPE[0] = name
+    try:
+        yield
+    finally:
+        _PSCOPE[0] = old
+
+
 def gemm_role(role):
     """Choose the mode for a GEMM of `role` (call before packing its A operand); the first call
     applies the VST_GEMM_POLICY environment variable (default "f32")."""
     _ensure_policy()
     m = None
-    sc = _SCOPE[0]
+    sc = _PSCOPE[0] if _PSCOPE[0] is not None else _SCOPE[0]
     while sc is not None and m is None:
         m = GEMM_POLICY.get(f"{sc}.{role}")
         sc = sc.rpartition(".")[0] or None
@@ -572,6 +590,7 @@ class Conv2dFn(Function):
             out = conv_gemm(x, packed_weight(w, False), Cout, ks, Ho, Wo, GM_REFLECT if pad_mode == "reflect" else GM_ZERO,
                             stride, pad, up, epi=epi, bias=bias, aux=aux)
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
+        ctx.scope = _SCOPE[0]
         ctx.relu_flags = (bool(mask_dx), bool(premasked))
         ctx.has_bias = b is not None and bias_const is None
         ctx.params = (w, b)  # leaves: weight gradients go straight into their .grad when possible
@@ -580,6 +599,11 @@ class Conv2dFn(Function):
 
     @staticmethod
     def backward(ctx, gy):
+        with policy_scope(ctx.scope):
+            return Conv2dFn._backward(ctx, gy)
+
+    @staticmethod
+    def _backward(ctx, gy):
         x, w, y, t = ctx.saved_tensors
         ks, stride, pad, pad_mode, up, act = ctx.geom
         gy = gy.contiguous()
