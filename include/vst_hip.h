@@ -99,7 +99,9 @@ int vst_rowsplit_reduce(const float* P, const float* bias, float* out, float* au
 int vst_pack_weight_phase2(const float* w, float* packed, int Cout, int Cin, int KS, int Mpad, int Kpad, int mode, void* stream);
 int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, float* dx, float* border, int N,
                       int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
-int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream);
+/* mask (optional, dx-shaped): the fold adds only where mask > 0 (the producer's ReLU backward fused
+ * into a masked data gradient: the GEMM epilogue already zeroed dx there) */
+int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream);
 /* Thin-channel convolutions (RC/network.py:155 conv1 = ConvLayer(3, 48, 9), :169 deconv3 =
  * ConvTanh(48, 3, 9) backward, VGG conv1_1): a tensor with C*K <= Cu channels is kw-unfolded,
  *   out[n][c*K + kw][y][v] = src[n][c][y][v + sgn*kw + off]  (reflect or zero outside; zero channels
@@ -123,19 +125,21 @@ int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, 
                        int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
                        int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
                        int mode, void* stream);
-int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
-                              int Cin, int H, int W, int KS, int pad, int mode, void* stream);
+int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, const float* mask, float* dx, float* border, int N,
+                              int Cu, int Ho, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 /* data gradient of a zero-padded stride-1 KxK conv with few input channels (VGG conv1_1, 64 -> 3):
  * P = tap-split 1x1 transposed GEMM (vst_conv_gemm with A = vst_pack_weight of w viewed as
  * [Cout][Cin*K*K][1][1], transposed; rows (c, kh, kw)), then
  *   dx[n][c][y][x] (+)= sum_{kh,kw} P[n][(c*K+kh)*K+kw][y+pad-kh][x+pad-kw]  (zero outside). */
 int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int pad, int accumulate, void* stream);
 /* stride-1 reflect-pad data gradient (ResidualBlock / ConvTanh backward, RC/network.py:72-75,
- * 145-150, 83-85): the transposed GEMM (A = vst_pack_weight(transposed=1)) runs over the padded
- * grid (H+2p) x (W+2p); interior pixels go straight into dx, the p-wide border into border
- * [N][Cin][H+2p][W+2p]; then vst_fold_border. */
-int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,
-                          int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
+ * 145-150, 83-85; the AdaAttN decoder's Conv / ConvReLU, AA/network.py:11-33): the transposed GEMM
+ * (A = vst_pack_weight(transposed=1)) runs over the padded grid (H+2p) x (W+2p); interior pixels go
+ * straight into dx, the p-wide border into border [N][Cin][H+2p][W+2p]; then vst_fold_border.
+ * mask (optional, dx-shaped; the same pointer to vst_fold_border): dx is written only where
+ * mask > 0 (the ReLU backward of a conv+ReLU producing this conv's input, fused). */
+int vst_conv_dgrad_padout(const float* dy, const float* wpack, const float* mask, float* dx, float* border, int N,
+                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 /* Reflect-pad dgrad without the padded grid (ConvLayer / UpsampleConvLayer backward,
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of

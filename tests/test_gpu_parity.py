@@ -182,6 +182,45 @@ def test_conv_relu_frozen_weights_dgrad_mask():
     assert rel_err(C(xg.grad), xr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16x6", "f16"])
+@pytest.mark.parametrize("cmid,cout", [(32, 48), (64, 3)])
+def test_reflect_conv_relu_chain_masked_dgrad(mode, cmid, cout):
+    """AdaAttN decoder chain (AA/network.py:24-33, 79-99): reflect-pad conv + ReLU whose output only
+    feeds the next reflect-pad conv -> the producer skips its ReLU-backward pass (premasked) and the
+    consumer's data gradient applies the mask in its padded-grid epilogue and border fold (mask_dx;
+    cout = 3 takes the kw-unfolded thin path).  Input and weight gradients vs fp32 torch."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 16, 11, 19, generator=g)
+    w1 = torch.randn(cmid, 16, 3, 3, generator=g) * 0.15
+    b1 = torch.randn(cmid, generator=g) * 0.1
+    w2 = torch.randn(cout, cmid, 3, 3, generator=g) * 0.1
+    b2 = torch.randn(cout, generator=g) * 0.1
+    ref = [t.clone().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y1 = torch.relu(F.conv2d(R.reflect_pad(ref[0], 1), ref[1], ref[2]))
+    y2 = F.conv2d(R.reflect_pad(y1, 1), ref[3], ref[4])
+    gy = torch.randn(y2.shape, generator=g)
+    y2.backward(gy)
+    ops.gemm_role("fwd")
+    old = ops.POLICY_NAME[0]
+    ops.set_gemm_mode(mode, policy={})
+    try:
+        hip = [G(t).requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+        z1 = ops.conv2d(hip[0], hip[1], hip[2], pad=1, pad_mode="reflect", act="relu", premasked=True)
+        z2 = ops.conv2d(z1, hip[3], hip[4], pad=1, pad_mode="reflect", mask_dx=True)
+        z2.backward(G(gy))
+        torch.cuda.synchronize()
+    finally:
+        ops.use_policy(old)
+    # fp16: 2^-11 products, and the fp16 forward's ReLU decisions near 0 differ from fp32's, which moves
+    # the masked gradients (the conv tests' BF16_RELU_GRAD_TOL reasoning)
+    tol = 1e-2 if mode == "f16" else 1e-4
+    assert _norm_err(C(z2), y2.detach()) < tol
+    for a, b_, nm in zip(hip, ref, ("dx", "dw1", "db1", "dw2", "db2")):
+        assert _norm_err(C(a.grad), b_.grad) < (5e-2 if mode == "f16" else tol), nm
+
+
 def test_vgg_slice_fused_relu_backward():
     """run_vgg_slice: ReLU outputs consumed only by the next conv / pool get their backward mask
     from the consumer (dgrad epilogue, pool backward); the slice output keeps its own pass."""

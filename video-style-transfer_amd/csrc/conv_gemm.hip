@@ -207,8 +207,8 @@ __global__ void pack_kwu_kernel(const float* __restrict__ w, float* __restrict__
 
 // dx (+)= the reflect-pad border of the padded-grid gradient (the interior went straight to dx):
 // one thread per element of dx's border band (rows/cols within pad+1 of an edge)
-__global__ void fold_border_kernel(const float* __restrict__ border, float* __restrict__ dx, int NC, int Hs, int Ws,
-                                   int pad) {
+__global__ void fold_border_kernel(const float* __restrict__ border, const float* __restrict__ mask,
+                                   float* __restrict__ dx, int NC, int Hs, int Ws, int pad) {
   const int nb = pad < Hs / 2 ? pad + 1 : Hs;  // band rows at each edge (rows 0..pad and Hs-1-pad..Hs-1)
   const int band_rows = nb >= Hs ? Hs : 2 * nb;
   const int nbc = pad < Ws / 2 ? pad + 1 : Ws;
@@ -239,7 +239,9 @@ __global__ void fold_border_kernel(const float* __restrict__ border, float* __re
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       if ((i | j) && us[i] >= 0 && vs[j] >= 0) s += b[(long)us[i] * Wp + vs[j]];
-  dx[((long)nc * Hs + y) * Ws + x] += s;
+  const long o = ((long)nc * Hs + y) * Ws + x;
+  if (mask && !(mask[o] > 0.f)) return;  // masked: the epilogue already wrote 0
+  dx[o] += s;
 }
 
 }  // namespace
@@ -557,34 +559,34 @@ int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K,
   return vst_launch_status();
 }
 
-int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, float* dx, float* border, int N, int Cu, int Ho,
-                              int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, const float* mask, float* dx, float* border, int N,
+                              int Cu, int Ho, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dyu && wpack && dx && border && N > 0 && Cu % 16 == 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
                 pad < W && Ho == H + 2 * pad - KS + 1);
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  return conv_gemm_launch(dyu, wpack, nullptr, nullptr, dx, N, Cu, Ho, Wp, Cin, KS * Cu, Hp, Wp, KS, 1, GM_TRANSPOSED, 1,
-                          0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, mode, stream, nullptr, nullptr, nullptr, nullptr, border,
-                          H, W, pad);
+  return conv_gemm_launch(dyu, wpack, nullptr, mask, dx, N, Cu, Ho, Wp, Cin, KS * Cu, Hp, Wp, KS, 1, GM_TRANSPOSED, 1,
+                          0, 0, 1, EPI_PADOUT | (mask ? EPI_MASK : 0), 0, nullptr, nullptr, mode, stream, nullptr,
+                          nullptr, nullptr, nullptr, border, H, W, pad);
 }
 
-int vst_conv_dgrad_padout(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout, int Ho,
-                          int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+int vst_conv_dgrad_padout(const float* dy, const float* wpack, const float* mask, float* dx, float* border, int N,
+                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
                 pad < W && Ho == H + 2 * pad - KS + 1 && Wo == W + 2 * pad - KS + 1);
-  return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, Cin, KS * KS * Cout, H + 2 * pad,
-                          W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT, 0, nullptr, nullptr, mode, stream,
-                          nullptr, nullptr, nullptr, nullptr, border, H, W, pad);
+  return conv_gemm_launch(dy, wpack, nullptr, mask, dx, N, Cout, Ho, Wo, Cin, KS * KS * Cout, H + 2 * pad,
+                          W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT | (mask ? EPI_MASK : 0), 0, nullptr,
+                          nullptr, mode, stream, nullptr, nullptr, nullptr, nullptr, border, H, W, pad);
 }
 
-int vst_fold_border(const float* border, float* dx, long NC, int H, int W, int pad, void* stream) {
+int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream) {
   VST_CHECK_ARG(border && dx && NC > 0 && H > 0 && W > 0 && pad >= 0 && pad < H && pad < W);
   if (pad == 0) return VST_OK;
   const int nb = pad < H / 2 ? pad + 1 : H, nbc = pad < W / 2 ? pad + 1 : W;
   const int br = nb >= H ? H : 2 * nb, bc = nbc >= W ? W : 2 * nbc;
   const long total = ((long)br * W + (long)(H - br) * bc) * NC;
-  fold_border_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(border, dx, (int)NC, H, W, pad);
+  fold_border_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(border, mask, dx, (int)NC, H, W, pad);
   return vst_launch_status();
 }
 

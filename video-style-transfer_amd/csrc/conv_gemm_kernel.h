@@ -459,12 +459,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
         const bool in = y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W;
         float* base = in ? dx_n + (long)y * P.ph_W + x : bd_n + (long)I * Wp + J;
         const long cstride = in ? (long)P.ph_H * P.ph_W : (long)Hp * Wp;
+        // EPI_MASK: interior values gated by the dx-shaped mask (the border keeps the raw values;
+        // vst_fold_border applies the same mask when it folds them in)
+        const float* mk = (in && (P.epi & EPI_MASK)) ? P.mask + (long)n * Cx * P.ph_H * P.ph_W + (long)y * P.ph_W + x
+                                                      : nullptr;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int ci = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (ci < Cx) base[ci * cstride] = acc[i][j][r];
+            if (ci < Cx) base[ci * cstride] = (mk && !(mk[ci * cstride] > 0.f)) ? 0.f : acc[i][j][r];
           }
         continue;
       }

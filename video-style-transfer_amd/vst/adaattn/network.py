@@ -27,9 +27,10 @@ class Conv(nn.Module):
         self.pad = nn.ReflectionPad2d(pad)
         self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride)
 
-    def run(self, x, act=None):
+    def run(self, x, act=None, mask_dx=False, premasked=False):
         c = self.conv
-        return ops.conv2d(x, c.weight, c.bias, stride=c.stride[0], pad=self.pad.padding[0], pad_mode="reflect", act=act)
+        return ops.conv2d(x, c.weight, c.bias, stride=c.stride[0], pad=self.pad.padding[0], pad_mode="reflect", act=act,
+                          mask_dx=mask_dx, premasked=premasked)
 
     def forward(self, x):
         return self.run(x)
@@ -42,6 +43,9 @@ class ConvReLU(nn.Module):
         super().__init__()
         self.conv = Conv(in_channels, out_channels, kernel_size, stride)
         self.relu = nn.ReLU()
+
+    def run(self, x, act="relu", mask_dx=False, premasked=False):
+        return self.conv.run(x, act=act, mask_dx=mask_dx, premasked=premasked)
 
     def forward(self, x):
         return self.conv.run(x, act="relu")
@@ -97,13 +101,23 @@ class Decoder(nn.Module):
             return self._forward(x5, x4, x3)
 
     def _forward(self, x5, x4, x3):
+        # a ConvReLU whose output only feeds the next conv leaves its ReLU backward to that conv's
+        # data gradient (premasked -> mask_dx: the mask is applied in the dgrad epilogue and border
+        # fold); the outputs that feed an upsample keep the separate ReLU-backward pass
+        def run(m, x, mask_dx=False, premasked=False):
+            return m.run(x, act="relu" if isinstance(m, ConvReLU) else None, mask_dx=mask_dx, premasked=premasked)
+
         x = ops.upsample2x(x5, addend=x4)
-        x = self.conv1(x)
-        x = ops.upsample_cat(self.conv2(x), x3)
-        x = self.conv3(x)
-        x = ops.upsample2x(self.conv4(x))
-        x = ops.upsample2x(self.conv6(self.conv5(x)))
-        return self.conv8(self.conv7(x))
+        x = run(self.conv1, x, premasked=True)
+        x = ops.upsample_cat(run(self.conv2, x, mask_dx=True), x3)
+        x = run(self.conv3[0], x, premasked=True)
+        x = run(self.conv3[1], x, mask_dx=True, premasked=True)
+        x = run(self.conv3[2], x, mask_dx=True, premasked=True)
+        x = ops.upsample2x(run(self.conv4, x, mask_dx=True))
+        x = run(self.conv5, x, premasked=True)
+        x = ops.upsample2x(run(self.conv6, x, mask_dx=True))
+        x = run(self.conv7, x, premasked=True)
+        return run(self.conv8, x, mask_dx=True)
 
 
 class Softmax(nn.Module):

@@ -330,7 +330,8 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
 
 def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=None):
     """Input gradient of (upsample x`up` -> pad -> conv(stride)) given the conv-output grad gz;
-    dmask: multiply the result by (dmask > 0) in the GEMM epilogue (zero-pad path only)."""
+    dmask: multiply the result by (dmask > 0) in the GEMM epilogue (zero-pad path, and the
+    stride-1 reflect-pad padded-grid path with its border fold)."""
     gemm_role("dgrad")
     N, Cin, H, W = x_shape
     Cout = w.shape[0]
@@ -348,16 +349,18 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
         return conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1,
                          gmask=gmask, algo_flops=flops, epi=EPI_MASK if dmask is not None else 0,
                          mask=dmask.contiguous() if dmask is not None else None)
-    if dmask is not None:
-        raise VstError("dgrad: fused ReLU mask only on the zero-pad (VGG) path")
+    padout = pad_mode == "reflect" and stride == 1 and up == 1 and gmask is None and 0 < pad < min(H, W)
+    if dmask is not None and not padout:
+        raise VstError("dgrad: fused ReLU mask only on the zero-pad and stride-1 reflect-pad paths")
     if pad_mode != "reflect":
         raise VstError("dgrad: zero padding with upsampling is not on the reference path")
     if stride == 2 and up == 1:
         return conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask, flops)
-    if stride == 1 and up == 1 and gmask is None and 0 < pad < min(H, W):
+    if padout:
+        dm = dmask.contiguous() if dmask is not None else None
         if kwu_ok(Cout, ks, stride, up, W + 2 * pad) and w.shape[2] == ks:
-            return conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops)
-        return conv_dgrad_padout(gz, w, x_shape, ks, pad, flops)
+            return conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dm)
+        return conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dm)
     if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
         return conv_dgrad_ring(gz, w, x_shape, ks, up, flops)
     Hp, Wp = H * up + 2 * pad, W * up + 2 * pad
@@ -368,7 +371,7 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
     return dx
 
 
-def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops):
+def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dmask=None):
     """Stride-1 reflect-pad conv input gradient: the transposed GEMM over the padded grid writes
     its interior straight into dx and its border into a side buffer, folded into dx's border band."""
     N, Cin, H, W = x_shape
@@ -378,14 +381,14 @@ def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops):
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
     tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
-    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad, gemm_mode(),
-                              stream())
+    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
+                              gemm_mode(), stream())
     kprof.end(tok)
-    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
+    lib.vst_fold_border(ptr(border), ptr(dmask), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
 
 
-def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops):
+def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dmask=None):
     """conv_dgrad_padout for a thin output gradient (ConvTanh 48->3): dy is kw-unfolded first,
     dyu[co*K + kw][y][v] = dy[co][y][v - kw] over the padded width, so the transposed GEMM is a
     Kx1 gather over 16-multiple channels."""
@@ -398,10 +401,10 @@ def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops):
     tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, dyu.shape[1], Ho, W + 2 * pad, Cin, H + 2 * pad, W + 2 * pad, 1, ks, GM_TRANSPOSED, 1, 0, 1),
                       gemm_mode())
-    lib.vst_conv_dgrad_padout_kwu(ptr(dyu), ptr(wp), ptr(dx), ptr(border), N, dyu.shape[1], Ho, Cin, H, W, ks, pad,
-                                  gemm_mode(), stream())
+    lib.vst_conv_dgrad_padout_kwu(ptr(dyu), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, dyu.shape[1], Ho, Cin, H, W,
+                                  ks, pad, gemm_mode(), stream())
     kprof.end(tok)
-    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
+    lib.vst_fold_border(ptr(border), ptr(dmask), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
 
 
@@ -444,7 +447,7 @@ def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
     lib.vst_conv_dgrad_s2(ptr(gz), ptr(wp), ptr(gmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
                           gemm_mode(), stream())
     kprof.end(tok)
-    lib.vst_fold_border(ptr(border), ptr(dx), N * Cin, H, W, pad, stream())
+    lib.vst_fold_border(ptr(border), None, ptr(dx), N * Cin, H, W, pad, stream())
     return dx
 
 
