@@ -299,21 +299,23 @@ def test_train_image_step_golden(golden, step_policy):
         assert np.abs(got - s[f"phead/{n}"])[sel].max(initial=0) < 1e-5, n
 
 
-# BASELINE config 5 runs AdaAttN on half-precision MFMA.  Here that is the "bf16" policy: every
-# GEMM a single bf16 product (8-bit significand, ~2^-8 = 3.9e-3 relative per product) with fp32
-# accumulation and fp32 everywhere else.  The reference has no half-precision path (AA/utilities.py:81
-# forces .float()), so its step is the fp32 golden and the bar is this policy's own, stated here and
-# set from the measured errors (tests/test_gpu_adaattn.py::test_train_video_step_bf16_policy log line):
+# BASELINE config 5 runs AdaAttN on half-precision MFMA.  Its policy here is "f16": every
+# convolution a single fp16 product (11-bit significand, ~2^-11 relative per operand rounding) with
+# fp32 accumulation and a static 2^12 loss scale, the AdaAttN modules and the image-similarity
+# products on bf16x3 ("Config 5's precision, measured").  "bf16" (single bf16
+# products, 2^-8) is kept as an option and "bf16x3" (2^-16) is the fp32-class alternative.  The
+# reference has no half-precision path (AA/utilities.py:81 forces .float()), so its step is the fp32
+# golden and the bar is a single-half-precision-product policy's own, stated here (set at round 2
+# from bf16's errors at this size; at 512x1024 bench.py's full_size_parity applies it too, where
+# bf16 fails it and f16 passes):
 #   loss terms            <= 2e-2 relative
 #   each gradient tensor  norm within 5e-2 of the reference norm (+5e-3 of the largest norm)
 #   whole gradient        cosine similarity with the reference >= 0.99
-# fp16 (11-bit significand) is not used: the backward operands of this step span far below fp16's
-# normal range (tools/fp16_range.py, profiles/r02_fp16_range.json) and would need loss scaling; bf16
-# keeps fp32's exponent range.
 BF16_LOSS_TOL, BF16_GNORM_TOL, BF16_COS_MIN = 2e-2, 5e-2, 0.99
 
 
-def test_train_video_step_bf16_policy(golden):
+@pytest.mark.parametrize("policy", ["f16", "bf16", "bf16x3"])
+def test_train_video_step_reduced_policy(golden, policy):
     from vst import ops
     from vst.adaattn.network import StylizingNetwork
     from vst.adaattn.train import AdaAttNTrainer
@@ -322,7 +324,7 @@ def test_train_video_step_bf16_policy(golden):
     s = golden("aa_step")
     seeds = s["seeds"]
     old = ops.POLICY_NAME[0] or ops.DEFAULT_POLICY
-    ops.use_policy("bf16")
+    ops.use_policy(policy)
     try:
         model = _seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), int(seeds[0])).to(DEV)
         vgg = _seeded(VGG19(), shapes.vgg19(), int(seeds[1])).to(DEV)
@@ -330,22 +332,22 @@ def test_train_video_step_bf16_policy(golden):
         frames = torch.stack([G(s["c1"]), G(s["c2"]), G(s["style"])])
         tr.flat.zero_grad()
         out = tr.losses(frames)
-        out["loss"].backward()
+        unscale = tr.backward(out["loss"])  # the policy's static loss scale, as the trainer steps
         torch.cuda.synchronize()
     finally:
         ops.use_policy(old if old in ops.POLICIES else ops.DEFAULT_POLICY)
     lerr = {k: rel_err(out[k].item(), s[k]) for k in ("loss", "loss_gs", "loss_lf", "loss_is")}
     names = list(s["names"])
-    named = dict(model.named_parameters())
+    grads = {n: C(p.grad * unscale) for n, p in model.named_parameters()}
     gmax = max(float(s[f"gnorm/{n}"]) for n in names)
-    gerr = {n: abs(float(C(named[n].grad).double().norm()) - float(s[f"gnorm/{n}"])) /
+    gerr = {n: abs(float(grads[n].double().norm()) - float(s[f"gnorm/{n}"])) /
             (float(s[f"gnorm/{n}"]) + 0.1 * gmax) for n in names}
     # direction of the whole gradient from the sampled elements (256 per tensor, golden indices)
-    a = np.concatenate([C(named[n].grad).reshape(-1)[s[f"gidx/{n}"]].numpy() / float(s[f"gnorm/{n}"] + 1e-30)
+    a = np.concatenate([grads[n].reshape(-1)[s[f"gidx/{n}"]].numpy() / float(s[f"gnorm/{n}"] + 1e-30)
                         for n in names])
     b = np.concatenate([s[f"gval/{n}"] / float(s[f"gnorm/{n}"] + 1e-30) for n in names])
     cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
-    print(f"bf16 policy: loss rel err {lerr}, worst grad-norm err {max(gerr.values()):.3e} "
+    print(f"{policy} policy: loss rel err {lerr}, worst grad-norm err {max(gerr.values()):.3e} "
           f"({max(gerr, key=gerr.get)}), sampled-gradient cosine {cos:.6f}")
     assert max(lerr.values()) <= BF16_LOSS_TOL, lerr
     assert max(gerr.values()) <= BF16_GNORM_TOL, gerr
