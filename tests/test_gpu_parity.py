@@ -653,3 +653,33 @@ def test_sd2_distillation_step_golden(golden):
         assert abs(float(gr.double().norm()) - gn) <= 1e-3 * gn + 1e-4 * gmax, n
         idx = s[f"sd2_gidx/{n}"]
         assert np.abs(gr[idx].numpy() - s[f"sd2_gval/{n}"]).max() <= 1e-3 * gn + 1e-4 * gmax, n
+
+
+def test_fit_loop_sync_free_log(tmp_path):
+    """vst.reconet.loop.fit over a FramePairLoader-shaped batch stream with StepLog: the JSONL
+    means equal the per-step loss terms the trainer returned (read back only at the end), and the
+    epoch checkpoint has the reference's state_dict keys."""
+    import json
+
+    from vst.reconet import network as N
+    from vst.reconet.loop import StepLog, fit
+    from vst.reconet.train import ReCoNetTrainer
+    from vst.synthetic import frame_pair_batch, style_image
+
+    model = _seeded(N.ReCoNet(), shapes.reconet(), 1).to(DEV)
+    vgg = _seeded(N.Vgg16(), shapes.vgg16(), 2).to(DEV)
+    tr = ReCoNetTrainer(model, vgg, G(style_image(3, 32, 64)))
+    batches = [tuple(G(t) for t in frame_pair_batch(40 + i, 1, 32, 64, mask_fn=R.flow_warp_mask)) for i in range(3)]
+    outs = []
+    step = tr.step
+    tr.step = lambda *a: outs.append(step(*a)) or outs[-1]
+    log = StepLog(str(tmp_path / "log.jsonl"), every=2, units_per_step=1)
+    fit(tr, batches, epochs=1, log=log, checkpoint=str(tmp_path / "ckpt_{epoch}.pth"))
+    recs = [json.loads(line) for line in open(tmp_path / "log.jsonl")]
+    assert [r["steps"] for r in recs] == [2, 1]
+    for k in ("loss", "FTL", "OTL", "CL", "SL", "RL"):
+        vals = [float(o[k]) for o in outs]
+        assert abs(recs[0][k] - (vals[0] + vals[1]) / 2) <= 1e-6 * abs(recs[0][k]), k
+        assert abs(recs[1][k] - vals[2]) <= 1e-6 * abs(recs[1][k]), k
+    sd = torch.load(tmp_path / "ckpt_1.pth", weights_only=True)
+    assert sorted(sd) == sorted(n for n, _ in shapes.reconet())

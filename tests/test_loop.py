@@ -1,0 +1,49 @@
+"""vst.reconet.loop: sync-free step logging and the reference's epoch loop (host logic, CPU)."""
+import json
+
+import torch
+
+from vst.reconet.loop import StepLog, fit
+
+
+def test_steplog_window_means_and_jsonl(tmp_path):
+    path = tmp_path / "log.jsonl"
+    log = StepLog(str(path), every=2, units_per_step=8)
+    vals = [1.0, 3.0, 5.0, 7.0, 11.0]
+    for i, v in enumerate(vals):
+        log.add({"loss": torch.tensor(v), "CL": torch.tensor(2 * v), "not_scalar": torch.ones(3)}, epoch=1)
+    assert len(log.records) == 2 and log.window  # the last step waits for the next flush
+    log.flush()
+    recs = [json.loads(line) for line in open(path)]
+    assert [r["steps"] for r in recs] == [2, 2, 1]
+    assert [r["loss"] for r in recs] == [2.0, 6.0, 11.0]
+    assert [r["CL"] for r in recs] == [4.0, 12.0, 22.0]
+    assert all("not_scalar" not in r and r["frame-pairs/s"] > 0 and r["epoch"] == 1 for r in recs)
+    assert recs[-1]["step"] == 5
+
+
+class _StubTrainer:
+    """records the batches it is stepped with; returns the reference's loss terms as 0-d tensors"""
+
+    def __init__(self):
+        self.model = torch.nn.Linear(2, 2)
+        self.seen = []
+
+    def step(self, frames, flow=None, mask=None):
+        self.seen.append((tuple(frames.shape), tuple(flow.shape), tuple(mask.shape)))
+        n = float(len(self.seen))
+        return {"loss": torch.tensor(n), "FTL": torch.tensor(n / 2)}
+
+
+def test_fit_epochs_batches_and_checkpoints(tmp_path):
+    B, H, W = 2, 4, 6
+    batch = (torch.zeros(B, 3, H, W), torch.zeros(B, 3, H, W), torch.zeros(B, 2, H, W), torch.zeros(B, H, W))
+    tr = _StubTrainer()
+    log = StepLog(every=10)
+    fit(tr, [batch] * 3, epochs=2, log=log, checkpoint=str(tmp_path / "m_epoch_{epoch}.pth"))
+    assert tr.seen == [((2, B, 3, H, W), (B, 2, H, W), (B, H, W))] * 6
+    assert [r["steps"] for r in log.records] == [3, 3]          # flushed at each epoch end
+    assert [r["loss"] for r in log.records] == [2.0, 5.0]
+    for e in (1, 2):
+        sd = torch.load(tmp_path / f"m_epoch_{e}.pth", weights_only=True)
+        assert sorted(sd) == ["bias", "weight"]
