@@ -236,6 +236,12 @@ int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W
  * (AA/network.py:59,80,85,90,94 decoder upsampling backward) */
 int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
                             void* stream);
+/* adjoint of the x2 upsample (Ho = 2H, Wo = 2W) of the decoder (AA/network.py:59,80,85,90,94), with
+ * the fixed 4-tap weights per axis; ymask (optional, the upsample's input = a ReLU output): gx = 0
+ * where ymask <= 0, i.e. the producer ConvReLU's ReLU backward fused in (AA/network.py:28-33).  W odd or
+ * unaligned pointers fall back to the generic gather (VST_EUNSUPPORTED if a mask was asked for) */
+int vst_upsample2x_bwd(const float* gout, const float* ymask, float* gx, long NC, int C, int H, int W, long gout_bs,
+                       void* stream);
 
 /* ---- losses (RC/train_single/train_candy.py:90-145) ----------------------------------------
  * ws: >= 2048 floats; out: 3 floats {loss, weight/denom, denom count}.  Backward reads gout[0]
@@ -292,6 +298,10 @@ int vst_square_concat_bwd(const float* dVV2, const float* V, float* dV, int N, l
 /* out = sqrt(clamp(E2 - M^2, 1e-6)) * IN(c_x) + M, MV[n] = [M; E2] (AA/network.py:209-220) */
 int vst_adaattn_out(const float* MV, const float* cn, float* out, int N, long per, void* stream);
 int vst_adaattn_out_bwd(const float* dout, const float* MV, const float* cn, float* dMV, int N, long per, void* stream);
+/* the same, both halves of dMV times colscale[n][p] (per = dv * P): dRh = dMV / rs of the linear-form
+ * cosine attention (attention.py LinearCosineAttnFn) in the same pass */
+int vst_adaattn_out_bwd_scaled(const float* dout, const float* MV, const float* cn, const float* colscale, float* dMV,
+                               int N, long per, int P, void* stream);
 /* per-plane mean / unbiased std (global_stylized_loss, AA/lossfn.py:5-17) and backward */
 int vst_plane_meanstd(const float* x, float* mean, float* std_, long NC, int HW, void* stream);
 int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, const float* gmean, const float* gstd,

@@ -14,7 +14,7 @@ def test_header_parses_and_lists_entry_points():
                  # AdaAttN path
                  "vst_gemm_abt", "vst_pack_matrix", "vst_channel_norm", "vst_cos_attn_rows", "vst_cos_attn_rows_bwd",
                  "vst_softmax_rows", "vst_softmax_rows_bwd", "vst_adaattn_out", "vst_adaattn_out_bwd",
-                 "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_copy_planes",
+                 "vst_plane_meanstd", "vst_simloss", "vst_simloss_bwd", "vst_resize_bilinear_bwd", "vst_upsample2x_bwd", "vst_copy_planes",
                  "vst_build_id"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"

@@ -115,6 +115,25 @@ def test_resize_concat_ops_bwd():
     assert rel_err(C(o), ref.detach()) < 1e-5
     (o * G(w2)).sum().backward()
     assert rel_err(C(xg.grad), xr.grad) < 1e-5 and rel_err(C(yg.grad), yr.grad) == 0.0
+    # fixed-stencil x2 adjoint (even W) with and without the fused ReLU mask of a ConvReLU producer,
+    # plain and into the concat buffer; edge rows / columns (H or W = 1, 2) and an odd-W fallback
+    for (N_, C_, H_, W_) in ((2, 3, 5, 8), (1, 2, 1, 2), (1, 3, 2, 6), (2, 2, 4, 16), (1, 2, 3, 5)):
+        z = torch.randn(N_, C_, H_, W_, generator=g)
+        xr = torch.relu(z).requires_grad_(True)
+        wu = torch.randn(N_, C_, 2 * H_, 2 * W_, generator=g)
+        (A.upsample2(xr) * wu).sum().backward()
+        for relu_mask in (False, True):
+            xg = G(torch.relu(z)).requires_grad_(True)
+            (ops.upsample2x(xg, relu_mask=relu_mask) * G(wu)).sum().backward()
+            want = xr.grad * (xr.detach() > 0) if relu_mask else xr.grad
+            assert rel_err(C(xg.grad), want) < 1e-6, (N_, C_, H_, W_, relu_mask)
+        ys = torch.randn(N_, 2, 2 * H_, 2 * W_, generator=g)
+        wc = torch.randn(N_, C_ + 2, 2 * H_, 2 * W_, generator=g)
+        xr2 = torch.relu(z).requires_grad_(True)
+        (torch.cat([A.upsample2(xr2), ys], dim=1) * wc).sum().backward()
+        xg = G(torch.relu(z)).requires_grad_(True)
+        (ops.upsample_cat(xg, G(ys), relu_mask=True) * G(wc)).sum().backward()
+        assert rel_err(C(xg.grad), xr2.grad * (xr2.detach() > 0)) < 1e-6, (N_, C_, H_, W_)
     # feature_down_sample with gradient to every level
     feats = [torch.randn(2, c, hh, ww, generator=g) for c, hh, ww in ((3, 16, 20), (4, 8, 10), (5, 4, 5))]
     fr = [f.clone().requires_grad_(True) for f in feats]

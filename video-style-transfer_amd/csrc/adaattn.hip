@@ -191,6 +191,23 @@ __global__ void adaattn_out_bwd_kernel(const float* __restrict__ dout, const flo
   dMV[n * 2 * per + per + t] = dvar;
 }
 
+// the same, with the result's both halves scaled per column (dMV * w[n][p], per = dv * P): the
+// linear-form cosine attention's dRh = dMV / rs without a second pass over [M; E2]
+__global__ void adaattn_out_bwd_scaled_kernel(const float* __restrict__ dout, const float* __restrict__ MV,
+                                              const float* __restrict__ cn, const float* __restrict__ w,
+                                              float* __restrict__ dMV, int N, long per, int P) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)N * per) return;
+  long n = idx / per, t = idx - n * per;
+  const float m = MV[n * 2 * per + t], e2 = MV[n * 2 * per + per + t];
+  const float var = e2 - m * m;
+  const float g = dout[idx];
+  const float dvar = var >= 1e-6f ? g * cn[idx] * 0.5f / sqrtf(var) : 0.f;
+  const float s = w[n * P + t % P];
+  dMV[n * 2 * per + t] = (g - 2.0f * m * dvar) * s;
+  dMV[n * 2 * per + per + t] = dvar * s;
+}
+
 // per-plane mean and unbiased std (torch .mean / .std over (H, W))
 __global__ void plane_meanstd_kernel(const float* __restrict__ x, float* __restrict__ mean, float* __restrict__ std_,
                                      int HW) {
@@ -393,6 +410,14 @@ int vst_adaattn_out_bwd(const float* dout, const float* MV, const float* cn, flo
                         void* stream) {
   VST_CHECK_ARG(dout && MV && cn && dMV && N > 0 && per > 0);
   adaattn_out_bwd_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(dout, MV, cn, dMV, N, per);
+  return vst_launch_status();
+}
+
+int vst_adaattn_out_bwd_scaled(const float* dout, const float* MV, const float* cn, const float* colscale, float* dMV,
+                               int N, long per, int P, void* stream) {
+  VST_CHECK_ARG(dout && MV && cn && colscale && dMV && N > 0 && per > 0 && P > 0 && per % P == 0);
+  adaattn_out_bwd_scaled_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(dout, MV, cn, colscale,
+                                                                                            dMV, N, per, P);
   return vst_launch_status();
 }
 

@@ -116,7 +116,11 @@ __device__ __forceinline__ int a_slot2(int idx) {
 // Block = WM x WN waves (4 on the LDS-A path; 2, 6 or 8 with A-direct, where the threads that
 // divide the B tile evenly -- all of them for 2, 4 and 8 waves, the first 256 for 6 -- gather and
 // split it and every wave reads it).
-template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false>
+// KD: k-tiles per LDS stage (one barrier per KD tiles; the loads of the next KD tiles are in flight
+// across the MFMAs of the current KD).  The single-product modes (bf16, fp16) do one MFMA per
+// fragment pair, so at KD 1 their k loop is paced by the barrier and the LDS round trip of every
+// 16-deep tile rather than by the MFMAs; KD 2 halves both per MFMA.
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false, int KD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(!ADIR || PREC == 3, "A-direct: bf16x6");
   static_assert(ADIR || WM * WN == 4, "LDS-A path: 4 waves");
@@ -142,10 +146,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   const bool bthread = NTT == NBT || threadIdx.x < NBT;  // wave-uniform
 
   static_assert(BK == 16, "packed A layout assumes 16-deep k-tiles");
-  // LDS row: the A block + 4 pad dwords (20 or 28 dwords: conflict-free ds_read_b128 / ds_write_b128)
-  constexpr int LS = AW + 4;
-  __shared__ __attribute__((aligned(16))) float As[2][ADIR ? 1 : BM][LS];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
+  static_assert(KD == 1 || KD == 2, "k-tiles per stage");
+  // LDS row: the staged block + 4 pad dwords (12, 20 or 28 dwords: conflict-free ds_read_b128 over
+  // the 4 x 16-lane groups / 64 banks, and ds_write_b128 over the 8 x 8-lane groups / 32 banks)
+  constexpr int LS = AWL + 4;
+  __shared__ __attribute__((aligned(16))) float As[2][KD][ADIR ? 1 : BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][KD][BN][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -191,9 +197,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x4 ra0[A_PER];
-  float rb0[B_PER];
-  float rg0[GM ? B_PER : 1];
+  f32x4 ra0[KD][A_PER];
+  float rb0[KD][B_PER];
+  float rg0[KD][GM ? B_PER : 1];
   // buffer descriptors over this image's source planes (wave-uniform inputs only)
   const int plane_i = P.Hs * P.Ws;
   const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane_i * 4u;
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   int ad_voff[ADIR ? TM : 1];
 #pragma unroll
   for (int i = 0; i < (ADIR ? TM : 1); ++i) ad_voff[i] = (((wm * TM + i) * 32 + lo) * AW + 4 * hi) * 4;
-  bf16x8_t arN[ADIR ? TM : 1][3], arC[ADIR ? TM : 1][3];
+  bf16x8_t arN[KD][ADIR ? TM : 1][3], arC[KD][ADIR ? TM : 1][3];
 
   // CFAST walk, tiles in k order: tap-major -- the (tap, channel) position advances by 16 channels
   // per tile and the gather offset is decoded once per tap (wave-uniform branch); channel-blocked
@@ -233,7 +239,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 
   // Issue every global load of tile t without branches (out-of-range taps read a clamped, valid
   // address and are zeroed at LDS-store time), so the loads stay in flight across the MFMAs.
-  auto load_tile = [&](int t, f32x4 (&ra)[A_PER], float (&rb)[B_PER], float (&rg)[GM ? B_PER : 1]) {
+  auto load_tile = [&](int t, f32x4 (&ra)[A_PER], float (&rb)[B_PER], float (&rg)[GM ? B_PER : 1],
+                       bf16x8_t (&arn)[ADIR ? TM : 1][3]) {
     const int k0 = t * BK;
     const int a_soff = __builtin_amdgcn_readfirstlane(((t * P.Mpad + m0) * AW) * 4);
     if constexpr (ADIR) {
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc)
-          arN[i][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff[i], a_soff + 32 * pc, 0));
+          arn[i][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff[i], a_soff + 32 * pc, 0));
     } else
 #pragma unroll
     for (int i = 0; i < A_PER; ++i)
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       }
     }
   };
-  auto store_tile = [&](int buf, const f32x4 (&ra)[A_PER], const float (&rb)[B_PER],
+  auto store_tile = [&](float (*Asb)[LS], float (*Bsb)[LS], const f32x4 (&ra)[A_PER], const float (&rb)[B_PER],
                         const float (&rg)[GM ? B_PER : 1]) {
 #pragma unroll
     for (int i = 0; i < (ADIR ? 0 : A_PER); ++i) {
@@ -307,12 +314,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       if (A_F4 % NT == 0 || idx < A_F4) {
         if (AWL == 8) {
           const int sl = a_slot2(idx);
-          *reinterpret_cast<f32x4*>(&As[buf][sl >> 1][(sl & 1) * 4]) = ra[i];
+          *reinterpret_cast<f32x4*>(&Asb[sl >> 1][(sl & 1) * 4]) = ra[i];
         } else if (AW == 16) {
           const int sl = a_slot(idx);
-          *reinterpret_cast<f32x4*>(&As[buf][sl >> 2][(sl & 3) * 4]) = ra[i];
+          *reinterpret_cast<f32x4*>(&Asb[sl >> 2][(sl & 3) * 4]) = ra[i];
         } else {
-          *reinterpret_cast<f32x4*>(&As[buf][idx / 6][(idx % 6) * 4]) = ra[i];
+          *reinterpret_cast<f32x4*>(&Asb[idx / 6][(idx % 6) * 4]) = ra[i];
         }
       }
     }
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
           split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
         }
       }
-      uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Bsb[bcol][0]);
       if constexpr (ROWSTEP == 4) {  // k = 4*brow0 .. 4*brow0+3: one b64 per piece
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
@@ -357,7 +364,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       uint32_t h[B_PER / 2], l[B_PER / 2];
 #pragma unroll
       for (int q = 0; q < B_PER / 2; ++q) split2<PREC>(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
-      uint32_t* d = reinterpret_cast<uint32_t*>(&Bs[buf][bcol][0]);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Bsb[bcol][0]);
       if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
         *reinterpret_cast<u32x4*>(d + 4 * brow0) = u32x4{h[0], h[1], h[2], h[3]};
         if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8 + 4 * brow0) = u32x4{l[0], l[1], l[2], l[3]};
@@ -370,11 +377,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
         }
       }
     } else if constexpr (ROWSTEP == 2) {  // rows k = brow0 + 2i: hi = brow0, s = i -> 8 contiguous floats
-      float* d = &Bs[buf][bcol][brow0 * 8];
+      float* d = &Bsb[bcol][brow0 * 8];
       *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[1], bv[2], bv[3]);
       *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[4], bv[5], bv[6], bv[7]);
     } else {             // ROWSTEP == 1: rows k = i
-      float* d = &Bs[buf][bcol][0];
+      float* d = &Bsb[bcol][0];
       *reinterpret_cast<f32x4*>(d) = mk4(bv[0], bv[2], bv[4], bv[6]);
       *reinterpret_cast<f32x4*>(d + 4) = mk4(bv[8], bv[10], bv[12], bv[14]);
       *reinterpret_cast<f32x4*>(d + 8) = mk4(bv[1], bv[3], bv[5], bv[7]);
@@ -382,25 +389,25 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     }
   };
 
-  auto compute_tile = [&](int buf) {
+  auto compute_tile = [&](int buf, int d) {
     if constexpr (ADIR) {
-      mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC, Bs[buf], wn * TN * 32, lane);
+      mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC[d], Bs[buf][d], wn * TN * 32, lane);
     } else if constexpr (PREC == 3) {
-      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf][d], Bs[buf][d], wm * TM * 32, wn * TN * 32, lane);
     } else if constexpr (PREC != 0) {
-      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf][d], Bs[buf][d], wm * TM * 32, wn * TN * 32, lane);
     } else {
       // each lane's 8 k-steps of every fragment: two ds_read_b128 per fragment, then the MFMA chain
       f32x4 a[TM][2], b[TN][2];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        const float* r = &As[buf][d][(wm * TM + i) * 32 + lo][hi * 8];
         a[i][0] = *reinterpret_cast<const f32x4*>(r);
         a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        const float* r = &Bs[buf][d][(wn * TN + j) * 32 + lo][hi * 8];
         b[j][0] = *reinterpret_cast<const f32x4*>(r);
         b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
       }
@@ -422,21 +429,40 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   auto rotate_a = [&]() {
     if constexpr (ADIR) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int d = 0; d < KD; ++d)
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) arC[i][pc] = arN[i][pc];
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int pc = 0; pc < 3; ++pc) arC[d][i][pc] = arN[d][i][pc];
     }
   };
-  load_tile(0, ra0, rb0, rg0);
-  store_tile(0, ra0, rb0, rg0);
+  // a stage = KD consecutive k-tiles (tile order is the walk order of load_tile); the tiles of a
+  // short last stage are neither loaded, stored nor computed (ntiles is block-uniform)
+  const int nst = (ntiles + KD - 1) / KD;
+  auto load_stage = [&](int s) {
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d == 0 || s * KD + d < ntiles) load_tile(s * KD + d, ra0[d], rb0[d], rg0[d], arN[d]);
+  };
+  auto store_stage = [&](int buf, int s) {
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d == 0 || s * KD + d < ntiles) store_tile(As[buf][d], Bs[buf][d], ra0[d], rb0[d], rg0[d]);
+  };
+  load_stage(0);
+  store_stage(0, 0);
   rotate_a();
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) load_tile(t + 1, ra0, rb0, rg0);
-    if (!(ABL & 32)) compute_tile(buf);
-    if (t + 1 < ntiles && !(ABL & 8)) store_tile(buf ^ 1, ra0, rb0, rg0);
-    if (t + 1 < ntiles) rotate_a();
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) load_stage(s + 1);
+    if (!(ABL & 32)) {
+#pragma unroll
+      for (int d = 0; d < KD; ++d)
+        if (d == 0 || s * KD + d < ntiles) compute_tile(buf, d);
+    }
+    if (s + 1 < nst && !(ABL & 8)) store_stage(buf ^ 1, s + 1);
+    if (s + 1 < nst) rotate_a();
     if (!(ABL & 16)) __syncthreads();
   }
 
@@ -579,9 +605,26 @@ inline int widen_cfg(int c, long HWo) {
 #define VST_MINW_A256 4
 #endif
 
-template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false>
+#ifndef VST_KD2
+#define VST_KD2 1
+#endif
+// two k-tiles per stage for the single-product modes on the 128- and 256-row tiles (VST_KD2=0 at
+// build or run time: one); the smaller tiles keep one (their two-tile stages exceed the register
+// budget of their occupancy target)
+inline bool kd2_on() {
+  static const bool on = VST_KD2 && (!getenv("VST_KD2") || atoi(getenv("VST_KD2")) != 0);
+  return on;
+}
+
+template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false, bool KD2OK = false>
 static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
-  conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR><<<grid, WM * WN * 64, 0, st>>>(P);
+  if constexpr (VST_KD2 && KD2OK && (PR == 2 || PR == 4)) {
+    if (kd2_on()) {
+      conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, 2><<<grid, WM * WN * 64, 0, st>>>(P);
+      return;
+    }
+  }
+  conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, 1><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 template <bool CF, bool GMK, int PR>
@@ -602,12 +645,12 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
     case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
     case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
     case T96W: launch_k<1, 3, 4, 2, CF, GMK, 2, PR>(grid, st, P); break;
-    case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR>(grid, st, P); break;
+    case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR, false, true>(grid, st, P); break;
     case T128A:  // four A-direct waves of 32 rows x 128 pixels
       if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 / fp16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
-      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR>(grid, st, P);
+      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR, false, true>(grid, st, P);
       break;
     default: launch_k<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR>(grid, st, P); break;
   }

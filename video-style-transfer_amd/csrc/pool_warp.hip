@@ -383,9 +383,78 @@ __global__ void resize_bwd_kernel(const float* __restrict__ gout, float* __restr
   gx[idx] = acc;
 }
 
+// Adjoint of the exact x2 bilinear upsample (align_corners=False, Ho = 2H, Wo = 2W), optionally
+// times the ReLU mask of its input (the producer ConvReLU's backward, y > 0: ATen's
+// threshold_backward on the ReLU result).  Along one axis input i is read by outputs 2i-1 .. 2i+2
+// with the fixed weights 0.25, 0.75 (1 at i = 0: src clamps to 0), 0.75 (1 at i = n-1: i0 = i1),
+// 0.25 -- the generic gather's per-candidate weight recomputation and +/-1 slack are gone.  Each
+// thread produces two adjacent input columns (j = 2t, 2t+1) from one aligned float4 and two
+// scalars per output row (W even; the launcher falls back to the generic gather otherwise).
+__device__ __forceinline__ void up2_axis_w(int i, int n, float (&w)[4]) {
+  w[0] = i >= 1 ? 0.25f : 0.f;
+  w[1] = i == 0 ? 1.f : 0.75f;
+  w[2] = i == n - 1 ? 1.f : 0.75f;
+  w[3] = i <= n - 2 ? 0.25f : 0.f;
+}
+
+__global__ void up2_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ ymask, float* __restrict__ gx,
+                               long NC, int C, int H, int W, long gout_bs) {
+  const int Wh = W >> 1;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NC * H * Wh) return;
+  const int t = (int)(idx % Wh);
+  const long r = idx / Wh;
+  const int iy = (int)(r % H);
+  const long nc = r / H;
+  const int Wo = 2 * W, Ho = 2 * H;
+  const float* g = gout + (nc / C) * gout_bs + (nc % C) * (long)Ho * Wo;
+  float wy[4], wa[4], wb[4];
+  up2_axis_w(iy, H, wy);
+  up2_axis_w(2 * t, W, wa);      // column j = 2t: outputs 4t-1 .. 4t+2
+  up2_axis_w(2 * t + 1, W, wb);  // column j = 2t+1: outputs 4t+1 .. 4t+4
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 4; ++dy) {
+    const int oy = 2 * iy - 1 + dy;
+    if (wy[dy] == 0.f) continue;  // out-of-range rows carry weight 0 (oy < 0 or oy >= Ho)
+    const float* row = g + (long)oy * Wo;
+    const f32x4 c = *reinterpret_cast<const f32x4*>(row + 4 * t);  // outputs 4t .. 4t+3
+    const float l = t > 0 ? row[4 * t - 1] : 0.f;
+    const float rr = 4 * t + 4 < Wo ? row[4 * t + 4] : 0.f;
+    const float s0 = wa[0] * l + wa[1] * c[0] + wa[2] * c[1] + wa[3] * c[2];
+    const float s1 = wb[0] * c[1] + wb[1] * c[2] + wb[2] * c[3] + wb[3] * rr;
+    a0 += wy[dy] * s0;
+    a1 += wy[dy] * s1;
+  }
+  const long o = (nc * H + iy) * (long)W + 2 * t;
+  if (ymask) {
+    const f32x2 m = *reinterpret_cast<const f32x2*>(ymask + o);
+    a0 = m[0] > 0.f ? a0 : 0.f;
+    a1 = m[1] > 0.f ? a1 : 0.f;
+  }
+  *reinterpret_cast<f32x2*>(gx + o) = f32x2{a0, a1};
+}
+
 }  // namespace
 
 extern "C" {
+
+int vst_upsample2x_bwd(const float* gout, const float* ymask, float* gx, long NC, int C, int H, int W, long gout_bs,
+                       void* stream) {
+  VST_CHECK_ARG(gout && gx && NC > 0 && C > 0 && H > 0 && W > 0 && NC % C == 0);
+  const long Ho = 2L * H, Wo = 2L * W;
+  if (gout_bs <= 0) gout_bs = (long)C * Ho * Wo;
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = (W % 2 == 0) && (gout_bs % 4 == 0) && (((uintptr_t)gout | (uintptr_t)gx | (uintptr_t)ymask) % 16 == 0);
+  if (!vec) {
+    if (ymask) return VST_EUNSUPPORTED;  // the generic gather has no mask epilogue
+    resize_bwd_kernel<<<ceil_div(NC * H * W, 256), 256, 0, st>>>(gout, gx, NC, C, H, W, (int)Ho, (int)Wo, gout_bs);
+    return vst_launch_status();
+  }
+  const long total = NC * H * (W / 2);
+  up2_bwd_kernel<<<ceil_div(total, 256), 256, 0, st>>>(gout, ymask, gx, NC, C, H, W, gout_bs);
+  return vst_launch_status();
+}
 
 int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream) {
   VST_CHECK_ARG(x && y && NC > 0 && H >= 2 && W >= 2);

@@ -75,10 +75,26 @@ def _vec(shape, like):
     return torch.empty(shape, device=like.device, dtype=torch.float32)
 
 
-def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None, role="attn"):
-    """out[n][m][p] = (sum_k x[n][k][m] b[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]."""
+_ONES = {}
+
+
+def _ones(n, like):
+    """A cached all-ones vector (the unit row / column scale of attn_gemm's affine epilogue)."""
+    key = (like.device, n)
+    v = _ONES.get(key)
+    if v is None:
+        v = torch.ones(n, device=like.device, dtype=torch.float32)
+        _ONES[key] = v
+    return v
+
+
+def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None, role="attn", transpose=False):
+    """out[n][m][p] = (sum_k Aop[n][k][m] b[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m] with
+    Aop as in bmm_at_b (x[n] = X[K][M], or X[M][K] when transpose); rb / cg None = 1."""
     N = b.shape[0]
-    ap, abs_ = packed_matrix(x, M, K, False, role)
+    rb = _ones(N * M, b) if rb is None else rb
+    cg = _ones(N * P, b) if cg is None else cg
+    ap, abs_ = packed_matrix(x, M, K, transpose, role)
     out = _empty((N, M, P), b)
     from .. import kprof
 
@@ -266,6 +282,13 @@ def _normalize_bwd(xh, dxh, nrm_inv):
     return out
 
 
+def _neg(x):
+    """-x (a small per-row vector) with the library's affine kernel: x + (-2) x, exact."""
+    out = _empty(x.shape, x)
+    lib.vst_outer_axpy(ptr(x), ptr(x), None, None, -2.0, ptr(out), 1, x.numel(), 1, stream())
+    return out
+
+
 def _recip(x):
     y = _empty(x.shape, x)
     lib.vst_reciprocal(ptr(x), ptr(y), x.numel(), stream())
@@ -300,8 +323,7 @@ class LinearCosineAttnFn(Function):
         rinv = _empty(qk.shape, qk)
         lib.vst_attn_fwd_rows(ptr(qk), ptr(qn), ptr(_empty(qk.shape, qk)), ptr(rinv), qk.numel(), Ns,
                               stream())                     # 1 / rs = 1 / (q . ksum / ||q|| + Ns)
-        MV = bmm_at_b(Gr, 2 * dv, d, False, Qh, Nc, role=role)  # G^T qh  [Nq][2dv][Nc]
-        _axpy(MV, u=usr, w=rinv)                            # (G^T qh + us) / rs
+        MV = attn_gemm(Gr, 2 * dv, d, Qh, Nc, rb=None, cg=rinv, ra=usr, role=role)  # (G^T qh + us) / rs
         out = _empty((Nq, dv, h, w), V)
         lib.vst_adaattn_out(ptr(MV), ptr(cn), ptr(out), Nq, dv * Nc, stream())
         ctx.dims = (Nq, Nk, d, dv, Nc, Ns, (h, w), (hs, ws))
@@ -317,10 +339,10 @@ class LinearCosineAttnFn(Function):
         role = "attn_" + COSINE
         if ctx.needs_input_grad[3]:
             raise VstError("adaattn: gradient w.r.t. the content features (norm_v(c_x)) is not on the reference path")
-        dMV = _empty(MV.shape, MV)
-        lib.vst_adaattn_out_bwd(ptr(dout.contiguous()), ptr(MV), ptr(cn), ptr(dMV), Nq, dv * Nc, stream())
-        te = _axpy(channel_dot(dMV, y=MV).view(Nq, 1, Nc), w=rinv, out=_empty((Nq, 1, Nc), MV)).view(Nq, Nc)
-        dRh = _axpy(dMV, w=rinv)                            # dMV / rs (in place)
+        dRh = _empty(MV.shape, MV)                          # dMV / rs, in the out-backward's pass
+        lib.vst_adaattn_out_bwd_scaled(ptr(dout.contiguous()), ptr(MV), ptr(cn), ptr(rinv), ptr(dRh), Nq, dv * Nc, Nc,
+                                       stream())
+        te = channel_dot(dRh, y=MV)                         # rs^-1 sum_v dMV MV
         dG = _sum_repeats(gemm_abt(Qh, dRh, role=role), r)  # [Nk][d][2dv]
         dQ = dK = dV = None
         if ctx.needs_input_grad[0]:
@@ -329,13 +351,11 @@ class LinearCosineAttnFn(Function):
             dQ = _normalize_bwd(Qh, dQh, qs).view(Nq, d, *hw)
         if ctx.needs_input_grad[1]:
             dks = _sum_repeats(plane_dot(Qh, te), r)       # -dksum
-            dKh = bmm_at_b(dG, d, 2 * dv, True, U, Ns, role=role)  # dG U  [Nk][d][Ns]
-            _axpy(dKh, u=dks, alpha=-1.0)
+            dKh = attn_gemm(dG, d, 2 * dv, U, Ns, rb=None, cg=None, ra=_neg(dks), role=role, transpose=True)  # dG U + dksum
             dK = _normalize_bwd(Kh, dKh, ks).view(Nk, d, *hws)
         if ctx.needs_input_grad[2]:
             dus = _sum_repeats(plane_dot(dRh), r)          # [Nk][2dv]
-            dU = bmm_at_b(dG, 2 * dv, d, False, Kh, Ns, role=role)  # dG^T Kh  [Nk][2dv][Ns]
-            _axpy(dU, u=dus)
+            dU = attn_gemm(dG, 2 * dv, d, Kh, Ns, rb=None, cg=None, ra=dus, role=role)  # dG^T Kh + dus
             dV = _empty(V.shape, V)
             lib.vst_square_concat_bwd(ptr(dU), ptr(V), ptr(dV), Nk, dv * Ns, stream())
         return dQ, dK, dV, None

@@ -103,19 +103,19 @@ class Decoder(nn.Module):
     def _forward(self, x5, x4, x3):
         # a ConvReLU whose output only feeds the next conv leaves its ReLU backward to that conv's
         # data gradient (premasked -> mask_dx: the mask is applied in the dgrad epilogue and border
-        # fold); the outputs that feed an upsample keep the separate ReLU-backward pass
+        # fold); one whose output feeds an upsample leaves it to the upsample's adjoint (relu_mask)
         def run(m, x, mask_dx=False, premasked=False):
             return m.run(x, act="relu" if isinstance(m, ConvReLU) else None, mask_dx=mask_dx, premasked=premasked)
 
         x = ops.upsample2x(x5, addend=x4)
         x = run(self.conv1, x, premasked=True)
-        x = ops.upsample_cat(run(self.conv2, x, mask_dx=True), x3)
+        x = ops.upsample_cat(run(self.conv2, x, mask_dx=True, premasked=True), x3, relu_mask=True)
         x = run(self.conv3[0], x, premasked=True)
         x = run(self.conv3[1], x, mask_dx=True, premasked=True)
         x = run(self.conv3[2], x, mask_dx=True, premasked=True)
-        x = ops.upsample2x(run(self.conv4, x, mask_dx=True))
+        x = ops.upsample2x(run(self.conv4, x, mask_dx=True, premasked=True), relu_mask=True)
         x = run(self.conv5, x, premasked=True)
-        x = ops.upsample2x(run(self.conv6, x, mask_dx=True))
+        x = ops.upsample2x(run(self.conv6, x, mask_dx=True, premasked=True), relu_mask=True)
         x = run(self.conv7, x, premasked=True)
         return run(self.conv8, x, mask_dx=True)
 

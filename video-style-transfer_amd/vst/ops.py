@@ -1000,6 +1000,26 @@ def resize_bilinear_bwd(gout, x_shape):
     return gx
 
 
+def upsample2x_bwd(gout, x, relu_mask=False):
+    """Adjoint of the x2 upsample w.r.t. its input x (fixed-stencil kernel), times (x > 0) when x is
+    a ReLU output whose backward is fused here (relu_mask)."""
+    N, C, H, W = x.shape
+    gptr, gbs = ptr_rows(gout)
+    if relu_mask and (W % 2 or (gptr | x.data_ptr()) % 16):  # the stencil kernel's float4 / float2 access
+        return relu_bwd(upsample2x_bwd(gout, x), x)
+    gx = _empty(x.shape, gout)
+    lib.vst_upsample2x_bwd(gptr, ptr(x) if relu_mask else None, ptr(gx), N * C, C, H, W,
+                           gbs if gbs != C * 4 * H * W else 0, stream())
+    return gx
+
+
+def relu_bwd(gy, y):
+    """gy * (y > 0) (ATen threshold_backward on a ReLU result)."""
+    gz = _empty(gy.shape, gy)
+    lib.vst_relu_bwd(ptr(gy), ptr(y), ptr(gz), gy.numel(), stream())
+    return gz
+
+
 def copy_into(src, dst):
     """dst[n] = src[n] for per-sample-contiguous src/dst (slices of concat buffers)."""
     if tuple(src.shape) != tuple(dst.shape):
@@ -1012,32 +1032,35 @@ def copy_into(src, dst):
 
 class Upsample2xFn(Function):
     """F.interpolate(x, scale_factor=2, mode='bilinear', align_corners=False) [+ addend]
-    (AA/network.py:59, 80; the decoder's `self.upsample(x5) + x4`)."""
+    (AA/network.py:59, 80; the decoder's `self.upsample(x5) + x4`).  relu_mask: x is the output of
+    a ConvReLU whose ReLU backward this op applies (the producer then runs with premasked=True)."""
 
     @staticmethod
-    def forward(ctx, x, addend):
+    def forward(ctx, x, addend, relu_mask):
         x = _check(x, "upsample input", 4)
         N, C, H, W = x.shape
-        ctx.shape = x.shape
         ctx.has_add = addend is not None
+        ctx.relu_mask = bool(relu_mask)
+        ctx.save_for_backward(x)
         return resize_bilinear(x, (2 * H, 2 * W), addend=addend)
 
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous()
-        gx = resize_bilinear_bwd(g, ctx.shape) if ctx.needs_input_grad[0] else None
-        return gx, (g if ctx.has_add and ctx.needs_input_grad[1] else None)
+        x, = ctx.saved_tensors
+        gx = upsample2x_bwd(g, x, ctx.relu_mask) if ctx.needs_input_grad[0] else None
+        return gx, (g if ctx.has_add and ctx.needs_input_grad[1] else None), None
 
 
-def upsample2x(x, addend=None):
-    return Upsample2xFn.apply(x, addend)
+def upsample2x(x, addend=None, relu_mask=False):
+    return Upsample2xFn.apply(x, addend, relu_mask)
 
 
 class UpsampleCatFn(Function):
     """torch.cat([upsample2x(x), y], dim=1) written straight into one buffer (AA/network.py:85-87)."""
 
     @staticmethod
-    def forward(ctx, x, y):
+    def forward(ctx, x, y, relu_mask):
         x = _check(x, "upsample-cat x", 4)
         y = _check(y, "upsample-cat y", 4)
         N, C1, H, W = x.shape
@@ -1047,23 +1070,27 @@ class UpsampleCatFn(Function):
         out = _empty((N, C1 + C2, 2 * H, 2 * W), x)
         resize_bilinear(x, (2 * H, 2 * W), out=out[:, :C1])
         copy_into(y, out[:, C1:])
-        ctx.dims = (x.shape, C1)
+        ctx.C1 = C1
+        ctx.relu_mask = bool(relu_mask)
+        ctx.save_for_backward(x)
         return out
 
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous()
-        xs, C1 = ctx.dims
-        gx = resize_bilinear_bwd(g[:, :C1], xs) if ctx.needs_input_grad[0] else None
+        x, = ctx.saved_tensors
+        C1 = ctx.C1
+        gx = upsample2x_bwd(g[:, :C1], x, ctx.relu_mask) if ctx.needs_input_grad[0] else None
         gy = None
         if ctx.needs_input_grad[1]:
             gs = g[:, C1:]
             gy = copy_into(gs, _empty(gs.shape, g))
-        return gx, gy
+        return gx, gy, None
 
 
-def upsample_cat(x, y):
-    return UpsampleCatFn.apply(x, y)
+def upsample_cat(x, y, relu_mask=False):
+    """cat([upsample2x(x), y]); relu_mask as in upsample2x."""
+    return UpsampleCatFn.apply(x, y, relu_mask)
 
 
 def flow_warp_mask(flo01, flo10, threshold=2.0):
