@@ -338,6 +338,16 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
       if ((cfg == T64W || cfg == T64) && (ad64 == 1 || (ad64 == 2 && dg))) cfg = T64A;
       if (cfg == T192 && (ad192 == 1 || (ad192 == 2 && dg))) cfg = T192A;
     }
+    // single-product modes (bf16, fp16): A-direct blocks with two k-tiles per stage -- the LDS-A
+    // tiles stage 256 weight rows x 32 B per k-tile through LDS for 8 MFMAs per wave, which puts
+    // their LDS store traffic past the array's write rate (VST_ADS=0: the LDS-A tiles)
+    static const int ads = env_mode("VST_ADS", 1);
+    if (VST_ADIR && VST_ADIR_SP && ads && (am == VST_GEMM_BF16 || am == VST_GEMM_F16)) {
+      if (cfg == T256) cfg = T256A;
+      if (cfg == T128) cfg = M % 256 == 0 ? T256A : T128A;
+      if (cfg == T64W || cfg == T64) cfg = T64A;
+      if (cfg == T192) cfg = T192A;
+    }
   }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);
   P.Mpad = (M + bm - 1) / bm * bm;

@@ -59,8 +59,11 @@ struct ConvParams {
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2, GM_CLAMP = 3 };
 enum { EPI_BIAS = 1, EPI_RELU = 2, EPI_TANH = 4, EPI_MASK = 8, EPI_ACCUM = 16, EPI_AFFINE = 32, EPI_PHASE2 = 64, EPI_PADOUT = 128 };
 
-// source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero
-// (select-only arithmetic: no divergent branches inside the k loop)
+// source offset (within one channel plane) of tap (kh,kw) for output pixel (oy,ox); -1 if zero.
+// Straight-line code: the three border rules of the forward gathers are all evaluated and the
+// block-uniform gmode picks one through bit masks (an if / else-if chain on gmode compiled into a
+// ~60-instruction branch ladder executed per k-tile, since the channel-blocked K walk changes the
+// tap every tile).
 __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox, int kh, int kw) {
   if (P.gmode == GM_TRANSPOSED) {
     int ty = oy + P.pad - kh, tx = ox + P.pad_x - kw;
@@ -74,21 +77,17 @@ __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox
     return ok ? ty * P.Ws + tx : -1;
   }
   const int Hv = P.Hs * P.up, Wv = P.Ws * P.up;
-  int y = oy * P.stride + kh - P.pad, x = ox * P.stride + kw - P.pad_x;
-  bool ok = true;
-  if (P.gmode == GM_REFLECT) {
-    y = abs(y);
-    y = y >= Hv ? 2 * Hv - 2 - y : y;
-    x = abs(x);
-    x = x >= Wv ? 2 * Wv - 2 - x : x;
-  } else if (P.gmode == GM_CLAMP) {  // edge clamp (phase-stacked nearest-x2 forward, vst_conv_up2_fwd)
-    y = min(max(y, 0), Hv - 1);
-    x = min(max(x, 0), Wv - 1);
-  } else {
-    ok = y >= 0 && y < Hv && x >= 0 && x < Wv;
-  }
+  const int y0 = oy * P.stride + kh - P.pad, x0 = ox * P.stride + kw - P.pad_x;
+  int yr = abs(y0), xr = abs(x0);  // reflect
+  yr = yr >= Hv ? 2 * Hv - 2 - yr : yr;
+  xr = xr >= Wv ? 2 * Wv - 2 - xr : xr;
+  const int yc = min(max(y0, 0), Hv - 1), xc = min(max(x0, 0), Wv - 1);  // edge clamp
+  const int mr = -(int)(P.gmode == GM_REFLECT), mc = -(int)(P.gmode == GM_CLAMP), mz = ~(mr | mc);
+  const int y = (yr & mr) | (yc & mc) | (y0 & mz), x = (xr & mr) | (xc & mc) | (x0 & mz);
+  const bool inb = (unsigned)y0 < (unsigned)Hv && (unsigned)x0 < (unsigned)Wv;
   const int sh = P.up - 1;
-  return ok ? (y >> sh) * P.Ws + (x >> sh) : -1;
+  const int off = (y >> sh) * P.Ws + (x >> sh);
+  return (inb || mz == 0) ? off : -1;
 }
 
 // float4 slot (row*4 + quad) of A-tile element idx: 8 consecutive lanes take 8 consecutive rows of
@@ -122,7 +121,7 @@ __device__ __forceinline__ int a_slot2(int idx) {
 // 16-deep tile rather than by the MFMAs; KD 2 halves both per MFMA.
 template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false, int KD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParams P) {
-  static_assert(!ADIR || PREC == 3, "A-direct: bf16x6");
+  static_assert(!ADIR || PREC >= 2, "A-direct: bf16x6, bf16, fp16");
   static_assert(ADIR || WM * WN == 4, "LDS-A path: 4 waves");
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -244,10 +243,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     const int k0 = t * BK;
     const int a_soff = __builtin_amdgcn_readfirstlane(((t * P.Mpad + m0) * AW) * 4);
     if constexpr (ADIR) {
+      // bf16x6: the hi / mid / lo pieces (32 B apart); bf16 / fp16: the hi piece only
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc)
+        for (int pc = 0; pc < (PREC == 3 ? 3 : 1); ++pc)
           arn[i][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff[i], a_soff + 32 * pc, 0));
     } else
 #pragma unroll
@@ -365,7 +365,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 #pragma unroll
       for (int q = 0; q < B_PER / 2; ++q) split2<PREC>(bv[2 * q], bv[2 * q + 1], h[q], l[q]);
       uint32_t* d = reinterpret_cast<uint32_t*>(&Bsb[bcol][0]);
-      if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
+      if constexpr (ROWSTEP == 4) {  // k = 4*brow0 .. 4*brow0+3 (8-wave blocks): one b64 per piece
+        *reinterpret_cast<u32x2*>(d + 2 * brow0) = u32x2{h[0], h[1]};
+        if (PREC == 1) *reinterpret_cast<u32x2*>(d + 8 + 2 * brow0) = u32x2{l[0], l[1]};
+      } else if constexpr (ROWSTEP == 2) {  // k = 8*brow0 .. 8*brow0+7
         *reinterpret_cast<u32x4*>(d + 4 * brow0) = u32x4{h[0], h[1], h[2], h[3]};
         if (PREC == 1) *reinterpret_cast<u32x4*>(d + 8 + 4 * brow0) = u32x4{l[0], l[1], l[2], l[3]};
       } else {                       // k = 0..15
@@ -390,8 +393,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   };
 
   auto compute_tile = [&](int buf, int d) {
-    if constexpr (ADIR) {
+    if constexpr (ADIR && PREC == 3) {
       mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC[d], Bs[buf][d], wn * TN * 32, lane);
+    } else if constexpr (ADIR) {
+      mfma_single_ktile_ra<TM, TN, PREC, LS>(acc, arC[d], Bs[buf][d], wn * TN * 32, lane);
     } else if constexpr (PREC == 3) {
       mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf][d], Bs[buf][d], wm * TM * 32, wn * TN * 32, lane);
     } else if constexpr (PREC != 0) {
@@ -433,7 +438,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int pc = 0; pc < 3; ++pc) arC[d][i][pc] = arN[d][i][pc];
+          for (int pc = 0; pc < (PREC == 3 ? 3 : 1); ++pc) arC[d][i][pc] = arN[d][i][pc];
     }
   };
   // a stage = KD consecutive k-tiles (tile order is the walk order of load_tile); the tiles of a
@@ -598,6 +603,10 @@ inline int widen_cfg(int c, long HWo) {
 #ifndef VST_ADIR
 #define VST_ADIR 1
 #endif
+// bf16 / fp16 A-direct tiles (VST_ADIR_SP=0: the LDS-A tiles for those modes)
+#ifndef VST_ADIR_SP
+#define VST_ADIR_SP 1
+#endif
 #ifndef VST_MINW_ADIR
 #define VST_MINW_ADIR 3
 #endif
@@ -629,25 +638,25 @@ static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
 
 template <bool CF, bool GMK, int PR>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
-  constexpr bool AD = PR == 3 && VST_ADIR;
+  constexpr bool AD = (PR == 3 || ((PR == 2 || PR == 4) && VST_ADIR_SP)) && VST_ADIR;
   switch (cfg) {
     case T32: launch_k<1, 1, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
     case T64: launch_k<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
     case T64A:
-      if constexpr (AD) launch_k<2, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
+      if constexpr (AD) launch_k<2, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true, true>(grid, st, P);
       break;
     case T192A:
-      if constexpr (AD) launch_k<6, 1, 1, 4, CF, GMK, 3, PR, true>(grid, st, P);
+      if constexpr (AD) launch_k<6, 1, 1, 4, CF, GMK, 3, PR, true, true>(grid, st, P);
       break;
     case T256A:  // all eight waves gather the B tile (4 elements each)
-      if constexpr (AD) launch_k<8, 1, 1, 4, CF, GMK, VST_MINW_A256, PR, true>(grid, st, P);
+      if constexpr (AD) launch_k<8, 1, 1, 4, CF, GMK, VST_MINW_A256, PR, true, true>(grid, st, P);
       break;
     case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
     case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
     case T96W: launch_k<1, 3, 4, 2, CF, GMK, 2, PR>(grid, st, P); break;
     case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR, false, true>(grid, st, P); break;
     case T128A:  // four A-direct waves of 32 rows x 128 pixels
-      if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true>(grid, st, P);
+      if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true, true>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 / fp16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
       if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR, false, true>(grid, st, P);

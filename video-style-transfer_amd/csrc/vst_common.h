@@ -308,6 +308,27 @@ __device__ __forceinline__ void mfma_bf16x6_ktile_ra(f32x16 (&acc)[TM][TN], cons
     }
 }
 
+// single-product (bf16 hi*hi, or fp16) k-tile with the A fragments in registers (loaded straight
+// from the packed weights: the hi piece of each 32-row fragment) and B from LDS
+template <int TM, int TN, int PREC, int LS>
+__device__ __forceinline__ void mfma_single_ktile_ra(f32x16 (&acc)[TM][TN], const bf16x8_t (&ar)[TM][3],
+                                                     float (*B)[LS], int b0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8_t bh[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bh[j] = *reinterpret_cast<const bf16x8_t*>(&B[b0 + j * 32 + r][4 * h]);
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (PREC == 4)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, ar[i][0]),
+                                                           __builtin_bit_cast(f16x8_t, bh[j]), acc[i][j], 0, 0, 0);
+      else
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[i][0], bh[j], acc[i][j], 0, 0, 0);
+    }
+}
+
 // A wave-uniform pointer forced into SGPRs: a buffer descriptor built from a pointer the compiler
 // keeps in VGPRs (e.g. after a 64-bit VALU multiply) makes every buffer load a waterfall loop.
 __device__ __forceinline__ void* uniform_ptr(const void* p) {

@@ -378,12 +378,15 @@ struct Wg2Params {
   int asplit, Ha;  // row-split A (vst_conv_wgrad_rowsplit): m = co*asplit + kh reads a[co][oy-kh][ox], a has Ha rows
 };
 
-template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE>
+// KD: k-tiles per LDS stage (one barrier per KD tiles); two for the single-product modes, whose
+// k loop does 4-6 MFMAs per wave and tile and is otherwise paced by the per-tile barrier
+template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int LS = PREC == 3 ? 28 : 20;
+  // LDS row: the staged k-tile + 4 pad dwords (bf16 / fp16 stage only their 8-dword hi half)
+  constexpr int LS = (PREC == 2 || PREC == 4) ? 12 : (PREC == 3 ? 28 : 20);
   // A task = AQ consecutive pixels of one dY row.  8 (two float4) unless 2*BM tasks would leave
   // some waves with one task more than others (the 192-row tile: 384 tasks on 256 threads): then 4,
   // so every thread splits the same number of elements (3 x 4 A + 8 B) and no wave waits at the
@@ -395,8 +398,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   constexpr int OOR = 0x7ffffff0;
   static_assert(BK == 16, "16-pixel k-tiles");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LS];
+  __shared__ __attribute__((aligned(16))) float As[2][KD][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][KD][BN][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -465,8 +468,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x4 RA[1][A_IT][2];  // the prefetched tile's registers
-  float RB[1][B_IT][8];
+  f32x4 RA[KD][A_IT][2];  // the prefetched stage's registers
+  float RB[KD][B_IT][8];
   // tile position (scalar): output row oy, first column ox0
   int t_oy = __builtin_amdgcn_readfirstlane(r_begin / P.Wo);
   int t_ox = __builtin_amdgcn_readfirstlane(r_begin - t_oy * P.Wo);
@@ -612,16 +615,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       if (AQ == 4) {
-        if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) store4(&As[buf][a_row[i]][0], a_half[i], ra[i][0]);
+        if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) store4(&As[buf][s][a_row[i]][0], a_half[i], ra[i][0]);
       } else if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) {
         const float v[8] = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
                             ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
-        store8(&As[buf][a_row[i]][0], a_half[i], v, true);
+        store8(&As[buf][s][a_row[i]][0], a_half[i], v, true);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i)
-      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][b_col[i]][0], b_half[i], rb[i], false);
+      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][s][b_col[i]][0], b_half[i], rb[i], false);
   };
   auto advance = [&]() {
     t_ox += BK;
@@ -632,22 +635,22 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   };
 
   const int lo = lane & 31, hi = lane >> 5;
-  auto mfma_tile = [&](int buf) {
+  auto mfma_tile = [&](int buf, int d) {
     if constexpr (PREC == 3) {
-      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+      mfma_bf16x6_ktile<TM, TN, LS>(acc, As[buf][d], Bs[buf][d], wm * TM * 32, wn * TN * 32, lane);
     } else if constexpr (PREC != 0) {
-      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf], Bs[buf], wm * TM * 32, wn * TN * 32, lane);
+      mfma_bf16_ktile<TM, TN, PREC, LS>(acc, As[buf][d], Bs[buf][d], wm * TM * 32, wn * TN * 32, lane);
     } else {
       f32x4 a[TM][2], b[TN][2];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float* r = &As[buf][(wm * TM + i) * 32 + lo][hi * 8];
+        const float* r = &As[buf][d][(wm * TM + i) * 32 + lo][hi * 8];
         a[i][0] = *reinterpret_cast<const f32x4*>(r);
         a[i][1] = *reinterpret_cast<const f32x4*>(r + 4);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const float* r = &Bs[buf][(wn * TN + j) * 32 + lo][hi * 8];
+        const float* r = &Bs[buf][d][(wn * TN + j) * 32 + lo][hi * 8];
         b[j][0] = *reinterpret_cast<const f32x4*>(r);
         b[j][1] = *reinterpret_cast<const f32x4*>(r + 4);
       }
@@ -662,20 +665,39 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     }
   };
 
+  // a stage = KD consecutive k-tiles in walk order; the tiles of a short last stage are neither
+  // loaded, stored nor computed (ntiles is block-uniform)
+  const int nst = (ntiles + KD - 1) / KD;
   if (ntiles > 0) {
-    load_tile(0, 0);
-    advance();
-    store_tile(0, 0);
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d < ntiles) {
+        load_tile(d, d);
+        advance();
+      }
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d < ntiles) store_tile(0, d);
   }
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) {
-      load_tile(0, t + 1);
-      advance();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) {
+#pragma unroll
+      for (int d = 0; d < KD; ++d)
+        if (d == 0 || (st + 1) * KD + d < ntiles) {
+          load_tile(d, (st + 1) * KD + d);
+          advance();
+        }
     }
-    mfma_tile(buf);
-    if (t + 1 < ntiles) store_tile(buf ^ 1, 0);
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d == 0 || st * KD + d < ntiles) mfma_tile(buf, d);
+    if (st + 1 < nst) {
+#pragma unroll
+      for (int d = 0; d < KD; ++d)
+        if (d == 0 || (st + 1) * KD + d < ntiles) store_tile(buf ^ 1, d);
+    }
     __syncthreads();
   }
 
@@ -812,17 +834,30 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
   return best;
 }
 
+template <int PR, int GMD, int KD>
+static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
+  switch (c) {
+    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+  }
+}
+
+// two k-tiles per stage for the single-product modes (VST_WKD2=0 at run time: one)
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
-  switch (c) {
-    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
-    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD><<<g, NT, 0, st>>>(P); break;
+  static const bool kd2 = !getenv("VST_WKD2") || atoi(getenv("VST_WKD2")) != 0;
+  if constexpr (PR == 2 || PR == 4) {
+    if (kd2) {
+      launch_wg2_pk<PR, GMD, 2>(c, g, st, P);
+      return;
+    }
   }
+  launch_wg2_pk<PR, GMD, 1>(c, g, st, P);
 }
 
 template <int GMD>

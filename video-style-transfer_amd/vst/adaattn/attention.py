@@ -44,14 +44,27 @@ def packed_matrix(x, M, K, transpose, role="attn"):
     return ap, per
 
 
-def bmm_at_b(x, M, K, transpose, b, P, out=None, role="attn"):
+def bmm_at_b(x, M, K, transpose, b, P, out=None, role="attn", accumulate=False):
     """out[n] = Aop[n]^T-as-packed @ b[n]:  out[n][m][p] = sum_k Aop[n][k][m] b[n][k][p], where
-    Aop[n][k][m] = x[n][k][m] (transpose=False) or x[n][m][k] (transpose=True)."""
+    Aop[n][k][m] = x[n][k][m] (transpose=False) or x[n][m][k] (transpose=True); accumulate: out +=."""
     N = b.shape[0]
     ap, abs_ = packed_matrix(x, M, K, transpose, role)
     o = ops.conv_gemm(b.view(N, K, 1, P), ap, M, 1, 1, P, ops.GM_ZERO, 1, 0, 1, a_batch_stride=abs_,
-                      out=None if out is None else out.view(N, M, 1, P))
+                      out=None if out is None else out.view(N, M, 1, P), epi=ops.EPI_ACCUM if accumulate else 0)
     return o.view(N, M, P)
+
+
+def copy_cols(src, c0, C, dst=None, d0=0):
+    """Column block [.., c0:c0+C] of src [N][R][P] into dst [N][R][Pd] at column d0 (a new dense
+    [N][R][C] when dst is None): N*R rows of C floats through the plane-copy kernel."""
+    N, R, P = src.shape
+    if dst is None:
+        dst = _empty((N, R, C), src)
+    Pd = dst.shape[2]
+    if not (src.is_contiguous() and dst.is_contiguous() and dst.shape[:2] == (N, R) and c0 + C <= P and d0 + C <= Pd):
+        raise VstError("copy_cols: shapes")
+    lib.vst_copy_planes(ptr(src) + 4 * c0, P, ptr(dst) + 4 * d0, Pd, N * R, C, stream())
+    return dst
 
 
 def gemm_abt(a, b, scale=1.0, role="attn"):
@@ -139,12 +152,32 @@ def attention_rows(S, activation, qn=None, kn=None):
     raise ValueError(f"Unknown activation function: {activation}")
 
 
+# Softmax attention (the image trainer's activation, AA/network.py:102-108, 191-220) has no linear
+# form: A = softmax_rows(Q^T K) must be formed.  It is formed in blocks of query rows (columns of
+# Q): each block's S / A ([N][rows][Ns]) is computed, used and dropped, so HBM holds
+# O(rows * Ns) per image instead of O(Nc * Ns) (config-5 size, relu3_1: 4 GB -> <= the block budget
+# per image).  A row's softmax sees its whole key row, so every element is computed exactly as in
+# the full-matrix form; the backward recomputes a block's S and A instead of storing them
+# (flash-attention's trade: one extra Q^T K GEMM), and accumulates dK and dV over the blocks.
+SOFTMAX_BLOCK_BYTES = 256 << 20  # S (or A, dS) bytes per block over the whole batch
+
+
+def _softmax_rows_per_block(N, Nc, Ns, budget=None):
+    budget = SOFTMAX_BLOCK_BYTES if budget is None else budget
+    rows = max(1, budget // (4 * N * Ns))
+    if rows >= Nc:
+        return Nc
+    return max(32, rows // 32 * 32)
+
+
 class AdaAttnFn(Function):
     """out = sqrt(clamp(A V^2 - (A V)^2, 1e-6)) * cn + A V  with A = activation(Q^T K)
-    (AA/network.py:191-220 after the 1x1 convs; cn = norm_v(c_x)).  Gradients for Q, K, V."""
+    (AA/network.py:191-220 after the 1x1 convs).  Gradients for Q, K, V.  Softmax: query-row blocks
+    (see above); cosine with a materialised A (kept for tests; the product path uses
+    LinearCosineAttnFn)."""
 
     @staticmethod
-    def forward(ctx, Q, K, V, cn, activation):
+    def forward(ctx, Q, K, V, cn, activation, block_rows=None):
         N, d, h, w = Q.shape
         _, _, hs, ws = K.shape
         dv = V.shape[1]
@@ -155,6 +188,8 @@ class AdaAttnFn(Function):
         Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
         role = "attn_" + activation
         qn = kn = S = rowsum = None
+        VV2 = _empty((N, 2 * dv, Ns), V)
+        lib.vst_square_concat(ptr(V), ptr(VV2), N, dv * Ns, stream())
         if activation == COSINE:
             qn, kn = channel_norm(Qm), channel_norm(Km)
             ks = _vec((N, Ns), Q)
@@ -164,66 +199,111 @@ class AdaAttnFn(Function):
             lib.vst_attn_fwd_rows(ptr(qkbar), ptr(qn), ptr(c), ptr(e), N * Nc, Ns, stream())
             A = attn_gemm(Qm, Nc, d, Km, Ns, rb=c, cg=ks, rd=e, role=role)  # [N][Nc][Ns], S never stored
             rowsum = (ks, c, e)
+            MV = gemm_abt(VV2, A, role=role)  # [N][2dv][Nc]
+            C = Nc
+        elif activation == SOFTMAX:
+            C = _softmax_rows_per_block(N, Nc, Ns) if block_rows is None else min(int(block_rows), Nc)
+            A = None
+            if C == Nc:
+                S = bmm_at_b(Qm, Nc, d, False, Km, Ns, role=role)  # [N][Nc][Ns]
+                A, _ = attention_rows(S, activation)
+                del S
+                MV = gemm_abt(VV2, A, role=role)
+            else:
+                MV = _empty((N, 2 * dv, Nc), V)
+                for c0 in range(0, Nc, C):
+                    Cb = min(C, Nc - c0)
+                    Ab = _softmax_block(Qm, Km, c0, Cb, role)
+                    copy_cols(gemm_abt(VV2, Ab, role=role), 0, Cb, dst=MV, d0=c0)
         else:
-            S = bmm_at_b(Qm, Nc, d, False, Km, Ns, role=role)  # [N][Nc][Ns]
-            A, _ = attention_rows(S, activation)
-        VV2 = _empty((N, 2 * dv, Ns), V)
-        lib.vst_square_concat(ptr(V), ptr(VV2), N, dv * Ns, stream())
-        MV = gemm_abt(VV2, A, role=role)  # [N][2dv][Nc]
+            raise ValueError(f"Unknown activation function: {activation}")
         out = _empty((N, dv, h, w), V)
         lib.vst_adaattn_out(ptr(MV), ptr(cn), ptr(out), N, dv * Nc, stream())
         ctx.activation = activation
-        ctx.dims = (N, d, dv, Nc, Ns)
+        ctx.dims = (N, d, dv, Nc, Ns, C)
         if any(ctx.needs_input_grad[:3]):
             extra = rowsum if rowsum is not None else (None, None, None)
-            ctx.save_for_backward(Q, K, V, cn, qn, kn, S, A, VV2, MV, *extra)
+            ctx.save_for_backward(Q, K, V, cn, qn, kn, A, VV2, MV, *extra)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        Q, K, V, cn, qn, kn, S, A, VV2, MV, ks, c, e = ctx.saved_tensors
-        N, d, dv, Nc, Ns = ctx.dims
+        Q, K, V, cn, qn, kn, A, VV2, MV, ks, c, e = ctx.saved_tensors
+        N, d, dv, Nc, Ns, C = ctx.dims
         role = "attn_" + ctx.activation
+        if ctx.needs_input_grad[3]:
+            raise VstError("adaattn: gradient w.r.t. the content features (norm_v(c_x)) is not on the reference path")
         dout = dout.contiguous()
         dMV = _empty(MV.shape, MV)
         lib.vst_adaattn_out_bwd(ptr(dout), ptr(MV), ptr(cn), ptr(dMV), N, dv * Nc, stream())
+        Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
+        gq, gk, gv = ctx.needs_input_grad[:3]
+        if ctx.activation == SOFTMAX:
+            dQm = _empty((N, d, Nc), Q) if gq else None
+            dKm = _empty((N, d, Ns), K) if gk else None
+            dVV2 = _empty((N, 2 * dv, Ns), V) if gv else None
+            for c0 in range(0, Nc, C):
+                Cb = min(C, Nc - c0)
+                full = Cb == Nc
+                Ab = A if full and A is not None else _softmax_block(Qm, Km, c0, Cb, role)  # recomputed
+                dMVb = dMV if full else copy_cols(dMV, c0, Cb)
+                Qb = Qm if full else copy_cols(Qm, c0, Cb)
+                if gv:
+                    bmm_at_b(dMVb, 2 * dv, Cb, True, Ab, Ns, out=dVV2, role=role, accumulate=c0 > 0)
+                if gq or gk:
+                    dS = bmm_at_b(dMVb, Cb, 2 * dv, False, VV2, Ns, role=role)  # dA  [N][Cb][Ns]
+                    lib.vst_softmax_rows_bwd(ptr(dS), ptr(Ab), ptr(dS), N * Cb, Ns, stream())
+                    if gq:
+                        dQb = gemm_abt(Km, dS, role=role)  # [N][d][Cb]
+                        if full:
+                            dQm = dQb
+                        else:
+                            copy_cols(dQb, 0, Cb, dst=dQm, d0=c0)
+                    if gk:
+                        bmm_at_b(Qb, d, Cb, True, dS, Ns, out=dKm, role=role, accumulate=c0 > 0)  # [N][d][Ns]
+            dV = None
+            if gv:
+                dV = _empty(V.shape, V)
+                lib.vst_square_concat_bwd(ptr(dVV2), ptr(V), ptr(dV), N, dv * Ns, stream())
+            return (dQm.view(Q.shape) if gq else None, dKm.view(K.shape) if gk else None, dV, None, None, None)
         dQ = dK = dV = None
-        if ctx.needs_input_grad[2]:
+        if gv:
             dVV2 = bmm_at_b(dMV, 2 * dv, Nc, True, A, Ns, role=role)  # [N][2dv][Ns]
             dV = _empty(V.shape, V)
             lib.vst_square_concat_bwd(ptr(dVV2), ptr(V), ptr(dV), N, dv * Ns, stream())
             del dVV2
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            Qm, Km = Q.view(N, d, Nc), K.view(N, d, Ns)
-            if ctx.activation == COSINE:
-                r = channel_dot(dMV, y=MV)                 # sum_j dA_ij A_ij
-                DA = channel_dot(dMV, v=plane_dot(VV2))    # sum_j dA_ij
-                dqn, nr, cr = _vec((N, Nc), Q), _vec((N, Nc), Q), _vec((N, Nc), Q)
-                lib.vst_attn_bwd_rows(ptr(r), ptr(DA), ptr(qn), ptr(c), ptr(e), ptr(dqn), ptr(nr), ptr(cr), N * Nc, Ns,
-                                      stream())
-                dS = attn_gemm(dMV, Nc, 2 * dv, VV2, Ns, rb=c, cg=ks, ra=nr, role=role)  # (dA - r) c ks
-            else:
-                dS = bmm_at_b(dMV, Nc, 2 * dv, False, VV2, Ns, role=role)  # dA
-                lib.vst_softmax_rows_bwd(ptr(dS), ptr(A), ptr(dS), N * Nc, Ns, stream())
-            if ctx.needs_input_grad[0]:
+        if gq or gk:
+            r = channel_dot(dMV, y=MV)                 # sum_j dA_ij A_ij
+            DA = channel_dot(dMV, v=plane_dot(VV2))    # sum_j dA_ij
+            dqn, nr, cr = _vec((N, Nc), Q), _vec((N, Nc), Q), _vec((N, Nc), Q)
+            lib.vst_attn_bwd_rows(ptr(r), ptr(DA), ptr(qn), ptr(c), ptr(e), ptr(dqn), ptr(nr), ptr(cr), N * Nc, Ns,
+                                  stream())
+            dS = attn_gemm(dMV, Nc, 2 * dv, VV2, Ns, rb=c, cg=ks, ra=nr, role=role)  # (dA - r) c ks
+            if gq:
                 dQ = gemm_abt(Km, dS, role=role)  # [N][d][Nc]
-                if ctx.activation == COSINE:
-                    lib.vst_norm_grad_add(ptr(dQ), ptr(dqn), ptr(qn), ptr(Qm), N, d, Nc, stream())
+                lib.vst_norm_grad_add(ptr(dQ), ptr(dqn), ptr(qn), ptr(Qm), N, d, Nc, stream())
                 dQ = dQ.view(Q.shape)
-            if ctx.needs_input_grad[1]:
+            if gk:
                 dK = bmm_at_b(Qm, d, Nc, True, dS, Ns, role=role)  # [N][d][Ns]
-                if ctx.activation == COSINE:
-                    dMVc = _empty(dMV.shape, dMV)
-                    lib.vst_scale_cols(ptr(dMV), ptr(c), ptr(dMVc), N, 2 * dv, Nc, stream())
-                    Z = gemm_abt(dMVc, Qm, role=role)  # [N][2dv][d]
-                    Y = bmm_at_b(Z, d, 2 * dv, False, VV2, Ns, role=role)  # [N][d][Ns]
-                    dkn = _vec((N, Ns), K)
-                    lib.vst_attn_dkn(ptr(Km), ptr(Y), ptr(plane_dot(Qm, cr)), ptr(ks), ptr(dkn), N, d, Ns, stream())
-                    lib.vst_norm_grad_add(ptr(dK), ptr(dkn), ptr(kn), ptr(Km), N, d, Ns, stream())
+                dMVc = _empty(dMV.shape, dMV)
+                lib.vst_scale_cols(ptr(dMV), ptr(c), ptr(dMVc), N, 2 * dv, Nc, stream())
+                Z = gemm_abt(dMVc, Qm, role=role)  # [N][2dv][d]
+                Y = bmm_at_b(Z, d, 2 * dv, False, VV2, Ns, role=role)  # [N][d][Ns]
+                dkn = _vec((N, Ns), K)
+                lib.vst_attn_dkn(ptr(Km), ptr(Y), ptr(plane_dot(Qm, cr)), ptr(ks), ptr(dkn), N, d, Ns, stream())
+                lib.vst_norm_grad_add(ptr(dK), ptr(dkn), ptr(kn), ptr(Km), N, d, Ns, stream())
                 dK = dK.view(K.shape)
-        if ctx.needs_input_grad[3]:
-            raise VstError("adaattn: gradient w.r.t. the content features (norm_v(c_x)) is not on the reference path")
-        return dQ, dK, dV, None, None
+        return dQ, dK, dV, None, None, None
+
+
+def _softmax_block(Qm, Km, c0, C, role):
+    """A rows c0 .. c0+C-1: softmax_rows(Q[:, :, c0:c0+C]^T K)  [N][C][Ns]."""
+    N, d, Nc = Qm.shape
+    Ns = Km.shape[2]
+    Qb = Qm if (c0 == 0 and C == Nc) else copy_cols(Qm, c0, C)
+    S = bmm_at_b(Qb, C, d, False, Km, Ns, role=role)
+    A, _ = attention_rows(S, SOFTMAX)
+    return A
 
 
 # ---------------------------------------------------------------------------------------------
@@ -361,15 +441,16 @@ class LinearCosineAttnFn(Function):
         return dQ, dK, dV, None
 
 
-def adaattn(Q, K, V, cn, activation=COSINE):
+def adaattn(Q, K, V, cn, activation=COSINE, block_rows=None):
     """AdaAttN attention + modulation (AA/network.py:191-220 after the 1x1 convs).  Cosine: the
     linear form (no Nc x Ns matrix; K / V may hold a divisor of Q's batch, broadcast over repeats);
-    softmax: the materialised-attention path."""
+    softmax: attention formed in blocks of query rows (block_rows; default from
+    SOFTMAX_BLOCK_BYTES)."""
     if activation == COSINE:
         return LinearCosineAttnFn.apply(Q, K, V, cn)
     if K.shape[0] != Q.shape[0]:
         raise VstError("adaattn (softmax): Q and K/V batches must match")
-    return AdaAttnFn.apply(Q, K, V, cn, activation)
+    return AdaAttnFn.apply(Q, K, V, cn, activation, block_rows)
 
 
 _AFFINE_ID = {}

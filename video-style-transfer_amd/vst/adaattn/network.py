@@ -197,17 +197,20 @@ class StylizingNetwork(nn.Module):
         ])
         self.decoder = Decoder()
 
-    def forward(self, fc, fs):
+    def forward(self, fc, fs, down=None):
+        """down (optional, not in the reference's signature): ({idx: feature_down_sample(fc, idx)},
+        {idx: feature_down_sample(fs, idx)}) for idx 2..4, already formed by the caller (the
+        trainers form them once per step for the model and the AdaAttnNoConv loss targets)."""
         with ops.gemm_scope("stylizer"):
-            return self._forward(fc, fs)
+            return self._forward(fc, fs, down)
 
-    def _forward(self, fc, fs):
+    def _forward(self, fc, fs, down=None):
         fc = list(fc.values())
         fs = list(fs.values())
         outs = []
         for i in range(3):
             idx = i + 2
-            c_1x = feature_down_sample(fc, idx)
-            s_1x = feature_down_sample(fs, idx)
+            c_1x = feature_down_sample(fc, idx) if down is None else down[0][idx]
+            s_1x = feature_down_sample(fs, idx) if down is None else down[1][idx]
             outs.append(self.adaattn[i](fc[idx], fs[idx], c_1x, s_1x))
         return self.decoder(outs[2], outs[1], outs[0])

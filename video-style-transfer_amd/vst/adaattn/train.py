@@ -53,6 +53,15 @@ def _cat2(x, y):
     return out
 
 
+def _down_sampled(fc, fs):
+    """({idx: feature_down_sample(fc, idx)}, {idx: feature_down_sample(fs, idx)}) for the three
+    attention levels (AA/network.py:247-249, AA/train_video.py:96-101), data features only."""
+    with torch.no_grad():
+        lc, ls = list(fc.values()), list(fs.values())
+        return ({idx: feature_down_sample(lc, idx) for idx in (2, 3, 4)},
+                {idx: feature_down_sample(ls, idx) for idx in (2, 3, 4)})
+
+
 class AdaAttNTrainer:
     def __init__(self, model, vgg, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weights=None, activation="cosine",
                  process_group=None):
@@ -90,7 +99,11 @@ class AdaAttNTrainer:
         # cosine attention takes the style side once for both content frames (K / V broadcast over
         # the two halves of the batch: the style 1x1 convs, down-sampling and K U^T run on B images)
         fs2 = fs if self.activation == "cosine" else {k: _cat2(v, v) for k, v in fs.items()}
-        fcs = self.vgg(self.model(fc12, fs2))  # cs1 ++ cs2
+        # feature_down_sample of the data features, once per step: the stylizer takes both content
+        # frames' and the style's, the AdaAttnNoConv loss targets frame 1's (the first half of the
+        # content batch) and the style's (the first half when the style side is doubled)
+        down = _down_sampled(fc12, fs2)
+        fcs = self.vgg(self.model(fc12, fs2, down=down))  # cs1 ++ cs2
         fcs1 = {k: v[:B] for k, v in fcs.items()}
         fcs2 = {k: v[B:] for k, v in fcs.items()}
         gs = None
@@ -102,7 +115,7 @@ class AdaAttNTrainer:
         for i in range(3):
             idx = i + 2
             with torch.no_grad():
-                target = self.noconv[i](l1[idx], ls[idx], feature_down_sample(l1, idx), feature_down_sample(ls, idx))
+                target = self.noconv[i](l1[idx], ls[idx], down[0][idx][:B], down[1][idx][:B])
             t = local_feature_loss(fcs1[FEATURES[idx]], target, weight=w["LAMBDA_L"])
             lf = t if lf is None else lf + t
         isl = None
@@ -118,7 +131,8 @@ class AdaAttNTrainer:
         w = self.w
         with torch.no_grad():
             fc, fs = self.vgg(c), self.vgg(s)
-        fcs = self.vgg(self.model(fc, fs))
+        down = _down_sampled(fc, fs)
+        fcs = self.vgg(self.model(fc, fs, down=down))
         gs = None
         for k in FEATURES[1:]:
             t = global_stylized_loss(fcs[k], fs[k], weight=w["LAMBDA_G"])
@@ -128,7 +142,7 @@ class AdaAttNTrainer:
         for i in range(3):
             idx = i + 2
             with torch.no_grad():
-                target = self.noconv[i](lc[idx], ls[idx], feature_down_sample(lc, idx), feature_down_sample(ls, idx))
+                target = self.noconv[i](lc[idx], ls[idx], down[0][idx], down[1][idx])
             t = local_feature_loss(fcs[FEATURES[idx]], target, weight=w["LAMBDA_L"])
             lf = t if lf is None else lf + t
         return {"loss": gs + lf, "loss_gs": gs, "loss_lf": lf}
