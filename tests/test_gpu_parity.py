@@ -79,6 +79,11 @@ CONV_CASES = [
     (2, 3, 12, 20, 64, 3, 1, "zero", 1, "relu"),      # VGG conv1_1
     (2, 64, 8, 12, 128, 3, 1, "zero", 1, "relu"),     # VGG conv
     (1, 256, 4, 6, 512, 3, 1, "zero", 1, "relu"),     # VGG conv4_x
+    # AdaAttN decoder conv7 / conv6 (64 outputs over >= 64 channels, 3x3 reflect): the weight
+    # gradient as the row-split GEMM (rows (co, kh), columns (kw, ci)); ragged width: 3 x 16 + 5
+    (2, 64, 6, 32, 64, 3, 1, "reflect", 1, "relu"),
+    (1, 128, 5, 53, 64, 3, 1, "reflect", 1, "relu"),
+    (2, 64, 8, 32, 3, 3, 1, "reflect", 1, None),      # AdaAttN decoder conv8 (dgrad: 3 source channels)
 ]
 
 

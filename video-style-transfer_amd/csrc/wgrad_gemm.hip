@@ -10,6 +10,8 @@
 // which keeps the result deterministic (no float atomics).
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "vst_common.h"
 #include "vst_hip.h"
 
@@ -380,7 +382,9 @@ struct Wg2Params {
 
 // KD: k-tiles per LDS stage (one barrier per KD tiles); two for the single-product modes, whose
 // k loop does 4-6 MFMAs per wave and tile and is otherwise paced by the per-tile barrier
-template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1>
+// PF: stages of global loads in flight (2 for the single-product modes: two register sets, the
+// loads of stage s+2 issued before the MFMAs of stage s)
+template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1, int PF = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
@@ -468,15 +472,14 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x4 RA[KD][A_IT][2];  // the prefetched stage's registers
-  float RB[KD][B_IT][8];
+  static_assert(PF == 1 || PF == 2, "prefetch depth");
+  f32x4 RA[PF][KD][A_IT][2];  // the prefetched stages' registers (set q holds stage j with j % PF == q)
+  float RB[PF][KD][B_IT][8];
   // tile position (scalar): output row oy, first column ox0
   int t_oy = __builtin_amdgcn_readfirstlane(r_begin / P.Wo);
   int t_ox = __builtin_amdgcn_readfirstlane(r_begin - t_oy * P.Wo);
 
-  auto load_tile = [&](int s, int t) {
-    auto& ra = RA[s];
-    auto& rb = RB[s];
+  auto load_tile = [&](f32x4 (&ra)[A_IT][2], float (&rb)[B_IT][8], int t) {
     const int soff = __builtin_amdgcn_readfirstlane((r_begin + t * BK) * 4);
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
@@ -609,9 +612,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       if (PREC == 1) *reinterpret_cast<u32x2*>(d + 8) = u32x2{l0, l1};
     }
   };
-  auto store_tile = [&](int buf, int s) {
-    auto& ra = RA[s];
-    auto& rb = RB[s];
+  auto store_tile = [&](int buf, int s, const f32x4 (&ra)[A_IT][2], const float (&rb)[B_IT][8]) {
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       if (AQ == 4) {
@@ -665,40 +666,59 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     }
   };
 
-  // a stage = KD consecutive k-tiles in walk order; the tiles of a short last stage are neither
-  // loaded, stored nor computed (ntiles is block-uniform)
+  // a stage = KD consecutive k-tiles in walk order (loaded in order: load_tile's row walk advances
+  // per tile); the tiles of a short last stage are neither loaded, stored nor computed (ntiles is
+  // block-uniform)
   const int nst = (ntiles + KD - 1) / KD;
-  if (ntiles > 0) {
+  auto load_stage = [&](int st, auto set) {
+    constexpr int q = decltype(set)::value;
 #pragma unroll
     for (int d = 0; d < KD; ++d)
-      if (d < ntiles) {
-        load_tile(d, d);
+      if (d == 0 || st * KD + d < ntiles) {
+        load_tile(RA[q][d], RB[q][d], st * KD + d);
         advance();
       }
+  };
+  auto store_stage = [&](int buf, int st, auto set) {
+    constexpr int q = decltype(set)::value;
 #pragma unroll
     for (int d = 0; d < KD; ++d)
-      if (d < ntiles) store_tile(0, d);
+      if (d == 0 || st * KD + d < ntiles) store_tile(buf, d, RA[q][d], RB[q][d]);
+  };
+  auto compute_stage = [&](int st) {
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+      if (d == 0 || st * KD + d < ntiles) mfma_tile(st & 1, d);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, PF - 1>;
+  if (ntiles > 0) {
+    load_stage(0, I0{});
+    if (PF == 2 && nst > 1) load_stage(1, I1{});
+    store_stage(0, 0, I0{});
   }
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nst) {
-#pragma unroll
-      for (int d = 0; d < KD; ++d)
-        if (d == 0 || (st + 1) * KD + d < ntiles) {
-          load_tile(d, (st + 1) * KD + d);
-          advance();
-        }
+  if constexpr (PF == 1) {
+    for (int st = 0; st < nst; ++st) {
+      if (st + 1 < nst) load_stage(st + 1, I0{});
+      compute_stage(st);
+      if (st + 1 < nst) store_stage((st & 1) ^ 1, st + 1, I0{});
+      __syncthreads();
     }
-#pragma unroll
-    for (int d = 0; d < KD; ++d)
-      if (d == 0 || st * KD + d < ntiles) mfma_tile(buf, d);
-    if (st + 1 < nst) {
-#pragma unroll
-      for (int d = 0; d < KD; ++d)
-        if (d == 0 || (st + 1) * KD + d < ntiles) store_tile(buf ^ 1, d);
+  } else {
+    // stage j's registers in set j & 1: at iteration s the set of stage s is free (stored at s-1)
+    // and takes the loads of stage s+2; stage s+1's set is stored after the MFMAs of stage s
+    auto iter = [&](int st, auto par) {
+      using Q = decltype(par);
+      if (st + 2 < nst) load_stage(st + 2, Q{});
+      compute_stage(st);
+      if (st + 1 < nst) store_stage(Q::value ^ 1, st + 1, std::integral_constant<int, 1 - Q::value>{});
+      __syncthreads();
+    };
+    for (int st = 0; st < nst; st += 2) {
+      iter(st, I0{});
+      if (st + 1 < nst) iter(st + 1, I1{});
     }
-    __syncthreads();
   }
 
   float* slab = P.slab + (long)bz * P.Mpad * P.Jpad;
@@ -834,16 +854,16 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
   return best;
 }
 
-template <int PR, int GMD, int KD>
+template <int PR, int GMD, int KD, int PF = 1>
 static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
   switch (c) {
-    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
   }
 }
 
@@ -851,9 +871,13 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
   static const bool kd2 = !getenv("VST_WKD2") || atoi(getenv("VST_WKD2")) != 0;
+  static const bool pf2 = !getenv("VST_PF2") || atoi(getenv("VST_PF2")) != 0;
   if constexpr (PR == 2 || PR == 4) {
     if (kd2) {
-      launch_wg2_pk<PR, GMD, 2>(c, g, st, P);
+      if (pf2)
+        launch_wg2_pk<PR, GMD, 2, 2>(c, g, st, P);
+      else
+        launch_wg2_pk<PR, GMD, 2, 1>(c, g, st, P);
       return;
     }
   }

@@ -18,6 +18,8 @@ Multi-GPU: one process per GPU, (content1, content2, style) triples sharded acro
 RCCL all-reduce of the flat gradient per step; Adam applies the 1/world average.  Every loss term
 is a per-rank mean or per-rank sum exactly as the reference computes it on its own batch.
 """
+import os
+
 import torch
 
 from .. import ops
@@ -51,6 +53,38 @@ def _cat2(x, y):
     ops.copy_into(x.contiguous(), out[:x.shape[0]])
     ops.copy_into(y.contiguous(), out[x.shape[0]:])
     return out
+
+
+class _Halves(torch.autograd.Function):
+    """(x[:B], x[B:]) along the batch, whose backward writes the two halves' gradients straight into
+    one buffer (autograd's slice backward zero-fills a full-size tensor per half and then adds the
+    two: two fills, two copies and an add per VGG feature)."""
+
+    @staticmethod
+    def forward(ctx, x, B):
+        ctx.B = B
+        ctx.shape = x.shape
+        return x[:B].view_as(x[:B]), x[B:].view_as(x[B:])
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        B = ctx.B
+        gx = torch.empty(ctx.shape, device=(g1 if g1 is not None else g2).device, dtype=torch.float32)
+        for g, dst in ((g1, gx[:B]), (g2, gx[B:])):
+            if g is None:
+                dst.zero_()
+            else:
+                ops.copy_into(g.contiguous(), dst)
+        return gx, None
+
+
+_HALVES = os.environ.get("VST_HALVES", "1") != "0"
+
+
+def _halves(v, B):
+    if not (_HALVES and v.requires_grad):
+        return v[:B], v[B:]
+    return _Halves.apply(v, B)
 
 
 def _down_sampled(fc, fs):
@@ -104,8 +138,9 @@ class AdaAttNTrainer:
         # content batch) and the style's (the first half when the style side is doubled)
         down = _down_sampled(fc12, fs2)
         fcs = self.vgg(self.model(fc12, fs2, down=down))  # cs1 ++ cs2
-        fcs1 = {k: v[:B] for k, v in fcs.items()}
-        fcs2 = {k: v[B:] for k, v in fcs.items()}
+        halves = {k: _halves(v, B) for k, v in fcs.items()}
+        fcs1 = {k: h[0] for k, h in halves.items()}
+        fcs2 = {k: h[1] for k, h in halves.items()}
         gs = None
         for k in FEATURES[1:]:
             t = global_stylized_loss(fcs1[k], fs[k], weight=w["LAMBDA_G"])

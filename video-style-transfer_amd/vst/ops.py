@@ -492,6 +492,21 @@ def rowsplit_ok(Cout, ks, stride, pad_mode, up):
     return Cout * ks <= 32 and ks > 1 and stride == 1 and pad_mode == "reflect" and up == 1
 
 
+RS_WGRAD = os.environ.get("VST_RSW", "1") != "0"
+
+
+def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
+    """Weight gradients that run as row-split GEMMs: the tiny-Cout convs above, and 64-output
+    3x3 stride-1 reflect convs over >= 64 channels (the AdaAttN decoder's conv6 / conv7,
+    AA/network.py:93-96).  Rows (co, kh) read dY[co][y - kh], columns (kw, ci) read x[ci][y][x + kw]:
+    M = 3 Cout and J = 3 Cin instead of M = Cout and J = 9 Cin, so each dY tile feeds 3x the rows and
+    is re-read for 3x fewer column tiles (64 x 576 -> 192 x 192 for 64 -> 64)."""
+    if rowsplit_ok(Cout, ks, stride, pad_mode, up):
+        return True
+    return (RS_WGRAD and Cout <= 64 and Cin >= 64 and ks == 3 and stride == 1 and pad_mode == "reflect" and up == 1
+            and W % 16 == 0)
+
+
 def conv_fwd_rowsplit(x, w, b, epi, aux):
     N, Cin, H, W = x.shape
     Cout, _, K, _ = w.shape
@@ -625,7 +640,7 @@ class Conv2dFn(Function):
                             dmask=x if ctx.relu_flags[0] else None)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
-            if rowsplit_ok(w.shape[0], ks, stride, pad_mode, up) and pad == ks // 2:
+            if rowsplit_wgrad_ok(w.shape[0], w.shape[1], ks, stride, pad_mode, up, x.shape[3]) and pad == ks // 2:
                 dw = conv_wgrad_rowsplit(gz, x, w.shape, out=sink)
             else:
                 dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up, out=sink)
