@@ -14,12 +14,4 @@ bash tools/pmc_busy_r02.sh reconet > gpurun_out/r03b_busy.log 2>&1 || exit 4
 python tools/pmc_busy.py reconet gpurun_out/r03_mfma_busy_reconet.json > gpurun_out/r03b_busy2.log 2>&1 || exit 4
 timeout -k 10 500 python bench.py > gpurun_out/r03b_bench.json 2> gpurun_out/r03b_bench.err || exit 5
 timeout -k 10 300 python bench.py --gemm f32 --steps 60 --no-cpu-baseline > gpurun_out/r03b_bench_f32.json 2> gpurun_out/r03b_bench_f32.err || exit 6
-timeout -k 10 400 python bench.py --model adaattn --steps 40 > gpurun_out/r03b_bench_aa4.json 2> gpurun_out/r03b_bench_aa4.err || exit 7
-timeout -k 10 600 python bench.py --model adaattn --batch 8 --height 512 --width 1024 --steps 20 --prof-steps 3 --cpu-steps 1 --cpu-warmup 0 --no-vgg19 > gpurun_out/r03b_bench_aa5.json 2> gpurun_out/r03b_bench_aa5.err || exit 8
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r03b_prof3 -o run -- \
-  python3 bench.py --steps 20 --prof-steps 5 --no-cpu-baseline --no-vgg19 > gpurun_out/r03b_prof3.log 2>&1 || exit 9
-python tools/prof_summary.py gpurun_out/r03b_prof3 30 > gpurun_out/r03b_kernel_summary.txt 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r03b_prof5 -o run -- \
-  python3 bench.py --model adaattn --batch 8 --height 512 --width 1024 --steps 5 --prof-steps 2 --no-cpu-baseline --no-vgg19 > gpurun_out/r03b_prof5.log 2>&1 || exit 10
-python tools/prof_summary.py gpurun_out/r03b_prof5 12 > gpurun_out/r03b_adaattn_c5_kernel_summary.txt 2>&1
 echo done

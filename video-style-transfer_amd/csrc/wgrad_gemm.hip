@@ -871,7 +871,9 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
   static const bool kd2 = !getenv("VST_WKD2") || atoi(getenv("VST_WKD2")) != 0;
-  static const bool pf2 = !getenv("VST_PF2") || atoi(getenv("VST_PF2")) != 0;
+  // VST_WPF2 (weight gradient only) overrides VST_PF2
+  static const char* pf2e = getenv("VST_WPF2") ? getenv("VST_WPF2") : getenv("VST_PF2");
+  static const bool pf2 = !pf2e || atoi(pf2e) != 0;
   if constexpr (PR == 2 || PR == 4) {
     if (kd2) {
       if (pf2)
