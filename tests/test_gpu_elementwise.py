@@ -1,0 +1,148 @@
+"""Vector / row-grid forms of the pooling, resize and attention elementwise kernels, on a real MI355X.
+
+The library picks them when the shapes and alignments allow (W % 4 == 0 and 16-byte aligned planes
+for the 2x2 max-pool, a plane count that fits the grid for resize / outer_axpy / column-norm
+adjoint / copy_planes, n % 4 == 0 for the ReLU backward) and falls back to the flat per-element
+kernels otherwise; both forms are checked here against the torch fp32 CPU reference of the same op
+(MaxPool2d routes a window's gradient to its first maximum in scan order; F.interpolate bilinear,
+align_corners=False, AA/network.py:59 / AA/utilities.py:98-109).  Pooling and copies are bit-exact;
+resize within 1e-6 relative.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def G(t):
+    return t.to(DEV)
+
+
+def C(t):
+    return t.detach().cpu()
+
+
+# (N, C, H, W): odd H (trailing row), W % 4 == 0 (vector form); W % 4 != 0 (flat form)
+POOL_SHAPES = [(2, 8, 9, 16), (3, 4, 8, 32), (1, 5, 12, 20), (2, 3, 9, 15), (2, 4, 8, 10)]
+
+
+@pytest.mark.parametrize("shape", POOL_SHAPES)
+def test_maxpool_fwd_bwd(shape):
+    from vst import ops
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(shape, generator=g)
+    x[0, 0, 0, 1] = float("nan")  # NaN wins its window (forward value and routed gradient)
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xg = G(x).requires_grad_(True)
+    y = ops.maxpool2x2(xg)
+    y.backward(G(gy))
+    assert torch.equal(C(y).isnan(), yr.detach().isnan())
+    assert torch.equal(torch.nan_to_num(C(y)), torch.nan_to_num(yr.detach()))
+    assert torch.equal(C(xg.grad), xr.grad)
+
+
+@pytest.mark.parametrize("shape", POOL_SHAPES)
+def test_maxpool_relu_mask_and_feature_pool(shape):
+    """pool backward with the producer's ReLU mask folded in, and the slice-boundary form
+    relu_mask(pool_bwd(g_pool) + g_feature)."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(5)
+    h = torch.relu(torch.randn(shape, generator=g))
+    gp = torch.randn(shape[:2] + (shape[2] // 2, shape[3] // 2), generator=g)
+    gf = torch.randn(shape, generator=g)
+    hr = h.clone().requires_grad_(True)
+    F.max_pool2d(hr, 2, 2).backward(gp)
+    ref_pool = hr.grad * (h > 0)
+    ref_feat = (hr.grad + gf) * (h > 0)
+
+    hg = G(h).requires_grad_(True)
+    ops.maxpool2x2(hg, relu_mask=True).backward(G(gp))
+    assert torch.equal(C(hg.grad), ref_pool)
+
+    hg = G(h).requires_grad_(True)
+    f, p = ops.feature_pool(hg)
+    torch.autograd.backward([f, p], [G(gf), G(gp)])
+    assert torch.equal(C(hg.grad), ref_feat)
+
+    hg = G(h).requires_grad_(True)  # only the feature gradient (g_pool is None)
+    f, p = ops.feature_pool(hg)
+    f.backward(G(gf))
+    assert torch.equal(C(hg.grad), gf * (h > 0))
+
+
+@pytest.mark.parametrize("src,dst", [((2, 16, 17, 30), (9, 12)), ((3, 8, 64, 128), (16, 32)), ((2, 4, 8, 16), (16, 32))])
+def test_resize_bilinear(src, dst):
+    from vst import ops
+
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(src, generator=g)
+    ref = F.interpolate(x, size=dst, mode="bilinear", align_corners=False)
+    out = ops.resize_bilinear(G(x), dst)
+    assert rel_err(C(out), ref) < 1e-6
+    # per-channel scale into a channel slice of a larger buffer (concat target)
+    sc = torch.rand(src[1], generator=g)
+    buf = torch.zeros((src[0], src[1] + 3) + dst, device=DEV)
+    ops.resize_bilinear(G(x), dst, chscale=G(sc), out=buf[:, 3:])
+    assert rel_err(C(buf[:, 3:]), ref * sc.view(1, -1, 1, 1)) < 1e-6
+    assert not C(buf[:, :3]).any()
+    # + addend (dense output)
+    add = torch.randn((src[0], src[1]) + dst, generator=g)
+    out = ops.resize_bilinear(G(x), dst, addend=G(add))
+    assert rel_err(C(out), ref + add) < 1e-6
+
+
+@pytest.mark.parametrize("n", [4096 * 3, 4097])
+def test_relu_bwd(n):
+    from vst import ops
+
+    g = torch.Generator().manual_seed(9)
+    gy, y = torch.randn(n, generator=g), torch.relu(torch.randn(n, generator=g))
+    out = ops.relu_bwd(G(gy).view(1, 1, 1, n), G(y).view(1, 1, 1, n))
+    assert torch.equal(C(out).view(-1), gy * (y > 0))
+
+
+@pytest.mark.parametrize("N,M,P", [(2, 24, 300), (3, 5, 1024), (1, 7, 1)])
+def test_outer_axpy_and_normalize_bwd(N, M, P):
+    from vst import _lib
+    from vst.adaattn import attention as A
+
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, M, P, generator=g)
+    u = torch.randn(N, M, generator=g)
+    v = torch.randn(N, P, generator=g)
+    w = torch.rand(N, P, generator=g) + 0.5
+    ref = (x + 0.75 * u[:, :, None] * v[:, None, :]) * w[:, None, :]
+    out = torch.empty(N, M, P, device=DEV)
+    _lib.lib.vst_outer_axpy(*(t.data_ptr() for t in (G(x), G(u), G(v), G(w))), 0.75, out.data_ptr(), N, M, P,
+                            torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel_err(C(out), ref) < 1e-6
+    # column-normalisation adjoint: (dxh - xh * t) * s with t = sum_c xh dxh
+    xh, dxh = G(x), G(torch.randn(N, M, P, generator=g))
+    s = G(w)
+    got = A._normalize_bwd(xh, dxh, s)
+    t = (C(xh) * C(dxh)).sum(1, keepdim=True)
+    assert rel_err(C(got), (C(dxh) - C(xh) * t) * w[:, None, :]) < 1e-5
+
+
+def test_copy_planes():
+    from vst import ops
+
+    g = torch.Generator().manual_seed(17)
+    src = torch.randn(3, 4, 8, 16, generator=g)
+    buf = torch.zeros(3, 9, 8, 16, device=DEV)
+    ops.copy_into(G(src), buf[:, 2:6])  # vector form: strides and offsets multiples of 4 floats
+    assert torch.equal(C(buf[:, 2:6]), src) and not C(buf[:, :2]).any() and not C(buf[:, 6:]).any()
+    src = torch.randn(3, 1, 5, 3, generator=g)  # 15 floats per image: flat form
+    buf = torch.zeros(3, 2, 5, 3, device=DEV)
+    ops.copy_into(G(src), buf[:, 1:])
+    assert torch.equal(C(buf[:, 1:]), src) and not C(buf[:, :1]).any()

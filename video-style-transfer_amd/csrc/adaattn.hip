@@ -478,6 +478,15 @@ __global__ void copy_planes_kernel(const float* __restrict__ src, long src_bs, f
   dst[n * dst_bs + t] = src[n * src_bs + t];
 }
 
+// copy_planes_kernel with the image on blockIdx.y and four floats per thread (per, src_bs, dst_bs
+// multiples of 4 and 16-byte aligned bases): no per-element 64-bit division
+__global__ __launch_bounds__(256) void copy_planes_vec_kernel(const float4* __restrict__ src, long src_bs4,
+                                                              float4* __restrict__ dst, long dst_bs4, long per4) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= per4) return;
+  dst[blockIdx.y * dst_bs4 + t] = src[blockIdx.y * src_bs4 + t];
+}
+
 // D = 1 - G / (un_i vn_j + 1e-6)  (cosine_distance, AA/lossfn.py:25-38)
 __global__ void cosdist_kernel(const float* __restrict__ G, const float* __restrict__ un, const float* __restrict__ vn,
                                float* __restrict__ D, int N, int C) {
@@ -493,6 +502,11 @@ __global__ void cosdist_kernel(const float* __restrict__ G, const float* __restr
 
 extern "C" int vst_copy_planes(const float* src, long src_bs, float* dst, long dst_bs, int N, long per, void* stream) {
   VST_CHECK_ARG(src && dst && N > 0 && per > 0);
+  if (N <= 65535 && ((per | src_bs | dst_bs) & 3) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    copy_planes_vec_kernel<<<dim3((unsigned)ceil_div(per / 4, 256), (unsigned)N), 256, 0, (hipStream_t)stream>>>(
+        (const float4*)src, src_bs / 4, (float4*)dst, dst_bs / 4, per / 4);
+    return vst_launch_status();
+  }
   copy_planes_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(src, src_bs, dst, dst_bs, N, per);
   return vst_launch_status();
 }
@@ -722,6 +736,21 @@ __global__ void outer_axpy_kernel(const float* __restrict__ x, const float* __re
   out[idx] = a;
 }
 
+// outer_axpy_kernel with the (n, m) row on blockIdx.y (P on x): the flat form's two 64-bit divisions
+// per element made it VALU-bound (config 5: 18 launches, 213 us each)
+__global__ __launch_bounds__(256) void outer_axpy_rows_kernel(const float* __restrict__ x, const float* __restrict__ u,
+                                                              const float* __restrict__ v, const float* __restrict__ w,
+                                                              float alpha, float* out, int M, long P) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int nm = blockIdx.y, n = nm / M;
+  const long idx = (long)nm * P + p;
+  float a = x[idx];
+  if (u) a += alpha * u[nm] * (v ? v[n * P + p] : 1.0f);
+  if (w) a *= w[n * P + p];
+  out[idx] = a;
+}
+
 // out[i] = sum_{r < R} x[r * per + i]  (gradients of operands broadcast over R repeats of a batch)
 __global__ void sum_repeats_kernel(const float* __restrict__ x, float* __restrict__ out, int R, long per) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -742,12 +771,30 @@ __global__ void normalize_cols_bwd_kernel(const float* __restrict__ xh, const fl
   const long np = n * P + p;
   out[idx] = (dxh[idx] - xh[idx] * t[np]) * s[np];
 }
+
+// normalize_cols_bwd_kernel with the (n, c) row on blockIdx.y
+__global__ __launch_bounds__(256) void normalize_cols_bwd_rows_kernel(const float* __restrict__ xh,
+                                                                      const float* __restrict__ dxh,
+                                                                      const float* __restrict__ t,
+                                                                      const float* __restrict__ s,
+                                                                      float* __restrict__ out, int C, long P) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int nc = blockIdx.y, n = nc / C;
+  const long idx = (long)nc * P + p, np = (long)n * P + p;
+  out[idx] = (dxh[idx] - xh[idx] * t[np]) * s[np];
+}
 }  // namespace
 
 extern "C" int vst_outer_axpy(const float* x, const float* u, const float* v, const float* w, float alpha, float* out,
                               int N, int M, long P, void* stream) {
   VST_CHECK_ARG(x && out && N > 0 && M > 0 && P > 0);
   const long total = (long)N * M * P;
+  if ((long)N * M <= 65535 && P >= 64) {  // (short rows, e.g. _neg's P = 1, keep the flat form)
+    outer_axpy_rows_kernel<<<dim3((unsigned)ceil_div(P, 256), (unsigned)(N * M)), 256, 0, (hipStream_t)stream>>>(
+        x, u, v, w, alpha, out, M, P);
+    return vst_launch_status();
+  }
   outer_axpy_kernel<<<ceil_div(total, RT), RT, 0, (hipStream_t)stream>>>(x, u, v, w, alpha, out, M, P, total);
   return vst_launch_status();
 }
@@ -762,6 +809,11 @@ extern "C" int vst_normalize_cols_bwd(const float* xh, const float* dxh, const f
                                       int N, int C, long P, void* stream) {
   VST_CHECK_ARG(xh && dxh && t && s && out && N > 0 && C > 0 && P > 0);
   const long total = (long)N * C * P;
+  if ((long)N * C <= 65535 && P >= 64) {
+    normalize_cols_bwd_rows_kernel<<<dim3((unsigned)ceil_div(P, 256), (unsigned)(N * C)), 256, 0,
+                                     (hipStream_t)stream>>>(xh, dxh, t, s, out, C, P);
+    return vst_launch_status();
+  }
   normalize_cols_bwd_kernel<<<ceil_div(total, RT), RT, 0, (hipStream_t)stream>>>(xh, dxh, t, s, out, C, P, total);
   return vst_launch_status();
 }

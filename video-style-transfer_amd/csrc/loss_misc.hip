@@ -218,6 +218,15 @@ __global__ void relu_bwd_kernel(const float* __restrict__ gy, const float* __res
   gx[i] = y[i] > 0.f ? gy[i] : 0.f;
 }
 
+// four elements per thread (n % 4 == 0, 16-byte aligned): one float4 per stream
+__global__ __launch_bounds__(256) void relu_bwd_vec_kernel(const float4* __restrict__ gy, const float4* __restrict__ y,
+                                                           float4* __restrict__ gx, long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 g = gy[i], v = y[i];
+  gx[i] = make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f, v.w > 0.f ? g.w : 0.f);
+}
+
 __constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
 __constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
 
@@ -476,6 +485,11 @@ int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, f
 
 int vst_relu_bwd(const float* gy, const float* y, float* gx, long n, void* stream) {
   VST_CHECK_ARG(gy && y && gx && n > 0);
+  if ((n & 3) == 0 && (((uintptr_t)gy | (uintptr_t)y | (uintptr_t)gx) & 15) == 0) {
+    relu_bwd_vec_kernel<<<ceil_div(n / 4, 256), 256, 0, (hipStream_t)stream>>>((const float4*)gy, (const float4*)y,
+                                                                               (float4*)gx, n / 4);
+    return vst_launch_status();
+  }
   relu_bwd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(gy, y, gx, n);
   return vst_launch_status();
 }

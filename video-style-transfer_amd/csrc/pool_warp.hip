@@ -101,6 +101,94 @@ __global__ void maxpool_bwd_add_kernel(const float* __restrict__ x, const float*
   }
 }
 
+// Vector forms of the three pooling kernels above, for W % 4 == 0 and 16-byte aligned planes (every
+// VGG layer of the training steps).  The per-element kernels decode (plane, row, column) with 64-bit
+// division by runtime H / W per element, which made them VALU-bound at well under half the HBM rate
+// (config-5 pool backward: 844 us per launch); here the plane is blockIdx.z, the row blockIdx.y*4 +
+// threadIdx.y, and each thread owns two adjacent 2x2 windows: two float4 loads of x, one float2 of gy,
+// two float4 stores of gx -- no division at all.  Same routing rule (first maximum in scan order,
+// NaN wins) and the same trailing-row treatment for odd H.
+__device__ __forceinline__ int pool_arg(float a, float b, float c, float d) {
+  int arg = 0;
+  float m = a;
+  if (b > m || isnan(b)) m = b, arg = 1;
+  if (c > m || isnan(c)) m = c, arg = 2;
+  if (d > m || isnan(d)) m = d, arg = 3;
+  return arg;
+}
+
+__global__ __launch_bounds__(256) void maxpool_fwd_vec_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                              int H, int W) {
+  const int Ho = H >> 1, Wo = W >> 1, Wq = W >> 2;
+  const int j = blockIdx.x * 64 + threadIdx.x, oy = blockIdx.y * 4 + threadIdx.y;
+  if (j >= Wq || oy >= Ho) return;
+  const float* p = x + (long)blockIdx.z * H * W + (long)(2 * oy) * W + 4 * j;
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + W);
+  float m0 = a.x, m1 = a.z;
+  if (a.y > m0 || isnan(a.y)) m0 = a.y;
+  if (b.x > m0 || isnan(b.x)) m0 = b.x;
+  if (b.y > m0 || isnan(b.y)) m0 = b.y;
+  if (a.w > m1 || isnan(a.w)) m1 = a.w;
+  if (b.z > m1 || isnan(b.z)) m1 = b.z;
+  if (b.w > m1 || isnan(b.w)) m1 = b.w;
+  *reinterpret_cast<float2*>(y + (long)blockIdx.z * Ho * Wo + (long)oy * Wo + 2 * j) = make_float2(m0, m1);
+}
+
+// gx = relu_mask(pool_bwd(gy) + addend) (gy / addend may be NULL): maxpool_bwd_kernel when addend is
+// NULL, maxpool_bwd_add_kernel otherwise
+__global__ __launch_bounds__(256) void maxpool_bwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                                              const float* __restrict__ addend, float* __restrict__ gx,
+                                                              int H, int W, int relu_mask) {
+  const int Ho = H >> 1, Wo = W >> 1, Hc = (H + 1) >> 1, Wq = W >> 2;
+  const int j = blockIdx.x * 64 + threadIdx.x, oy = blockIdx.y * 4 + threadIdx.y;
+  if (j >= Wq || oy >= Hc) return;
+  const bool full = oy < Ho;  // the window's second row exists (else: the trailing row of an odd H)
+  const long o = (long)blockIdx.z * H * W + (long)(2 * oy) * W + 4 * j;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 a = *reinterpret_cast<const float4*>(x + o);
+  const float4 b = full ? *reinterpret_cast<const float4*>(x + o + W) : z4;
+  float r0[4] = {0.f, 0.f, 0.f, 0.f}, r1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (gy && full) {
+    const float2 g = *reinterpret_cast<const float2*>(gy + (long)blockIdx.z * Ho * Wo + (long)oy * Wo + 2 * j);
+    const int a0 = pool_arg(a.x, a.y, b.x, b.y), a1 = pool_arg(a.z, a.w, b.z, b.w);
+    r0[0] = a0 == 0 ? g.x : 0.f;
+    r0[1] = a0 == 1 ? g.x : 0.f;
+    r1[0] = a0 == 2 ? g.x : 0.f;
+    r1[1] = a0 == 3 ? g.x : 0.f;
+    r0[2] = a1 == 0 ? g.y : 0.f;
+    r0[3] = a1 == 1 ? g.y : 0.f;
+    r1[2] = a1 == 2 ? g.y : 0.f;
+    r1[3] = a1 == 3 ? g.y : 0.f;
+  }
+  if (addend) {
+    const float4 d0 = *reinterpret_cast<const float4*>(addend + o);
+    const float4 d1 = full ? *reinterpret_cast<const float4*>(addend + o + W) : z4;
+    r0[0] += d0.x, r0[1] += d0.y, r0[2] += d0.z, r0[3] += d0.w;
+    r1[0] += d1.x, r1[1] += d1.y, r1[2] += d1.z, r1[3] += d1.w;
+  }
+  if (relu_mask) {
+    const float xa[4] = {a.x, a.y, a.z, a.w}, xb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!(xa[k] > 0.f)) r0[k] = 0.f;
+      if (!(xb[k] > 0.f)) r1[k] = 0.f;
+    }
+  }
+  *reinterpret_cast<float4*>(gx + o) = make_float4(r0[0], r0[1], r0[2], r0[3]);
+  if (full) *reinterpret_cast<float4*>(gx + o + W) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+}
+
+// the vector forms apply: W % 4 == 0, 16-byte aligned x / gx / addend, 8-byte aligned y / gy, and a
+// plane count that fits grid.z
+inline bool pool_vec_ok(long NC, int W, const void* a16, const void* b16, const void* c16, const void* d8) {
+  const uintptr_t m16 = (uintptr_t)a16 | (uintptr_t)b16 | (uintptr_t)c16;
+  return (W & 3) == 0 && NC <= 65535 && (m16 & 15) == 0 && ((uintptr_t)d8 & 7) == 0;
+}
+inline dim3 pool_vec_grid(long NC, int rows, int W) {
+  return dim3((unsigned)ceil_div((long)(W >> 2), 64), (unsigned)ceil_div((long)rows, 4), (unsigned)NC);
+}
+
 struct Bilin {
   int x0, y0;
   float w[4];  // nw, ne, sw, se
@@ -338,6 +426,29 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
   out[o] = v;
 }
 
+// resize_kernel with the plane on blockIdx.z and the output row on blockIdx.y * 4 + threadIdx.y: the
+// per-element 64-bit (plane, row, column) division of the flat form made it VALU-bound (config 5:
+// 22 launches, 268 us each); same arithmetic per output element
+__global__ __launch_bounds__(256) void resize_plane_kernel(const float* __restrict__ x, float* __restrict__ out, int C,
+                                                           int H, int W, int Ho, int Wo, const float* chscale,
+                                                           int binarize, long out_bs, const float* __restrict__ addend) {
+  const int ox = blockIdx.x * 64 + threadIdx.x, oy = blockIdx.y * 4 + threadIdx.y;
+  if (ox >= Wo || oy >= Ho) return;
+  const int nc = blockIdx.z, n = nc / C, c = nc - n * C;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  resize_axis(oy, H, Ho, y0, y1, ly);
+  resize_axis(ox, W, Wo, x0, x1, lx);
+  const float* p = x + (long)nc * H * W;
+  float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
+            ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
+  if (chscale) v *= chscale[c];
+  if (binarize) v = v > 0.f ? 1.f : 0.f;
+  const long o = (long)n * out_bs + (long)c * Ho * Wo + (long)oy * Wo + ox;
+  if (addend) v += addend[o];
+  out[o] = v;
+}
+
 // weight with which input index i enters output index d along one axis (0 if it does not)
 __device__ __forceinline__ float resize_weight(int d, int i, int n_in, int n_out) {
   int i0, i1;
@@ -458,6 +569,10 @@ int vst_upsample2x_bwd(const float* gout, const float* ymask, float* gx, long NC
 
 int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* stream) {
   VST_CHECK_ARG(x && y && NC > 0 && H >= 2 && W >= 2);
+  if (pool_vec_ok(NC, W, x, x, x, y)) {
+    maxpool_fwd_vec_kernel<<<pool_vec_grid(NC, H / 2, W), dim3(64, 4), 0, (hipStream_t)stream>>>(x, y, H, W);
+    return vst_launch_status();
+  }
   long total = NC * (H / 2) * (W / 2);
   maxpool_fwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, y, NC, H, W);
   return vst_launch_status();
@@ -465,6 +580,11 @@ int vst_maxpool2x2_fwd(const float* x, float* y, long NC, int H, int W, void* st
 
 int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int H, int W, int relu_mask, void* stream) {
   VST_CHECK_ARG(x && gy && gx && NC > 0 && H >= 2 && W >= 2);
+  if (pool_vec_ok(NC, W, x, gx, gx, gy)) {
+    maxpool_bwd_vec_kernel<<<pool_vec_grid(NC, (H + 1) / 2, W), dim3(64, 4), 0, (hipStream_t)stream>>>(
+        x, gy, nullptr, gx, H, W, relu_mask);
+    return vst_launch_status();
+  }
   long total = NC * H * W;
   maxpool_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, gx, NC, H, W, relu_mask);
   return vst_launch_status();
@@ -473,6 +593,11 @@ int vst_maxpool2x2_bwd(const float* x, const float* gy, float* gx, long NC, int 
 int vst_maxpool2x2_bwd_add(const float* x, const float* gy, const float* addend, float* gx, long NC, int H, int W,
                            int relu_mask, void* stream) {
   VST_CHECK_ARG(x && gx && NC > 0 && H >= 2 && W >= 2);
+  if (pool_vec_ok(NC, W, x, gx, addend, gy)) {
+    maxpool_bwd_vec_kernel<<<pool_vec_grid(NC, (H + 1) / 2, W), dim3(64, 4), 0, (hipStream_t)stream>>>(
+        x, gy, addend, gx, H, W, relu_mask);
+    return vst_launch_status();
+  }
   const long total = NC * ((H + 1) / 2) * ((W + 1) / 2);
   maxpool_bwd_add_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, gy, addend, gx, NC, H, W,
                                                                                  relu_mask);
@@ -534,6 +659,12 @@ int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W
   VST_CHECK_ARG(x && out && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
   long total = NC * Ho * Wo;
   if (out_bs <= 0) out_bs = (long)C * Ho * Wo;
+  if (NC <= 65535 && Ho <= 4 * 65535) {
+    const dim3 g((unsigned)ceil_div(Wo, 64), (unsigned)ceil_div(Ho, 4), (unsigned)NC);
+    resize_plane_kernel<<<g, dim3(64, 4), 0, (hipStream_t)stream>>>(x, out, C, H, W, Ho, Wo, chscale, binarize,
+                                                                    out_bs, addend);
+    return vst_launch_status();
+  }
   resize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, NC, C, H, W, Ho, Wo, chscale,
                                                                        binarize, out_bs, addend);
   return vst_launch_status();
