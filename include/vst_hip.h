@@ -360,6 +360,10 @@ int vst_vgg_normalize(float* x, float* out, int N, int HW, int inplace_scale, vo
 int vst_vgg_normalize_bwd(const float* gout, const float* gscaled, float* gx, int N, int HW, void* stream);
 /* ReLU backward: gx = gy * (y > 0) */
 int vst_relu_bwd(const float* gy, const float* y, float* gx, long n, void* stream);
+/* ReLU backward of an output with two consumers (a VGG19 slice output that is both a loss feature and
+ * the next slice's input, AA/vgg19.py:39-63): gx = (g1 + g2) * (y > 0) in one pass, replacing
+ * autograd's sum of the two gradients and the producer's separate ReLU backward; g2 may be NULL */
+int vst_relu_bwd_add(const float* g1, const float* g2, const float* y, float* gx, long n, void* stream);
 /* ConvTanh backward from the saved tanh value (prenorm: fold vgg_normalize's backward in) */
 int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, long HW, int prenorm, void* stream);
 

@@ -146,3 +146,43 @@ def test_copy_planes():
     buf = torch.zeros(3, 2, 5, 3, device=DEV)
     ops.copy_into(G(src), buf[:, 1:])
     assert torch.equal(C(buf[:, 1:]), src) and not C(buf[:, :1]).any()
+
+
+@pytest.mark.parametrize("n", [4096 * 3, 4097])
+def test_relu_bwd_add_and_feature_split(n):
+    """VGG19 slice boundary: relu_mask(g_feature + g_next) in one pass (AA/vgg19.py:39-63)."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(19)
+    h = torch.relu(torch.randn(1, 1, 1, n, generator=g))
+    g1, g2 = torch.randn(h.shape, generator=g), torch.randn(h.shape, generator=g)
+    hg = G(h).requires_grad_(True)
+    f, x = ops.feature_split(hg)
+    torch.autograd.backward([f, x], [G(g1), G(g2)])
+    assert torch.equal(C(hg.grad), (g1 + g2) * (h > 0))
+    hg = G(h).requires_grad_(True)  # one consumer only
+    f, x = ops.feature_split(hg)
+    (x * G(g2)).sum().backward()
+    assert torch.equal(C(hg.grad), g2 * (h > 0))
+
+
+@pytest.mark.parametrize("N,C,P", [(2, 6, 4096), (3, 5, 1030), (1, 3, 7)])
+def test_plane_and_channel_reductions(N, C, P):
+    """plane_dot / channel_dot (AdaAttN linear attention, AA/network.py:121-124) and channel_sum
+    (conv bias gradient): float4 forms when P % 4 == 0, scalar forms otherwise."""
+    from vst import ops
+    from vst.adaattn import attention as A
+
+    g = torch.Generator().manual_seed(23)
+    x, y = torch.randn(N, C, P, generator=g), torch.randn(N, C, P, generator=g)
+    w, v = torch.randn(N, P, generator=g), torch.randn(N, C, generator=g)
+    xd, yd = x.double(), y.double()
+    assert rel_err(C_(A.plane_dot(G(x))), xd.sum(2)) < 1e-6
+    assert rel_err(C_(A.plane_dot(G(x), G(w))), (xd * w.double()[:, None]).sum(2)) < 1e-6
+    assert rel_err(C_(A.channel_dot(G(x), y=G(y))), (xd * yd).sum(1)) < 1e-6
+    assert rel_err(C_(A.channel_dot(G(x), v=G(v))), (xd * v.double()[:, :, None]).sum(1)) < 1e-6
+    assert rel_err(C_(ops.channel_sum(G(x).view(N, C, 1, P))), xd.sum((0, 2))) < 1e-6
+
+
+def C_(t):
+    return t.detach().cpu().double()

@@ -587,6 +587,34 @@ __global__ void plane_dot_kernel(const float* __restrict__ x, const float* __res
   if (threadIdx.x == 0) out[plane] = (float)t;
 }
 
+// plane_dot_kernel over float4 (P % 4 == 0, 16-byte aligned x / w)
+__global__ __launch_bounds__(RT) void plane_dot_vec_kernel(const float4* __restrict__ x, const float4* __restrict__ w,
+                                                           float* __restrict__ out, int C, int P4) {
+  __shared__ double sh[RT / 64];
+  const long plane = blockIdx.x;
+  const float4* xp = x + plane * P4;
+  const float4* wp = w ? w + (long)(plane / C) * P4 : nullptr;
+  double acc = 0.0;
+  int i = threadIdx.x;
+  for (; i + RT < P4; i += 2 * RT) {
+    float4 a = xp[i], b = xp[i + RT];
+    if (wp) {
+      const float4 u = wp[i], v = wp[i + RT];
+      acc += (((double)a.x * u.x + (double)a.y * u.y) + ((double)a.z * u.z + (double)a.w * u.w)) +
+             (((double)b.x * v.x + (double)b.y * v.y) + ((double)b.z * v.z + (double)b.w * v.w));
+    } else {
+      acc += (((double)a.x + a.y) + ((double)a.z + a.w)) + (((double)b.x + b.y) + ((double)b.z + b.w));
+    }
+  }
+  if (i < P4) {
+    const float4 a = xp[i];
+    const float4 u = wp ? wp[i] : make_float4(1.f, 1.f, 1.f, 1.f);
+    acc += ((double)a.x * u.x + (double)a.y * u.y) + ((double)a.z * u.z + (double)a.w * u.w);
+  }
+  const double t = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) out[plane] = (float)t;
+}
+
 // out[n][p] = sum_c x[n][c][p] * (v ? v[n][c] : y[n][c][p])   (64 pixels x 4 channel groups per block)
 __global__ void channel_dot_kernel(const float* __restrict__ x, const float* __restrict__ v,
                                    const float* __restrict__ y, float* __restrict__ out, int N, int C, int P) {
@@ -605,6 +633,46 @@ __global__ void channel_dot_kernel(const float* __restrict__ x, const float* __r
   part[grp][lane] = s;
   __syncthreads();
   if (grp == 0 && p < P) out[(long)n * P + p] = (float)(part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+}
+
+// channel_dot_kernel with four consecutive pixels per lane (P % 4 == 0, 16-byte aligned x / y / out):
+// 256 pixels x 4 channel groups per block, one float4 per operand and channel
+__global__ __launch_bounds__(256) void channel_dot_vec_kernel(const float* __restrict__ x, const float* __restrict__ v,
+                                                              const float* __restrict__ y, float* __restrict__ out,
+                                                              int C, int P) {
+  __shared__ double part[4][64][4];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int n = blockIdx.y;
+  const int p = (blockIdx.x * 64 + lane) * 4;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  if (p < P) {
+    const float* xp = x + (long)n * C * P + p;
+    const float* yp = y ? y + (long)n * C * P + p : nullptr;
+    const float* vp = v ? v + (long)n * C : nullptr;
+    for (int c = grp; c < C; c += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(xp + (long)c * P);
+      float4 b;
+      if (vp) {
+        const float t = vp[c];
+        b = make_float4(t, t, t, t);
+      } else {
+        b = *reinterpret_cast<const float4*>(yp + (long)c * P);
+      }
+      s[0] += (double)a.x * b.x;
+      s[1] += (double)a.y * b.y;
+      s[2] += (double)a.z * b.z;
+      s[3] += (double)a.w * b.w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) part[grp][lane][k] = s[k];
+  __syncthreads();
+  if (grp == 0 && p < P) {
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = (float)(part[0][lane][k] + part[1][lane][k] + part[2][lane][k] + part[3][lane][k]);
+    *reinterpret_cast<float4*>(out + (long)n * P + p) = make_float4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 // forward row terms: rowsum = qkbar/qn + Ns; c = 1/(rowsum qn); e = 1/rowsum; (ks = 1/kn separately)
@@ -674,12 +742,22 @@ extern "C" {
 
 int vst_plane_dot(const float* x, const float* w, float* out, int N, int C, int P, void* stream) {
   VST_CHECK_ARG(x && out && N > 0 && C > 0 && P > 0);
+  if ((P & 3) == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0) {
+    plane_dot_vec_kernel<<<N * C, RT, 0, (hipStream_t)stream>>>(reinterpret_cast<const float4*>(x),
+                                                                reinterpret_cast<const float4*>(w), out, C, P / 4);
+    return vst_launch_status();
+  }
   plane_dot_kernel<<<N * C, RT, 0, (hipStream_t)stream>>>(x, w, out, C, P);
   return vst_launch_status();
 }
 
 int vst_channel_dot(const float* x, const float* v, const float* y, float* out, int N, int C, int P, void* stream) {
   VST_CHECK_ARG(x && out && (v || y) && N > 0 && C > 0 && P > 0);
+  if ((P & 3) == 0 && N <= 65535 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)out) & 15) == 0) {
+    channel_dot_vec_kernel<<<dim3((unsigned)ceil_div(P / 4, 64), (unsigned)N), 256, 0, (hipStream_t)stream>>>(
+        x, v, y, out, C, P);
+    return vst_launch_status();
+  }
   channel_dot_kernel<<<N * ceil_div(P, 64), 256, 0, (hipStream_t)stream>>>(x, v, y, out, N, C, P);
   return vst_launch_status();
 }

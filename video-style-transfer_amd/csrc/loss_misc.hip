@@ -218,6 +218,29 @@ __global__ void relu_bwd_kernel(const float* __restrict__ gy, const float* __res
   gx[i] = y[i] > 0.f ? gy[i] : 0.f;
 }
 
+// gx = (g1 + g2) * (y > 0); g2 may be NULL
+__global__ void relu_bwd_add_kernel(const float* __restrict__ g1, const float* __restrict__ g2,
+                                    const float* __restrict__ y, float* __restrict__ gx, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gx[i] = y[i] > 0.f ? g1[i] + (g2 ? g2[i] : 0.f) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_add_vec_kernel(const float4* __restrict__ g1,
+                                                               const float4* __restrict__ g2,
+                                                               const float4* __restrict__ y, float4* __restrict__ gx,
+                                                               long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 g = g1[i];
+  if (g2) {
+    const float4 h = g2[i];
+    g = make_float4(g.x + h.x, g.y + h.y, g.z + h.z, g.w + h.w);
+  }
+  const float4 v = y[i];
+  gx[i] = make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f, v.w > 0.f ? g.w : 0.f);
+}
+
 // four elements per thread (n % 4 == 0, 16-byte aligned): one float4 per stream
 __global__ __launch_bounds__(256) void relu_bwd_vec_kernel(const float4* __restrict__ gy, const float4* __restrict__ y,
                                                            float4* __restrict__ gx, long n4) {
@@ -480,6 +503,17 @@ int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, f
   long total = (long)N * Kpad * Mpad;
   symmetrize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(g, S, N, C, Kpad, Mpad, scale,
                                                                            apack_split(mode));
+  return vst_launch_status();
+}
+
+int vst_relu_bwd_add(const float* g1, const float* g2, const float* y, float* gx, long n, void* stream) {
+  VST_CHECK_ARG(g1 && y && gx && n > 0);
+  if ((n & 3) == 0 && (((uintptr_t)g1 | (uintptr_t)g2 | (uintptr_t)y | (uintptr_t)gx) & 15) == 0) {
+    relu_bwd_add_vec_kernel<<<ceil_div(n / 4, 256), 256, 0, (hipStream_t)stream>>>(
+        (const float4*)g1, (const float4*)g2, (const float4*)y, (float4*)gx, n / 4);
+    return vst_launch_status();
+  }
+  relu_bwd_add_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(g1, g2, y, gx, n);
   return vst_launch_status();
 }
 

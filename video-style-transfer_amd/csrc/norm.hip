@@ -343,6 +343,26 @@ __global__ __launch_bounds__(NTN) void plane_sum_kernel(const float* __restrict_
   if (threadIdx.x == 0) out[plane] = (float)s;
 }
 
+// plane_sum_kernel over float4 (HW % 4 == 0, 16-byte aligned x): two float4 loads in flight per
+// thread per iteration instead of one scalar (the config-5 bias gradients sum 512x1024 planes)
+__global__ __launch_bounds__(NTN) void plane_sum_vec_kernel(const float4* __restrict__ x, float* __restrict__ out,
+                                                            int HW4) {
+  __shared__ double sh[NTN / 64];
+  const float4* xp = x + (long)blockIdx.x * HW4;
+  double s = 0.0;
+  int i = threadIdx.x;
+  for (; i + NTN < HW4; i += 2 * NTN) {
+    const float4 a = xp[i], b = xp[i + NTN];
+    s += (((double)a.x + a.y) + ((double)a.z + a.w)) + (((double)b.x + b.y) + ((double)b.z + b.w));
+  }
+  if (i < HW4) {
+    const float4 a = xp[i];
+    s += ((double)a.x + a.y) + ((double)a.z + a.w);
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -382,7 +402,10 @@ int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const floa
 int vst_channel_sum(const float* x, float* out, float* partial, int N, int C, int HW, int accumulate, void* stream) {
   VST_CHECK_ARG(x && out && partial && N > 0 && C > 0 && HW > 0);
   hipStream_t st = (hipStream_t)stream;
-  plane_sum_kernel<<<N * C, NTN, 0, st>>>(x, partial, HW);
+  if ((HW & 3) == 0 && ((uintptr_t)x & 15) == 0)
+    plane_sum_vec_kernel<<<N * C, NTN, 0, st>>>(reinterpret_cast<const float4*>(x), partial, HW / 4);
+  else
+    plane_sum_kernel<<<N * C, NTN, 0, st>>>(x, partial, HW);
   sum_over_n_kernel<<<ceil_div(C, 256), 256, 0, st>>>(partial, N, C, 1, out, nullptr, nullptr, accumulate);
   return vst_launch_status();
 }

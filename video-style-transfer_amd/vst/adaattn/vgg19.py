@@ -4,8 +4,12 @@ Same slice layout and state_dict keys (`slice1.0.weight` ... `slice5.28.bias`). 
 to a local torchvision vgg19 state dict (the reference downloads IMAGENET1K_V1; there is no
 network here), otherwise torchvision's default initialisation.
 """
+import os
+
+import torch
 import torch.nn as nn
 
+from .. import ops
 from ..reconet.network import _load_torchvision_features, run_vgg_slice, vgg_features
 from .utilities import vgg_normalize
 
@@ -13,6 +17,8 @@ from .utilities import vgg_normalize
 _VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512]
 _SLICES = ((0, 2), (2, 7), (7, 12), (12, 21), (21, 30))
 FEATURES = ("relu1_1", "relu2_1", "relu3_1", "relu4_1", "relu5_1")
+# VST_FEATURE_SPLIT=0: slice boundaries through autograd's sum + a separate ReLU backward (A/B only)
+_SPLIT = os.environ.get("VST_FEATURE_SPLIT", "1") != "0"
 
 
 class VGG19(nn.Module):
@@ -32,6 +38,13 @@ class VGG19(nn.Module):
         x = vgg_normalize(x)
         out = {}
         for s, name in enumerate(FEATURES, 1):
-            x = run_vgg_slice(getattr(self, f"slice{s}"), x)
-            out[name] = x
+            last = s == len(FEATURES)
+            if _SPLIT and not last and torch.is_grad_enabled() and x.requires_grad:
+                # slice boundary with a gradient: the feature's two consumers (losses, next slice)
+                # meet in FeatureSplitFn's fused backward, so the producing conv runs premasked
+                x = run_vgg_slice(getattr(self, f"slice{s}"), x, premasked_out=True)
+                out[name], x = ops.feature_split(x)
+            else:
+                x = run_vgg_slice(getattr(self, f"slice{s}"), x)
+                out[name] = x
         return out

@@ -780,6 +780,36 @@ def feature_pool(h):
     return FeaturePoolFn.apply(h)
 
 
+class FeatureSplitFn(Function):
+    """A VGG slice output h (a ReLU output) that is both a loss feature and the next slice's conv
+    input (AA/vgg19.py:39-63: relu1_1 .. relu4_1 feed slice2 .. slice5 and the losses): returns two
+    views of h; the backward is relu_mask(g_feature + g_next) in one pass (vst_relu_bwd_add),
+    replacing autograd's sum of the two gradients and the producer's ReLU backward (the producing
+    conv is then built premasked)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        h = _check(h, "feature", 4)
+        ctx.save_for_backward(h)
+        ctx.set_materialize_grads(False)
+        return h.view_as(h), h.view_as(h)
+
+    @staticmethod
+    def backward(ctx, g_feat, g_next):
+        (h,) = ctx.saved_tensors
+        gs = [g.contiguous() for g in (g_feat, g_next) if g is not None]
+        if not gs:
+            return None
+        gx = _empty(h.shape, h)
+        lib.vst_relu_bwd_add(ptr(gs[0]), ptr(gs[1]) if len(gs) > 1 else None, ptr(h), ptr(gx), h.numel(), stream())
+        return gx
+
+
+def feature_split(h):
+    """(h, h) with the fused slice-boundary backward of FeatureSplitFn."""
+    return FeatureSplitFn.apply(h)
+
+
 class WarpFn(Function):
     """utilities.warp (RC/utilities.py:39-57); gradient w.r.t. x only (flow is data)."""
 
