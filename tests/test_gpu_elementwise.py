@@ -169,7 +169,8 @@ def test_relu_bwd_add_and_feature_split(n):
 @pytest.mark.parametrize("N,C,P", [(2, 6, 4096), (3, 5, 1030), (1, 3, 7)])
 def test_plane_and_channel_reductions(N, C, P):
     """plane_dot / channel_dot (AdaAttN linear attention, AA/network.py:121-124) and channel_sum
-    (conv bias gradient): float4 forms when P % 4 == 0, scalar forms otherwise."""
+    (conv bias gradient): plane_dot / channel_sum take their float4 forms when P % 4 == 0 and the
+    scalar forms otherwise; channel_dot is scalar."""
     from vst import ops
     from vst.adaattn import attention as A
 
@@ -186,3 +187,24 @@ def test_plane_and_channel_reductions(N, C, P):
 
 def C_(t):
     return t.detach().cpu().double()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("transpose", [0, 1])
+def test_pack_matrix_row_form_matches_flat_form(mode, transpose):
+    """vst_pack_matrix (the attention GEMMs' packed A operand): the one-thread-per-(k-tile, row) form
+    (16-byte aligned output) and the per-element form (taken for a misaligned output) write the same
+    bytes, in every GEMM mode, for both operand orientations and a ragged M x K."""
+    from vst import _lib
+
+    B, M, K, Mpad, Kpad = 3, 45, 70, 64, 80
+    g = torch.Generator().manual_seed(29)
+    x = G(torch.randn(B, M * K, generator=g))
+    words = B * Mpad * Kpad * (3 if mode == 3 else 2) // 2
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.full((words,), 7.0, device=DEV)
+    b = torch.full((words + 1,), 7.0, device=DEV)
+    _lib.lib.vst_pack_matrix(x.data_ptr(), a.data_ptr(), B, M, K, transpose, Mpad, Kpad, M * K, mode, st)
+    _lib.lib.vst_pack_matrix(x.data_ptr(), b.data_ptr() + 4, B, M, K, transpose, Mpad, Kpad, M * K, mode, st)
+    torch.cuda.synchronize()
+    assert torch.equal(C(a).view(torch.int32), C(b[1:]).view(torch.int32))

@@ -37,6 +37,63 @@ __global__ void pack_matrix_kernel(const float* __restrict__ x, float* __restric
   apack_store(out + b * per * ((bsplit & 3) == 2 ? 3 : 2) / 2, k, m, Mpad, v, bsplit);  // bf16x6 packs are 1.5x
 }
 
+// pack_matrix_kernel with one thread per (batch, k-tile, row m): the 16 k of its packed block are
+// gathered, split and written as whole 16-byte words (the per-element form decoded its position
+// with 64-bit division and wrote each piece as a separate 2-byte store); same arithmetic per element
+// (split_bf16x2 / split3_bf16x2 are apack_store's splits two elements at a time)
+__global__ __launch_bounds__(64) void pack_matrix_rows_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                              int M, int K, int transpose, int Mpad, int Kpad,
+                                                              long x_bs, int split) {
+  const int m = blockIdx.x * 64 + threadIdx.x;
+  if (m >= Mpad) return;
+  const int kt = blockIdx.y, b = blockIdx.z;
+  split &= 3;
+  const float* xb = x + b * x_bs;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = kt * 16 + i;
+    v[i] = (m < M && k < K) ? (transpose ? xb[(long)m * K + k] : xb[(long)k * M + m]) : 0.f;
+  }
+  const long per = (long)Mpad * Kpad;
+  float* ob = out + b * per * (split == 2 ? 3 : 2) / 2;
+  const long row = (long)kt * Mpad + m;
+  if (split == 0) {  // apack_index: even k in dwords 0..7, odd k in 8..15
+    f32x4* d = reinterpret_cast<f32x4*>(ob + row * 16);
+    d[0] = f32x4{v[0], v[2], v[4], v[6]};
+    d[1] = f32x4{v[8], v[10], v[12], v[14]};
+    d[2] = f32x4{v[1], v[3], v[5], v[7]};
+    d[3] = f32x4{v[9], v[11], v[13], v[15]};
+  } else if (split == 2) {  // bf16x6: [hi k0..15][mid][lo]
+    uint32_t h[8], md[8], l[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) split3_bf16x2(v[2 * q], v[2 * q + 1], h[q], md[q], l[q]);
+    u32x4* d = reinterpret_cast<u32x4*>(ob + row * 24);
+    d[0] = u32x4{h[0], h[1], h[2], h[3]};
+    d[1] = u32x4{h[4], h[5], h[6], h[7]};
+    d[2] = u32x4{md[0], md[1], md[2], md[3]};
+    d[3] = u32x4{md[4], md[5], md[6], md[7]};
+    d[4] = u32x4{l[0], l[1], l[2], l[3]};
+    d[5] = u32x4{l[4], l[5], l[6], l[7]};
+  } else {  // bf16x3 / bf16: [hi k0..15][lo]; fp16: [f16 k0..15][zeros]
+    uint32_t h[8], l[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (split == 3) {
+        h[q] = pack_f16x2(v[2 * q], v[2 * q + 1]);
+        l[q] = 0u;
+      } else {
+        split_bf16x2(v[2 * q], v[2 * q + 1], h[q], l[q]);
+      }
+    }
+    u32x4* d = reinterpret_cast<u32x4*>(ob + row * 16);
+    d[0] = u32x4{h[0], h[1], h[2], h[3]};
+    d[1] = u32x4{h[4], h[5], h[6], h[7]};
+    d[2] = u32x4{l[0], l[1], l[2], l[3]};
+    d[3] = u32x4{l[4], l[5], l[6], l[7]};
+  }
+}
+
 // out[n][p] = sqrt(sum_c x[n][c][p]^2)  (vector_norm over the channel axis)
 // block = 64 consecutive pixels x 4 channel quarters; coalesced 256-B row reads, LDS combine
 __global__ void channel_norm_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int C, int P) {
@@ -349,6 +406,12 @@ int vst_pack_matrix(const float* x, float* packed, int B, int M, int K, int tran
                     int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(x && packed && B > 0 && M > 0 && K > 0 && Mpad >= M && Kpad >= K);
+  if (Kpad % 16 == 0 && Kpad / 16 <= 65535 && B <= 65535 && ((uintptr_t)packed & 15) == 0) {
+    const dim3 g((unsigned)ceil_div(Mpad, 64), (unsigned)(Kpad / 16), (unsigned)B);
+    pack_matrix_rows_kernel<<<g, 64, 0, (hipStream_t)stream>>>(x, packed, M, K, transpose, Mpad, Kpad, x_bs,
+                                                               apack_split(mode));
+    return vst_launch_status();
+  }
   long total = (long)B * Mpad * Kpad;
   pack_matrix_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
       x, packed, B, M, K, transpose, Mpad, Kpad, x_bs, apack_split(mode));
@@ -635,46 +698,6 @@ __global__ void channel_dot_kernel(const float* __restrict__ x, const float* __r
   if (grp == 0 && p < P) out[(long)n * P + p] = (float)(part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
 }
 
-// channel_dot_kernel with four consecutive pixels per lane (P % 4 == 0, 16-byte aligned x / y / out):
-// 256 pixels x 4 channel groups per block, one float4 per operand and channel
-__global__ __launch_bounds__(256) void channel_dot_vec_kernel(const float* __restrict__ x, const float* __restrict__ v,
-                                                              const float* __restrict__ y, float* __restrict__ out,
-                                                              int C, int P) {
-  __shared__ double part[4][64][4];
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int n = blockIdx.y;
-  const int p = (blockIdx.x * 64 + lane) * 4;
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  if (p < P) {
-    const float* xp = x + (long)n * C * P + p;
-    const float* yp = y ? y + (long)n * C * P + p : nullptr;
-    const float* vp = v ? v + (long)n * C : nullptr;
-    for (int c = grp; c < C; c += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(xp + (long)c * P);
-      float4 b;
-      if (vp) {
-        const float t = vp[c];
-        b = make_float4(t, t, t, t);
-      } else {
-        b = *reinterpret_cast<const float4*>(yp + (long)c * P);
-      }
-      s[0] += (double)a.x * b.x;
-      s[1] += (double)a.y * b.y;
-      s[2] += (double)a.z * b.z;
-      s[3] += (double)a.w * b.w;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) part[grp][lane][k] = s[k];
-  __syncthreads();
-  if (grp == 0 && p < P) {
-    float r[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = (float)(part[0][lane][k] + part[1][lane][k] + part[2][lane][k] + part[3][lane][k]);
-    *reinterpret_cast<float4*>(out + (long)n * P + p) = make_float4(r[0], r[1], r[2], r[3]);
-  }
-}
-
 // forward row terms: rowsum = qkbar/qn + Ns; c = 1/(rowsum qn); e = 1/rowsum; (ks = 1/kn separately)
 __global__ void attn_fwd_rows_kernel(const float* __restrict__ qkbar, const float* __restrict__ qn, float* __restrict__ c,
                                      float* __restrict__ e, long n, int Ns) {
@@ -753,11 +776,6 @@ int vst_plane_dot(const float* x, const float* w, float* out, int N, int C, int 
 
 int vst_channel_dot(const float* x, const float* v, const float* y, float* out, int N, int C, int P, void* stream) {
   VST_CHECK_ARG(x && out && (v || y) && N > 0 && C > 0 && P > 0);
-  if ((P & 3) == 0 && N <= 65535 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)out) & 15) == 0) {
-    channel_dot_vec_kernel<<<dim3((unsigned)ceil_div(P / 4, 64), (unsigned)N), 256, 0, (hipStream_t)stream>>>(
-        x, v, y, out, C, P);
-    return vst_launch_status();
-  }
   channel_dot_kernel<<<N * ceil_div(P, 64), 256, 0, (hipStream_t)stream>>>(x, v, y, out, N, C, P);
   return vst_launch_status();
 }
