@@ -372,6 +372,20 @@ int vst_tanh_out_bwd(const float* gy, const float* t, float* gv, long total, lon
 int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
              long step, float gscale, void* stream);
 
+/* Adam under a dynamic loss scale (the fp16 policy's overflow guard; the reference steps in fp32
+ * every batch, AA/train_video.py:121-122, RC/train_single/train_candy.py:151-152, and needs none):
+ * one device-side pass flags any Inf / NaN in g; on a flagged step nothing is updated (p, m, v and
+ * the Adam step count untouched) and the scale is multiplied by `backoff`; a clean step is
+ * vst_adam with g * world_scale / scale, its step count read from the state, and the scale grows by
+ * `growth` after `growth_interval` clean steps in a row.  No host synchronisation.
+ * state: 8 floats, [0] scale (seed of the next backward), [1] clean steps since the last change,
+ * [2] Adam step count, [3] last step skipped (0/1), [4] step_size, [5] sqrt(bias correction 2),
+ * [6] last gradient factor, [7] skipped steps in total.  ws: >= VST_SCALER_WS floats; g 16-B aligned. */
+#define VST_SCALER_WS 1024
+int vst_adam_loss_scaled(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                         float eps, float world_scale, float* state, float* ws, int growth_interval, float growth,
+                         float backoff, void* stream);
+
 /* ---- RTNSTV (RT/train.py, RT/network.py) --------------------------------------------------
  * sqrt-TV regulariser (RT/train.py:57-61): out[0] = weight * mean over (nc, y < H-1, x < W-1) of
  * sqrt(clamp((s[y][x+1]-s[y][x])^2 + (s[y+1][x]-s[y][x])^2, 1e-8)); ws/out as vst_tv_fwd */

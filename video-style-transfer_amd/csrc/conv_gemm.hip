@@ -248,7 +248,7 @@ __global__ void fold_border_kernel(const float* __restrict__ border, const float
 
 extern "C" {
 
-int vst_version(void) { return 200; }
+int vst_version(void) { return 400; }
 
 #ifndef VST_BUILD_ID
 #define VST_BUILD_ID "unknown"
@@ -322,27 +322,22 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   int cfg = widen_cfg(select_cfg(M), (long)Ho * Wo);
   {
     // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
-    static const bool t256 = !getenv("VST_T256") || atoi(getenv("VST_T256")) != 0;
     const int am = vst_mode_arith(mode);
-    if (t256 && cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16))
+    if (cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16))
       cfg = T256;
-    // bf16x6 A-direct blocks (VST_AD64 / VST_AD128 / VST_AD192 / VST_AD256: 0 off, 1 on, 2 data
-    // gradients only)
-    auto env_mode = [](const char* n, int dflt) { const char* v = getenv(n); return v ? atoi(v) : dflt; };
-    static const int ad64 = env_mode("VST_AD64", 1), ad192 = env_mode("VST_AD192", 2), ad256 = env_mode("VST_AD256", 1),
-                     ad128 = env_mode("VST_AD128", 1);
+    // bf16x6 A-direct blocks: 64-, 128- and 256-row tiles always, the 192-row tile for data
+    // gradients only (its forward keeps the LDS-A tile: DESIGN.md §4.2 item 3)
     const bool dg = gmode == GM_TRANSPOSED;
     if (VST_ADIR && am == VST_GEMM_BF16X6) {
-      if (cfg == T128 && M % 256 == 0 && (ad256 == 1 || (ad256 == 2 && dg))) cfg = T256A;
-      if (cfg == T128 && (ad128 == 1 || (ad128 == 2 && dg))) cfg = T128A;
-      if ((cfg == T64W || cfg == T64) && (ad64 == 1 || (ad64 == 2 && dg))) cfg = T64A;
-      if (cfg == T192 && (ad192 == 1 || (ad192 == 2 && dg))) cfg = T192A;
+      if (cfg == T128 && M % 256 == 0) cfg = T256A;
+      if (cfg == T128) cfg = T128A;
+      if (cfg == T64W || cfg == T64) cfg = T64A;
+      if (cfg == T192 && dg) cfg = T192A;
     }
     // single-product modes (bf16, fp16): A-direct blocks with two k-tiles per stage -- the LDS-A
     // tiles stage 256 weight rows x 32 B per k-tile through LDS for 8 MFMAs per wave, which puts
-    // their LDS store traffic past the array's write rate (VST_ADS=0: the LDS-A tiles)
-    static const int ads = env_mode("VST_ADS", 1);
-    if (VST_ADIR && VST_ADIR_SP && ads && (am == VST_GEMM_BF16 || am == VST_GEMM_F16)) {
+    // their LDS store traffic past the array's write rate
+    if (VST_ADIR && VST_ADIR_SP && (am == VST_GEMM_BF16 || am == VST_GEMM_F16)) {
       if (cfg == T256) cfg = T256A;
       if (cfg == T128) cfg = M % 256 == 0 ? T256A : T128A;
       if (cfg == T64W || cfg == T64) cfg = T64A;

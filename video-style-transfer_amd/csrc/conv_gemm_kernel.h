@@ -2,7 +2,6 @@
 // conv_gemm_p{0,1,2}.hip, which each instantiate one GEMM arithmetic mode, and conv_gemm.hip,
 // which holds the host launcher and the C ABI).  See conv_gemm.hip for the algorithm.
 #pragma once
-#include <type_traits>
 
 #include "vst_common.h"
 
@@ -121,11 +120,10 @@ __device__ __forceinline__ int a_slot2(int idx) {
 // across the MFMAs of the current KD).  The single-product modes (bf16, fp16) do one MFMA per
 // fragment pair, so at KD 1 their k loop is paced by the barrier and the LDS round trip of every
 // 16-deep tile rather than by the MFMAs; KD 2 halves both per MFMA.
-// PF: stages of global loads in flight (2: the loads of stage s+2 are issued before the MFMAs of
-// stage s, two register sets).  The single-product k loop is latency-bound: a 16-MFMA stage per
-// wave does not cover a first-touch (HBM) gather at one stage of prefetch.
-template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false, int KD = 1,
-          int PF = 1>
+// One stage of global loads is in flight (the loads of stage s+1 across the MFMAs of stage s).  A
+// two-stage variant (round 3, `PF = 2`) measured slower and computed wrong gradients in the
+// train_video step; it was removed rather than shipped behind a switch.
+template <int WM, int TM, int WN, int TN, bool CFAST, bool GM, int MINW, int PREC, bool ADIR = false, int KD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParams P) {
   static_assert(!ADIR || PREC >= 2, "A-direct: bf16x6, bf16, fp16");
   static_assert(ADIR || WM * WN == 4, "LDS-A path: 4 waves");
@@ -202,10 +200,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  static_assert(PF == 1 || PF == 2, "prefetch depth");
-  f32x4 ra0[PF][KD][A_PER];
-  float rb0[PF][KD][B_PER];
-  float rg0[PF][KD][GM ? B_PER : 1];
+  f32x4 ra0[KD][A_PER];
+  float rb0[KD][B_PER];
+  float rg0[KD][GM ? B_PER : 1];
   // buffer descriptors over this image's source planes (wave-uniform inputs only)
   const int plane_i = P.Hs * P.Ws;
   const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane_i * 4u;
@@ -232,7 +229,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   int ad_voff[ADIR ? TM : 1];
 #pragma unroll
   for (int i = 0; i < (ADIR ? TM : 1); ++i) ad_voff[i] = (((wm * TM + i) * 32 + lo) * AW + 4 * hi) * 4;
-  bf16x8_t arN[PF][KD][ADIR ? TM : 1][3], arC[KD][ADIR ? TM : 1][3];
+  bf16x8_t arN[KD][ADIR ? TM : 1][3], arC[KD][ADIR ? TM : 1][3];
 
   // CFAST walk, tiles in k order: tap-major -- the (tap, channel) position advances by 16 channels
   // per tile and the gather offset is decoded once per tap (wave-uniform branch); channel-blocked
@@ -438,36 +435,29 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   // tile t+2 measured no gain: the loop is not waiting on global latency)
   // (A-direct: the A registers of tile t+1 land with the B loads the store waits for, then become
   // the current set -- register moves after that wait, no extra drain)
-  // register set q of the prefetch ring (a compile-time index: a runtime one would put the
-  // arrays in scratch)
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, PF - 1>;
-  auto rotate_a = [&](auto set) {
-    constexpr int q = decltype(set)::value;
+  auto rotate_a = [&]() {
     if constexpr (ADIR) {
 #pragma unroll
       for (int d = 0; d < KD; ++d)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int pc = 0; pc < (PREC == 3 ? 3 : 1); ++pc) arC[d][i][pc] = arN[q][d][i][pc];
+          for (int pc = 0; pc < (PREC == 3 ? 3 : 1); ++pc) arC[d][i][pc] = arN[d][i][pc];
     }
   };
   // a stage = KD consecutive k-tiles (tile order is the walk order of load_tile, so stages are
   // loaded in order); the tiles of a short last stage are neither loaded, stored nor computed
   // (ntiles is block-uniform)
   const int nst = (ntiles + KD - 1) / KD;
-  auto load_stage = [&](int s, auto set) {
-    constexpr int q = decltype(set)::value;
+  auto load_stage = [&](int s) {
 #pragma unroll
     for (int d = 0; d < KD; ++d)
-      if (d == 0 || s * KD + d < ntiles) load_tile(s * KD + d, ra0[q][d], rb0[q][d], rg0[q][d], arN[q][d]);
+      if (d == 0 || s * KD + d < ntiles) load_tile(s * KD + d, ra0[d], rb0[d], rg0[d], arN[d]);
   };
-  auto store_stage = [&](int buf, int s, auto set) {
-    constexpr int q = decltype(set)::value;
+  auto store_stage = [&](int buf, int s) {
 #pragma unroll
     for (int d = 0; d < KD; ++d)
-      if (d == 0 || s * KD + d < ntiles) store_tile(As[buf][d], Bs[buf][d], ra0[q][d], rb0[q][d], rg0[q][d]);
+      if (d == 0 || s * KD + d < ntiles) store_tile(As[buf][d], Bs[buf][d], ra0[d], rb0[d], rg0[d]);
   };
   auto compute_stage = [&](int s) {
     if (!(ABL & 32)) {
@@ -476,41 +466,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
         if (d == 0 || s * KD + d < ntiles) compute_tile(s & 1, d);
     }
   };
-  if constexpr (PF == 1) {
-    load_stage(0, I0{});
-    store_stage(0, 0, I0{});
-    rotate_a(I0{});
-    __syncthreads();
-    for (int s = 0; s < nst; ++s) {
-      if (s + 1 < nst) load_stage(s + 1, I0{});
-      compute_stage(s);
-      if (s + 1 < nst && !(ABL & 8)) store_stage((s & 1) ^ 1, s + 1, I0{});
-      if (s + 1 < nst) rotate_a(I0{});
-      if (!(ABL & 16)) __syncthreads();
-    }
-  } else {
-    // stage j's registers live in set j & 1: at iteration s the set of stage s is free (stored at
-    // s-1) and takes the loads of stage s+2; stage s+1's set is stored after the MFMAs of stage s
-    load_stage(0, I0{});
-    if (nst > 1) load_stage(1, I1{});
-    store_stage(0, 0, I0{});
-    rotate_a(I0{});
-    __syncthreads();
-    auto iter = [&](int s, auto par) {
-      using Q = decltype(par);
-      using R = std::integral_constant<int, 1 - Q::value>;
-      if (s + 2 < nst) load_stage(s + 2, Q{});
-      compute_stage(s);
-      if (s + 1 < nst) {
-        if (!(ABL & 8)) store_stage(Q::value ^ 1, s + 1, R{});
-        rotate_a(R{});
-      }
-      if (!(ABL & 16)) __syncthreads();
-    };
-    for (int s = 0; s < nst; s += 2) {
-      iter(s, I0{});
-      if (s + 1 < nst) iter(s + 1, I1{});
-    }
+  load_stage(0);
+  store_stage(0, 0);
+  rotate_a();
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    if (s + 1 < nst) load_stage(s + 1);
+    compute_stage(s);
+    if (s + 1 < nst && !(ABL & 8)) store_stage((s & 1) ^ 1, s + 1);
+    if (s + 1 < nst) rotate_a();
+    if (!(ABL & 16)) __syncthreads();
   }
 
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -659,37 +624,13 @@ inline int widen_cfg(int c, long HWo) {
 #ifndef VST_KD2
 #define VST_KD2 1
 #endif
-// two k-tiles per stage for the single-product modes on the 128- and 256-row tiles (VST_KD2=0 at
-// build or run time: one); the smaller tiles keep one (their two-tile stages exceed the register
-// budget of their occupancy target)
-inline bool kd2_on() {
-  static const bool on = VST_KD2 && (!getenv("VST_KD2") || atoi(getenv("VST_KD2")) != 0);
-  return on;
-}
-// ... with two stages of loads in flight (VST_PF2=0 at run time: one)
-inline bool pf2_on() {
-  static const bool on = !getenv("VST_PF2") || atoi(getenv("VST_PF2")) != 0;
-  return on;
-}
-
+// two k-tiles per stage for the single-product modes on the 128- and 256-row tiles; the smaller
+// tiles keep one (their two-tile stages exceed the register budget of their occupancy target).
+// Compile-time only: the library has one tested kernel per (shape, mode) -- no run-time switches.
 template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false, bool KD2OK = false>
 static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
-  if constexpr (VST_KD2 && KD2OK && (PR == 2 || PR == 4)) {
-    if (kd2_on()) {
-      // (two register sets only on the channel-fast gather without a gathered mask: the general
-      // per-element gather keeps its prefetch registers in scratch at PF 2 and computed wrong
-      // results in the train_video step, tests/test_gpu_adaattn.py)
-      if constexpr (CF && !GMK) {
-        if (pf2_on()) {
-          conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, 2, 2><<<grid, WM * WN * 64, 0, st>>>(P);
-          return;
-        }
-      }
-      conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, 2, 1><<<grid, WM * WN * 64, 0, st>>>(P);
-      return;
-    }
-  }
-  conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, 1><<<grid, WM * WN * 64, 0, st>>>(P);
+  constexpr int KD = (VST_KD2 && KD2OK && (PR == 2 || PR == 4)) ? 2 : 1;
+  conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, KD><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 template <bool CF, bool GMK, int PR>

@@ -307,6 +307,87 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   p[i] = p[i] + (-step_size) * (mi / denom);
 }
 
+// ---- dynamic loss scale (the fp16 training policy; torch.cuda.amp.GradScaler's rule, device-side)
+// state (8 floats): [0] scale S (the next backward's seed), [1] clean steps since the last change,
+// [2] Adam step count (advanced on clean steps only), [3] found-inf of the last step, [4] step_size
+// and [5] bc2_sqrt of the last clean step, [6] the last step's gradient factor world_scale / S,
+// [7] skipped steps in total.  Nothing is read back to the host.
+__device__ __forceinline__ bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
+
+// partial[b] = 1 if block b saw an Inf / NaN gradient (float4 grid-stride; the tail per element)
+__global__ void grad_nonfinite_kernel(const float* __restrict__ g, long n, float* __restrict__ partial) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  bool bad = false;
+  const long n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    bad = bad || nonfinite(v.x) || nonfinite(v.y) || nonfinite(v.z) || nonfinite(v.w);
+  }
+  if (blockIdx.x == 0)
+    for (long i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) bad = bad || nonfinite(g[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) any = 1;  // benign same-value LDS write
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (float)any;
+}
+
+// one block: fold the partial flags, decide skip / clean, advance the scale and Adam's step count
+__global__ void loss_scale_update_kernel(const float* __restrict__ partial, int nb, float* __restrict__ state,
+                                         float lr, float b1, float b2, float world_scale, int growth_interval,
+                                         float growth, float backoff) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  bool bad = false;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) bad |= partial[i] != 0.f;
+  if (__any(bad) && (threadIdx.x & 63) == 0) any = 1;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float S = state[0];
+  state[6] = world_scale / S;
+  if (any) {  // skip: parameters and moments untouched, scale backed off
+    state[3] = 1.f;
+    state[0] = S * backoff;
+    state[1] = 0.f;
+    state[7] += 1.f;
+    return;
+  }
+  const float step = state[2] + 1.f;
+  state[2] = step;
+  state[3] = 0.f;
+  // the same double-precision bias corrections as the host path (vst_adam)
+  const double bc1 = 1.0 - pow((double)b1, (double)step), bc2 = 1.0 - pow((double)b2, (double)step);
+  state[4] = (float)(lr / bc1);
+  state[5] = (float)sqrt(bc2);
+  float good = state[1] + 1.f;
+  if (good >= (float)growth_interval) {
+    state[0] = S * growth;
+    good = 0.f;
+  }
+  state[1] = good;
+}
+
+// adam_kernel with its step size, bias correction and gradient factor read from the state; a
+// skipped step returns before touching anything
+__global__ void adam_scaled_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                   float* __restrict__ v, long n, float b1, float b2, float eps,
+                                   const float* __restrict__ state) {
+  if (state[3] != 0.f) return;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float step_size = state[4], bc2_sqrt = state[5], gscale = state[6];
+  float gi = g[i] * gscale;
+  float mi = m[i];
+  mi = mi + (1.0f - b1) * (gi - mi);
+  float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] + (-step_size) * (mi / denom);
+}
+
 // RTNSTV regularisation (RT/train.py:57-61): mean over (n, c, y < H-1, x < W-1) of
 // sqrt(clamp(d1^2 + d2^2, 1e-8)), d1 = s[y][x+1] - s[y][x], d2 = s[y+1][x] - s[y][x]
 __device__ __forceinline__ float tv_sqrt_term(const float* p, int W) {
@@ -557,6 +638,23 @@ int vst_adam(float* p, const float* g, float* m, float* v, long n, float lr, flo
   float bc2_sqrt = (float)sqrt(bc2);
   adam_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(p, g, m, v, n, b1, b2, eps, step_size, bc2_sqrt,
                                                                  gscale);
+  return vst_launch_status();
+}
+
+int vst_adam_loss_scaled(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                         float eps, float world_scale, float* state, float* ws, int growth_interval, float growth,
+                         float backoff, void* stream) {
+  VST_CHECK_ARG(p && g && m && v && state && ws && n > 0 && growth_interval > 0 && growth >= 1.f && backoff > 0.f &&
+                backoff <= 1.f);
+  VST_CHECK_ARG((((uintptr_t)g) & 15) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long n4 = n >> 2;
+  long nbl = (n4 + 255) / 256;
+  nbl = nbl < 1 ? 1 : (nbl > VST_SCALER_WS ? VST_SCALER_WS : nbl);
+  const int nb = (int)nbl;
+  grad_nonfinite_kernel<<<nb, 256, 0, st>>>(g, n, ws);
+  loss_scale_update_kernel<<<1, 256, 0, st>>>(ws, nb, state, lr, b1, b2, world_scale, growth_interval, growth, backoff);
+  adam_scaled_kernel<<<ceil_div(n, 256), 256, 0, st>>>(p, g, m, v, n, b1, b2, eps, state);
   return vst_launch_status();
 }
 

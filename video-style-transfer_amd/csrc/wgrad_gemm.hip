@@ -382,9 +382,8 @@ struct Wg2Params {
 
 // KD: k-tiles per LDS stage (one barrier per KD tiles); two for the single-product modes, whose
 // k loop does 4-6 MFMAs per wave and tile and is otherwise paced by the per-tile barrier
-// PF: stages of global loads in flight (2 for the single-product modes: two register sets, the
-// loads of stage s+2 issued before the MFMAs of stage s)
-template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1, int PF = 1>
+// (one stage of loads in flight; the round-3 two-stage variant measured no gain and was removed)
+template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
@@ -472,9 +471,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  static_assert(PF == 1 || PF == 2, "prefetch depth");
-  f32x4 RA[PF][KD][A_IT][2];  // the prefetched stages' registers (set q holds stage j with j % PF == q)
-  float RB[PF][KD][B_IT][8];
+  f32x4 RA[KD][A_IT][2];  // the prefetched stage's registers
+  float RB[KD][B_IT][8];
   // tile position (scalar): output row oy, first column ox0
   int t_oy = __builtin_amdgcn_readfirstlane(r_begin / P.Wo);
   int t_ox = __builtin_amdgcn_readfirstlane(r_begin - t_oy * P.Wo);
@@ -670,55 +668,34 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   // per tile); the tiles of a short last stage are neither loaded, stored nor computed (ntiles is
   // block-uniform)
   const int nst = (ntiles + KD - 1) / KD;
-  auto load_stage = [&](int st, auto set) {
-    constexpr int q = decltype(set)::value;
+  auto load_stage = [&](int st) {
 #pragma unroll
     for (int d = 0; d < KD; ++d)
       if (d == 0 || st * KD + d < ntiles) {
-        load_tile(RA[q][d], RB[q][d], st * KD + d);
+        load_tile(RA[d], RB[d], st * KD + d);
         advance();
       }
   };
-  auto store_stage = [&](int buf, int st, auto set) {
-    constexpr int q = decltype(set)::value;
+  auto store_stage = [&](int buf, int st) {
 #pragma unroll
     for (int d = 0; d < KD; ++d)
-      if (d == 0 || st * KD + d < ntiles) store_tile(buf, d, RA[q][d], RB[q][d]);
+      if (d == 0 || st * KD + d < ntiles) store_tile(buf, d, RA[d], RB[d]);
   };
   auto compute_stage = [&](int st) {
 #pragma unroll
     for (int d = 0; d < KD; ++d)
       if (d == 0 || st * KD + d < ntiles) mfma_tile(st & 1, d);
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, PF - 1>;
   if (ntiles > 0) {
-    load_stage(0, I0{});
-    if (PF == 2 && nst > 1) load_stage(1, I1{});
-    store_stage(0, 0, I0{});
+    load_stage(0);
+    store_stage(0, 0);
   }
   __syncthreads();
-  if constexpr (PF == 1) {
-    for (int st = 0; st < nst; ++st) {
-      if (st + 1 < nst) load_stage(st + 1, I0{});
-      compute_stage(st);
-      if (st + 1 < nst) store_stage((st & 1) ^ 1, st + 1, I0{});
-      __syncthreads();
-    }
-  } else {
-    // stage j's registers in set j & 1: at iteration s the set of stage s is free (stored at s-1)
-    // and takes the loads of stage s+2; stage s+1's set is stored after the MFMAs of stage s
-    auto iter = [&](int st, auto par) {
-      using Q = decltype(par);
-      if (st + 2 < nst) load_stage(st + 2, Q{});
-      compute_stage(st);
-      if (st + 1 < nst) store_stage(Q::value ^ 1, st + 1, std::integral_constant<int, 1 - Q::value>{});
-      __syncthreads();
-    };
-    for (int st = 0; st < nst; st += 2) {
-      iter(st, I0{});
-      if (st + 1 < nst) iter(st + 1, I1{});
-    }
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) load_stage(st + 1);
+    compute_stage(st);
+    if (st + 1 < nst) store_stage((st & 1) ^ 1, st + 1);
+    __syncthreads();
   }
 
   float* slab = P.slab + (long)bz * P.Mpad * P.Jpad;
@@ -854,36 +831,23 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
   return best;
 }
 
-template <int PR, int GMD, int KD, int PF = 1>
+template <int PR, int GMD, int KD>
 static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
   switch (c) {
-    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
-    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD, PF><<<g, NT, 0, st>>>(P); break;
+    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
   }
 }
 
-// two k-tiles per stage for the single-product modes (VST_WKD2=0 at run time: one)
+// two k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
-  static const bool kd2 = !getenv("VST_WKD2") || atoi(getenv("VST_WKD2")) != 0;
-  // VST_WPF2 (weight gradient only) overrides VST_PF2
-  static const char* pf2e = getenv("VST_WPF2") ? getenv("VST_WPF2") : getenv("VST_PF2");
-  static const bool pf2 = !pf2e || atoi(pf2e) != 0;
-  if constexpr (PR == 2 || PR == 4) {
-    if (kd2) {
-      if (pf2)
-        launch_wg2_pk<PR, GMD, 2, 2>(c, g, st, P);
-      else
-        launch_wg2_pk<PR, GMD, 2, 1>(c, g, st, P);
-      return;
-    }
-  }
-  launch_wg2_pk<PR, GMD, 1>(c, g, st, P);
+  launch_wg2_pk<PR, GMD, (PR == 2 || PR == 4) ? 2 : 1>(c, g, st, P);
 }
 
 template <int GMD>
@@ -900,9 +864,8 @@ static void launch_wg2(int c, dim3 g, int mode, hipStream_t st, const Wg2Params&
 // row-tiled kernel applies: output rows a multiple of 16 wide (plain or row-split A gather), and
 // every source offset within the 2^31 B buffer range
 static bool wg2_ok(int asplit, int Wo) {
-  static const bool off = getenv("VST_WGRAD2") && atoi(getenv("VST_WGRAD2")) == 0;  // A/B switch
-  static const bool rs = !getenv("VST_WGRAD2_RS") || atoi(getenv("VST_WGRAD2_RS")) != 0;  // row-split A/B switch
-  return !off && (!asplit || rs) && Wo % BK == 0;
+  (void)asplit;
+  return Wo % BK == 0;
 }
 
 static int run_wg(const float* a, const float* src, float* slab, int N, int M, int Cs, int Hs, int Ws, int Ho, int Wo,
@@ -936,9 +899,8 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     // (ReCoNet conv1 J = 243, conv2 J = 432): the dY rows are split once per 256 columns instead of
     // per 128, and each wave runs twice the MFMAs per k-tile.  Same Mpad / Jpad / split count, so
     // the slab layout and the workspace size do not change.
-    static const bool wide = !getenv("VST_WG_WIDE") || atoi(getenv("VST_WG_WIDE")) != 0;  // A/B switch
     int cw = c;
-    if (wide && (c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
+    if ((c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
     dim3 g(Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
     if (gmode == 0) launch_wg2<0>(cw, g, mode, st, Q);
     else if (gmode == 2) launch_wg2<2>(cw, g, mode, st, Q);
@@ -987,8 +949,7 @@ static int splits_for(int N, int M, long J, int HWo) {
   int c = wsel(M);
   long Mpad = (M + wbm(c) - 1) / wbm(c) * wbm(c);
   long Jpad = (J + WBN - 1) / WBN * WBN;
-  static const int smul = getenv("VST_WGRAD_SMUL") ? atoi(getenv("VST_WGRAD_SMUL")) : 1;  // tuning experiments
-  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo, c, Mpad, Jpad) * (smul > 0 ? smul : 1);
+  int S = plan_splits((Mpad / wbm(c)) * (Jpad / WBN), N, HWo, c, Mpad, Jpad);
   const int maxs = (HWo + 2 * BK - 1) / (2 * BK);
   return S < maxs ? S : (maxs > 0 ? maxs : 1);
 }

@@ -14,9 +14,6 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvst_hip.so")
-# two stages of loads in flight in the single-product GEMMs (VST_PF2=1): off -- with it on, the
-# config-5 train_video golden step's decoder gradients came out ~3 % of their size
-os.environ.setdefault("VST_PF2", "0")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "vst_hip.h")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 

@@ -23,7 +23,7 @@ import os
 import torch
 
 from .. import ops
-from ..reconet._flat import FlatParams
+from ..reconet._flat import FlatParams, backward_and_adam
 from ..reconet.dist import GradBuckets, broadcast_params, world_info
 from .lossfn import global_stylized_loss, image_similarity_loss, local_feature_loss
 from .network import AdaAttnNoConv
@@ -114,7 +114,7 @@ class AdaAttNTrainer:
         # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
         broadcast_params(self.flat.p, process_group)
         self.dp = GradBuckets(model, self.flat, process_group)
-        self._seed = None
+        self.scaler = None  # LossScaler under the fp16 policy (config 5), created at its first step
 
     def encode(self, c1, c2=None, s=None):
         """VGG19 features of the data images (no gradient).  c1 may be a [3, B, 3, H, W] buffer."""
@@ -190,23 +190,22 @@ class AdaAttNTrainer:
         return self._update(self.losses, c1, c2, s)
 
     def backward(self, loss):
-        """loss.backward() under the policy's static loss scale (ops.loss_scale: every gradient,
-        the flat buffer included, comes out scaled); returns the factor that unscales them."""
+        """loss.backward() seeded as a fresh trainer's first step seeds it (the policy's initial loss
+        scale, `ops.loss_scale()`: 1 except under fp16); returns the factor that unscales the
+        gradients.  Used by the parity tests that inspect gradients before Adam; `step` itself
+        seeds with the dynamic scaler's device-resident scale."""
         s = ops.loss_scale()
         if s == 1.0:
             loss.backward()
             return 1.0
-        if self._seed is None or self._seed[0] != s:
-            self._seed = (s, torch.full((), s, device=loss.device))
-        loss.backward(self._seed[1])
+        loss.backward(torch.full((), s, device=loss.device))
         return 1.0 / s
 
     def _update(self, losses, *args):
+        """losses, backward, gradient exchange, Adam (AA/train_video.py:120-122); under the fp16
+        policy through the dynamic loss scaler (an overflowed step is skipped on the device)."""
         self.flat.zero_grad()
         self.dp.begin()
         out = losses(*args)
-        unscale = self.backward(out["loss"])
-        gscale = self.dp.finish() * unscale
-        self.step_count += 1
-        self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
+        backward_and_adam(self, out["loss"])
         return {k: v.detach() for k, v in out.items()}

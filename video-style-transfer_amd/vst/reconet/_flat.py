@@ -4,11 +4,18 @@ Every parameter becomes a view into one contiguous fp32 buffer and its `.grad` a
 second one, so autograd accumulates straight into the flat gradient (AccumulateGrad adds in
 place into an existing .grad), the DDP all-reduce is ONE RCCL call and Adam is ONE kernel
 (`vst_adam`) over the whole model (62 tensors / 3,763,011 floats for ReCoNet).
+
+`LossScaler` is the fp16 policy's overflow guard (the reference trains in fp32 and steps every
+batch, AA/train_video.py:121-122): a device-resident dynamic loss scale with
+torch.cuda.amp.GradScaler's rule (skip the step and halve the scale on an Inf / NaN gradient, double
+it after `growth_interval` clean steps), applied by `vst_adam_loss_scaled` without a host sync.
 """
 import torch
 from torch.autograd.graph import increment_version
 
 from .._lib import lib, ptr, stream
+
+SCALER_WS = 1024  # include/vst_hip.h VST_SCALER_WS
 
 
 class FlatParams:
@@ -43,9 +50,88 @@ class FlatParams:
             yield off, prm.numel()
             off += prm.numel()
 
+    def _updated(self):
+        # the kernel updated every parameter in place.  `prm.data = view` leaves each Parameter with
+        # its OWN version counter (not the flat buffer's), so bump every parameter's counter: a
+        # graph that saved a parameter before this step then refuses to run backward
+        increment_version(self.params)
+        increment_version(self.p)
+
     def adam(self, step, lr, betas, eps, gscale=1.0):
         lib.vst_adam(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), self.numel, float(lr), float(betas[0]),
                      float(betas[1]), float(eps), int(step), float(gscale), stream())
-        # the kernel updated every parameter in place: bump the version counter the parameter views
-        # share with the flat buffer, so a graph saved before this step refuses to run backward
-        increment_version(self.p)
+        self._updated()
+
+    def adam_scaled(self, scaler, lr, betas, eps, world_scale=1.0):
+        """One Adam step under `scaler` (skipped on device when the gradient holds an Inf / NaN)."""
+        scaler.apply(self, lr, betas, eps, world_scale)
+        self._updated()
+
+
+class LossScaler:
+    """Device-resident dynamic loss scale (state layout: include/vst_hip.h vst_adam_loss_scaled).
+
+    `seed` is the backward's seed tensor (a 0-d view of the state, so the scale a step uses is the
+    one the previous step left on the device); `apply` checks the flat gradient, then skips or
+    applies Adam and advances the scale.  Nothing is read back to the host unless asked
+    (`scale()`, `state_dict()`)."""
+
+    def __init__(self, device, init_scale=2.0 ** 12, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 step=0):
+        if not (init_scale > 0 and growth_factor >= 1.0 and 0 < backoff_factor <= 1.0 and growth_interval > 0):
+            raise ValueError("loss scaler: init_scale > 0, growth_factor >= 1, 0 < backoff_factor <= 1, "
+                             "growth_interval > 0")
+        self.state = torch.zeros(8, device=device, dtype=torch.float32)
+        self.state[0] = float(init_scale)
+        self.state[2] = float(step)
+        self.ws = torch.empty(SCALER_WS, device=device, dtype=torch.float32)
+        self.growth, self.backoff, self.interval = float(growth_factor), float(backoff_factor), int(growth_interval)
+
+    @property
+    def seed(self):
+        return self.state[0]
+
+    def apply(self, flat, lr, betas, eps, world_scale=1.0):
+        lib.vst_adam_loss_scaled(ptr(flat.p), ptr(flat.g), ptr(flat.m), ptr(flat.v), flat.numel, float(lr),
+                                 float(betas[0]), float(betas[1]), float(eps), float(world_scale), ptr(self.state),
+                                 ptr(self.ws), self.interval, self.growth, self.backoff, stream())
+
+    # host views (each one synchronises)
+    def scale(self):
+        return float(self.state[0].item())
+
+    def skipped_last(self):
+        return bool(self.state[3].item() != 0)
+
+    def state_dict(self):
+        st = self.state.cpu()
+        return {"scale": float(st[0]), "growth_tracker": int(st[1]), "step": int(st[2]), "skipped": int(st[7]),
+                "growth_factor": self.growth, "backoff_factor": self.backoff, "growth_interval": self.interval}
+
+    def load_state_dict(self, sd):
+        self.growth, self.backoff = float(sd["growth_factor"]), float(sd["backoff_factor"])
+        self.interval = int(sd["growth_interval"])
+        vals = torch.zeros(8, dtype=torch.float32)
+        vals[0], vals[1], vals[2], vals[7] = sd["scale"], sd["growth_tracker"], sd["step"], sd.get("skipped", 0)
+        self.state.copy_(vals)
+
+
+def backward_and_adam(trainer, loss):
+    """loss.backward(), the data-parallel gradient exchange and one Adam step for a trainer holding
+    `flat`, `dp`, `lr`, `betas`, `eps`, `step_count` and `scaler` (the reference's
+    `loss.backward(); optimizer.step()`).  Under a policy with a loss scale (`ops.loss_scale()`,
+    the fp16 policy) the backward is seeded with the device-resident dynamic scale and Adam runs
+    through the `LossScaler` (skipped on overflow); the scaler, once created, stays in use (its
+    Adam step count continues the trainer's)."""
+    from .. import ops  # (ops imports this module's siblings)
+
+    s = ops.loss_scale()
+    if s != 1.0 and trainer.scaler is None:
+        trainer.scaler = LossScaler(loss.device, init_scale=s, step=trainer.step_count)
+    trainer.step_count += 1
+    if trainer.scaler is None:
+        loss.backward()
+        trainer.flat.adam(trainer.step_count, trainer.lr, trainer.betas, trainer.eps, trainer.dp.finish())
+        return
+    loss.backward(trainer.scaler.seed)
+    trainer.flat.adam_scaled(trainer.scaler, trainer.lr, trainer.betas, trainer.eps, trainer.dp.finish())

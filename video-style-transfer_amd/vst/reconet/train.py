@@ -29,7 +29,7 @@ on its (per-rank) batch.
 import torch
 
 from .. import ops
-from ._flat import FlatParams
+from ._flat import FlatParams, backward_and_adam
 from .dist import GradBuckets, broadcast_params, world_info
 
 LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
@@ -80,7 +80,7 @@ class ReCoNetTrainer:
         # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
         broadcast_params(self.flat.p, process_group)
         self.dp = GradBuckets(model, self.flat, process_group)
-        self._seed = None
+        self.scaler = None  # LossScaler under a loss-scaled (fp16) policy, created at the first such step
         dev = self.flat.p.device
         self.chscale_cache = {}
         with torch.no_grad():
@@ -163,23 +163,23 @@ class ReCoNetTrainer:
         return out
 
     def backward(self, loss):
-        """loss.backward() under the policy's static loss scale (ops.loss_scale); returns the factor
-        that unscales the gradients."""
+        """loss.backward() seeded as a fresh trainer's first step seeds it (the policy's initial loss
+        scale, `ops.loss_scale()`: 1 except under fp16); returns the factor that unscales the
+        gradients.  Used by the parity tests that inspect gradients before Adam; `step` itself
+        seeds with the dynamic scaler's device-resident scale."""
         s = ops.loss_scale()
         if s == 1.0:
             loss.backward()
             return 1.0
-        if self._seed is None or self._seed[0] != s:
-            self._seed = (s, torch.full((), s, device=loss.device))
-        loss.backward(self._seed[1])
+        loss.backward(torch.full((), s, device=loss.device))
         return 1.0 / s
 
     def step(self, frames, flow=None, mask=None):
+        """One training step (train_candy.py:77-152): losses, backward, gradient exchange, Adam.
+        `step_count` counts calls; under the fp16 policy Adam's own count lives in `scaler` and does
+        not advance on a skipped (overflowed) step."""
         self.flat.zero_grad()
         self.dp.begin()
         out = self.losses(frames, flow, mask)
-        unscale = self.backward(out["loss"])
-        gscale = self.dp.finish() * unscale
-        self.step_count += 1
-        self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
+        backward_and_adam(self, out["loss"])
         return {k: v.detach() for k, v in out.items()}

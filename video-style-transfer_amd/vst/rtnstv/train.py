@@ -13,7 +13,7 @@ Multi-GPU: frame pairs sharded, one RCCL all-reduce of the flat gradient (vst.re
 import torch
 
 from .. import ops
-from ..reconet._flat import FlatParams
+from ..reconet._flat import FlatParams, backward_and_adam
 from ..reconet.dist import GradBuckets, broadcast_params, world_info
 
 # RT/train.py:28-31
@@ -27,6 +27,7 @@ class RTNSTVTrainer:
         self.lr, self.betas, self.eps = lr, betas, eps
         self.flat = FlatParams(model)
         self.step_count = 0
+        self.scaler = None  # LossScaler under a loss-scaled (fp16) policy
         self.pg = process_group
         self.rank, self.world = world_info(process_group)
         # DP: rank 0's initial parameters everywhere; gradient buckets all-reduced from backward
@@ -63,8 +64,5 @@ class RTNSTVTrainer:
         self.flat.zero_grad()
         self.dp.begin()
         out = self.losses(frames, flow, mask)
-        out["loss"].backward()
-        gscale = self.dp.finish()
-        self.step_count += 1
-        self.flat.adam(self.step_count, self.lr, self.betas, self.eps, gscale)
+        backward_and_adam(self, out["loss"])
         return {k: v.detach() for k, v in out.items()}
