@@ -53,6 +53,11 @@ const char* vst_build_id(void);
  * VST_GEMM_KBLOCK may be or-ed into the mode of a conv pack + GEMM pair (both must carry it):
  * channel-block-major, tap-minor K order (16 channels x every tap, then the next 16 channels), which
  * keeps each block's re-read source rows L2-resident; the sums then run in a different order.
+ * 3x3 stride-1 convs under VST_GEMM_KBLOCK (bf16x6 / bf16 / fp16) run on the halo-tiled kernel
+ * (the source patch of an output tile staged once per 16-channel block for all nine taps); its
+ * results are bitwise those of the per-tap kernel.  VST_GEMM_PERTAP or-ed into a GEMM call's mode
+ * selects the per-tap kernel instead (an explicit per-call choice for A/B measurement and the
+ * equivalence test; pack entries ignore it).
  * An unknown mode returns VST_EINVAL (-1). */
 #define VST_GEMM_F32 0
 #define VST_GEMM_BF16X3 1
@@ -60,6 +65,7 @@ const char* vst_build_id(void);
 #define VST_GEMM_BF16X6 3
 #define VST_GEMM_F16 4
 #define VST_GEMM_KBLOCK 16
+#define VST_GEMM_PERTAP 32
 
 /* ---- convolution (implicit GEMM on MFMA, arithmetic per the `mode` argument) ---------------
  * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv

@@ -1,0 +1,162 @@
+"""The halo-tiled 3x3 conv kernel (csrc/conv_halo_kernel.h) against the per-tap kernel and fp64.
+
+Every 3x3 stride-1 conv / data gradient in the channel-blocked K order (VST_GEMM_KBLOCK) runs on the
+halo kernel; VST_GEMM_PERTAP forces the per-tap kernel for the same call.  Both sum the same k-tiles
+in the same order with the same MFMA sequence, so their outputs must be BITWISE equal -- for every
+border rule (reflect / zero forward, transposed data gradient with and without the gathered ReLU
+mask, the padded-grid data gradient with its border side buffer), epilogue and ragged tile edge.
+The shapes are the training paths' 3x3 layers at reduced size (VGG16 / VGG19 64..512 channels,
+ReCoNet residual 192, AdaAttN decoder 256 / 128 / 64) plus ragged grids."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vst._lib import lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF16, BF16X6, F16 = 2, 3, 4
+KBLOCK, PERTAP = 16, 32
+GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM = 1, 2, 8, 16
+
+
+def _dims(M, K):
+    mp, kp = ctypes.c_int(), ctypes.c_int()
+    assert lib.vst_conv_pack_dims(M, K, ctypes.byref(mp), ctypes.byref(kp)) == 0
+    return mp.value, kp.value
+
+
+def _pack(w, mode, transposed=False):
+    Cout, Cin, KH, KW = w.shape
+    M = Cin if transposed else Cout
+    Mpad, Kpad = _dims(M, KH * KW * (Cout if transposed else Cin))
+    n = Mpad * Kpad * 3 // 2 if (mode & 7) == BF16X6 else Mpad * Kpad
+    p = torch.empty(n, device=DEV)
+    lib.vst_pack_weight(w.data_ptr(), p.data_ptr(), Cout, Cin, KH, KW, int(transposed), 0, Mpad, Kpad, mode,
+                        torch.cuda.current_stream().cuda_stream)
+    return p
+
+
+def _conv(src, wp, M, Ho, Wo, gmode, pad, mode, epi=0, bias=None, mask=None, gmask=None, out=None):
+    N, Cs, Hs, Ws = src.shape
+    if out is None:
+        out = torch.full((N, M, Ho, Wo), float("nan"), device=DEV)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    lib.vst_conv_gemm_padx(src.data_ptr(), wp.data_ptr(), P(bias), P(mask), out.data_ptr(), N, Cs, Hs, Ws, M, 9 * Cs,
+                           Ho, Wo, 3, 3, gmode, 1, pad, pad, 1, epi, 0, None, P(gmask), mode,
+                           torch.cuda.current_stream().cuda_stream)
+    return out
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV)
+
+
+MODES = [BF16X6, F16, BF16]
+# (N, Cin, H, W, Cout): VGG layers, ReCoNet residual, AdaAttN decoder, ragged tiles
+SHAPES = [(2, 64, 37, 70, 64), (1, 128, 16, 64, 128), (2, 192, 20, 36, 192), (1, 256, 9, 40, 256),
+          (1, 64, 12, 33, 512), (1, 32, 7, 31, 256), (2, 16, 5, 3, 64), (1, 256, 8, 16, 128)]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("pad_mode", ["reflect", "zero"])
+def test_halo_forward_bitwise(mode, shape, pad_mode):
+    N, Cin, H, W, Cout = shape
+    if pad_mode == "reflect" and min(H, W) < 2:
+        pytest.skip("reflect pad needs 2 pixels")
+    x = _rand(N, Cin, H, W, seed=1, scale=3.0)
+    w = _rand(Cout, Cin, 3, 3, seed=2, scale=0.05)
+    b = _rand(Cout, seed=3)
+    m = mode | KBLOCK
+    wp = _pack(w, m)
+    gm = GM_REFLECT if pad_mode == "reflect" else GM_ZERO
+    epi = EPI_BIAS | (EPI_RELU if pad_mode == "zero" else 0)
+    halo = _conv(x, wp, Cout, H, W, gm, 1, m, epi, bias=b)
+    ref = _conv(x, wp, Cout, H, W, gm, 1, m | PERTAP, epi, bias=b)
+    torch.cuda.synchronize()
+    assert torch.equal(halo, ref), float((halo - ref).abs().max())
+    # and the conv itself, against fp64
+    xp = F.pad(x.double(), (1, 1, 1, 1), mode="reflect" if pad_mode == "reflect" else "constant")
+    y = F.conv2d(xp, w.double(), b.double())
+    if pad_mode == "zero":
+        y = y.clamp_min(0)
+    err = float((halo.double() - y).abs().max() / y.abs().max())
+    assert err < (2e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", SHAPES[:5])
+@pytest.mark.parametrize("masked", [False, True])
+def test_halo_dgrad_bitwise(mode, shape, masked):
+    """Zero-pad data gradient (VGG): dX = transposed gather over dY, with the ReLU mask of the
+    layer's output gathered onto dY (gmask) and the input-side mask in the epilogue (EPI_MASK)."""
+    N, Cin, H, W, Cout = shape
+    dy = _rand(N, Cout, H, W, seed=4)
+    w = _rand(Cout, Cin, 3, 3, seed=5, scale=0.05)
+    m = mode | KBLOCK
+    wp = _pack(w, m, transposed=True)
+    gmask = _rand(N, Cout, H, W, seed=6) if masked else None
+    dmask = _rand(N, Cin, H, W, seed=7) if masked else None
+    epi = EPI_MASK if masked else 0
+    halo = _conv(dy, wp, Cin, H, W, GM_TRANSPOSED, 1, m, epi, mask=dmask, gmask=gmask)
+    ref = _conv(dy, wp, Cin, H, W, GM_TRANSPOSED, 1, m | PERTAP, epi, mask=dmask, gmask=gmask)
+    torch.cuda.synchronize()
+    assert torch.equal(halo, ref), float((halo - ref).abs().max())
+    g = dy.double() * (gmask > 0).double() if masked else dy.double()
+    dx = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double(), g, padding=1)
+    if masked:
+        dx = dx * (dmask > 0).double()
+    err = float((halo.double() - dx).abs().max() / dx.abs().max())
+    assert err < (2e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+
+
+@pytest.mark.parametrize("mode", [BF16X6, F16])
+@pytest.mark.parametrize("shape", [(2, 192, 20, 36, 192), (1, 64, 11, 45, 64), (1, 128, 6, 9, 128)])
+def test_halo_padout_dgrad_bitwise(mode, shape):
+    """ReCoNet ResidualBlock data gradient (reflect pad 1): the transposed GEMM over the padded grid,
+    interior straight into dx, border into the side buffer (EPI_PADOUT), then vst_fold_border."""
+    N, Cin, H, W, Cout = shape
+    dy = _rand(N, Cout, H, W, seed=8)
+    w = _rand(Cout, Cin, 3, 3, seed=9, scale=0.05)
+    m = mode | KBLOCK
+    wp = _pack(w, m, transposed=True)
+    st = torch.cuda.current_stream().cuda_stream
+    res = []
+    for mm in (m, m | PERTAP):
+        dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
+        border = torch.zeros(N, Cin, H + 2, W + 2, device=DEV)
+        lib.vst_conv_dgrad_padout(dy.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N, Cout, H, W,
+                                  Cin, H, W, 3, 1, mm, st)
+        lib.vst_fold_border(border.data_ptr(), None, dx.data_ptr(), N * Cin, H, W, 1, st)
+        res.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    x = torch.zeros(N, Cin, H, W, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w.double())
+    y.backward(dy.double())
+    err = float((res[0].double() - x.grad).abs().max() / x.grad.abs().max())
+    assert err < (2e-6 if mode == BF16X6 else 2e-3), err
+
+
+def test_halo_accumulate_and_fallbacks():
+    """EPI_ACCUM adds into the output; Cout = 3 / 96 (pack Mpad not a multiple of the halo block)
+    stay on the per-tap kernel and still compute the conv."""
+    x = _rand(1, 64, 10, 40, seed=10)
+    w = _rand(64, 64, 3, 3, seed=11, scale=0.05)
+    m = BF16X6 | KBLOCK
+    wp = _pack(w, m)
+    base = _rand(1, 64, 10, 40, seed=12)
+    a = _conv(x, wp, 64, 10, 40, GM_ZERO, 1, m, EPI_ACCUM, out=base.clone())
+    b = _conv(x, wp, 64, 10, 40, GM_ZERO, 1, m | PERTAP, EPI_ACCUM, out=base.clone())
+    assert torch.equal(a, b)
+    for cout in (3, 96):
+        w2 = _rand(cout, 64, 3, 3, seed=13, scale=0.05)
+        y = _conv(x, _pack(w2, m), cout, 10, 40, GM_REFLECT, 1, m)
+        ref = F.conv2d(F.pad(x.double(), (1, 1, 1, 1), mode="reflect"), w2.double())
+        assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-6

@@ -91,6 +91,98 @@ __device__ __forceinline__ int gather_offset(const ConvParams& P, int oy, int ox
   return (inb || mz == 0) ? off : -1;
 }
 
+// Epilogue of the implicit-GEMM conv kernels (conv_gemm_kernel, conv_halo_kernel): the C/D map of
+// the 32x32 MFMA (col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)); fragment (i, j) holds rows
+// mrow0 + 32i + row and the output pixel pix[j] (linear oy*Wo + ox; -1: outside the output)
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 (&acc)[TM][TN], int n, int mrow0,
+                                              const int (&pix)[TN], int hi) {
+  const int HWo = P.Ho * P.Wo;
+  float* out_n = P.out + (long)n * P.M * HWo;
+  const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
+  if (P.epi & (EPI_PHASE2 | EPI_PADOUT)) {
+    // PHASE2: the 4 consecutive rows of a C-register group are the 4 phases of one channel
+    const bool ph2 = P.epi & EPI_PHASE2;
+    const int Cx = ph2 ? P.M >> 2 : P.M, Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
+    float* dx_n = P.out + (long)n * Cx * P.ph_H * P.ph_W;
+    float* bd_n = P.ph_border + (long)n * Cx * Hp * Wp;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int pp = pix[j];
+      if (pp < 0) continue;
+      const int I = (int)fdiv((uint32_t)pp, P.fd_Wo), J = pp - I * P.Wo;
+      if (!ph2) {  // one padded-grid pixel per column: one interior/border decision for all rows
+        const int y = I - P.ph_pad, x = J - P.ph_pad;
+        const bool in = y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W;
+        float* base = in ? dx_n + (long)y * P.ph_W + x : bd_n + (long)I * Wp + J;
+        const long cstride = in ? (long)P.ph_H * P.ph_W : (long)Hp * Wp;
+        // EPI_MASK: interior values gated by the dx-shaped mask (the border keeps the raw values;
+        // vst_fold_border applies the same mask when it folds them in)
+        const float* mk = (in && (P.epi & EPI_MASK)) ? P.mask + (long)n * Cx * P.ph_H * P.ph_W + (long)y * P.ph_W + x
+                                                      : nullptr;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ci = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (ci < Cx) base[ci * cstride] = (mk && !(mk[ci * cstride] > 0.f)) ? 0.f : acc[i][j][r];
+          }
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int mb = mrow0 + i * 32 + 8 * g + 4 * hi;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ci = ph2 ? mb >> 2 : mb + r;
+            const int u = ph2 ? 2 * I + (r >> 1) : I, v = ph2 ? 2 * J + (r & 1) : J;
+            if (ci >= Cx) continue;
+            const int y = u - P.ph_pad, x = v - P.ph_pad;
+            const float val = acc[i][j][4 * g + r] + ((P.epi & EPI_BIAS) ? P.bias[ci] : 0.f);
+            if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W)
+              dx_n[((long)ci * P.ph_H + y) * P.ph_W + x] = val;
+            else if (P.ph_border && u < Hp && v < Wp)
+              bd_n[((long)ci * Hp + u) * Wp + v] = val;
+          }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int pp = pix[j];
+    if (pp < 0) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (m >= P.M) continue;
+        float v = acc[i][j][r];
+        if (P.epi & EPI_AFFINE) {
+          const long rm = (long)n * P.M + m;
+          v = (v + (P.ep_ra ? P.ep_ra[rm] : 0.f)) * P.ep_rb[rm] * P.ep_cg[(long)n * HWo + pp] +
+              (P.ep_rd ? P.ep_rd[rm] : 0.f);
+        }
+        if (P.epi & EPI_BIAS) v += P.bias[m];
+        if (P.epi & EPI_RELU) v = fmaxf(v, 0.f);
+        const long o = (long)m * HWo + pp;
+        if (P.epi & EPI_TANH) {
+          const float t = tanhf(v / 255.0f);
+          if (P.aux) P.aux[(long)n * P.M * HWo + o] = t;
+          v = t * 150.0f + 127.5f;
+        }
+        if (P.epi & EPI_MASK) v = mask_n[o] > 0.f ? v : 0.f;
+        if (P.epi & EPI_ACCUM) v += out_n[o];
+        out_n[o] = v;
+      }
+    }
+  }
+}
+
 // float4 slot (row*4 + quad) of A-tile element idx: 8 consecutive lanes take 8 consecutive rows of
 // one quad, so each 8-lane ds_write_b128 group hits 8 distinct 4-bank slots (rows are 20 dwords
 // apart; bank = dword mod 32) -- the plain row-major order put rows r and r+1's quads 0 and 3 on
@@ -478,90 +570,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     if (!(ABL & 16)) __syncthreads();
   }
 
-  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float* out_n = P.out + (long)n * P.M * HWo;
-  const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
-  if (P.epi & (EPI_PHASE2 | EPI_PADOUT)) {
-    // PHASE2: the 4 consecutive rows of a C-register group are the 4 phases of one channel
-    const bool ph2 = P.epi & EPI_PHASE2;
-    const int Cx = ph2 ? P.M >> 2 : P.M, Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
-    float* dx_n = P.out + (long)n * Cx * P.ph_H * P.ph_W;
-    float* bd_n = P.ph_border + (long)n * Cx * Hp * Wp;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int pp = p0 + (wn * TN + j) * 32 + lo;
-      if (pp >= HWo) continue;
-      const int I = (int)fdiv((uint32_t)pp, P.fd_Wo), J = pp - I * P.Wo;
-      if (!ph2) {  // one padded-grid pixel per column: one interior/border decision for all rows
-        const int y = I - P.ph_pad, x = J - P.ph_pad;
-        const bool in = y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W;
-        float* base = in ? dx_n + (long)y * P.ph_W + x : bd_n + (long)I * Wp + J;
-        const long cstride = in ? (long)P.ph_H * P.ph_W : (long)Hp * Wp;
-        // EPI_MASK: interior values gated by the dx-shaped mask (the border keeps the raw values;
-        // vst_fold_border applies the same mask when it folds them in)
-        const float* mk = (in && (P.epi & EPI_MASK)) ? P.mask + (long)n * Cx * P.ph_H * P.ph_W + (long)y * P.ph_W + x
-                                                      : nullptr;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ci = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (ci < Cx) base[ci * cstride] = (mk && !(mk[ci * cstride] > 0.f)) ? 0.f : acc[i][j][r];
-          }
-        continue;
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int mb = m0 + (wm * TM + i) * 32 + 8 * g + 4 * hi;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ci = ph2 ? mb >> 2 : mb + r;
-            const int u = ph2 ? 2 * I + (r >> 1) : I, v = ph2 ? 2 * J + (r & 1) : J;
-            if (ci >= Cx) continue;
-            const int y = u - P.ph_pad, x = v - P.ph_pad;
-            const float val = acc[i][j][4 * g + r] + ((P.epi & EPI_BIAS) ? P.bias[ci] : 0.f);
-            if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W)
-              dx_n[((long)ci * P.ph_H + y) * P.ph_W + x] = val;
-            else if (P.ph_border && u < Hp && v < Wp)
-              bd_n[((long)ci * Hp + u) * Wp + v] = val;
-          }
-        }
-      }
-    }
-    return;
-  }
+  int pix[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int pp = p0 + (wn * TN + j) * 32 + lo;
-    if (pp >= HWo) continue;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (m >= P.M) continue;
-        float v = acc[i][j][r];
-        if (P.epi & EPI_AFFINE) {
-          const long rm = (long)n * P.M + m;
-          v = (v + (P.ep_ra ? P.ep_ra[rm] : 0.f)) * P.ep_rb[rm] * P.ep_cg[(long)n * HWo + pp] +
-              (P.ep_rd ? P.ep_rd[rm] : 0.f);
-        }
-        if (P.epi & EPI_BIAS) v += P.bias[m];
-        if (P.epi & EPI_RELU) v = fmaxf(v, 0.f);
-        const long o = (long)m * HWo + pp;
-        if (P.epi & EPI_TANH) {
-          const float t = tanhf(v / 255.0f);
-          if (P.aux) P.aux[(long)n * P.M * HWo + o] = t;
-          v = t * 150.0f + 127.5f;
-        }
-        if (P.epi & EPI_MASK) v = mask_n[o] > 0.f ? v : 0.f;
-        if (P.epi & EPI_ACCUM) v += out_n[o];
-        out_n[o] = v;
-      }
-    }
+    pix[j] = pp < HWo ? pp : -1;
   }
+  conv_epilogue<TM, TN>(P, acc, n, m0 + wm * TM * 32, pix, hi);
 }
 
 // tile configurations (BM x BN)

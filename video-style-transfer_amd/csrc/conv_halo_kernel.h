@@ -1,0 +1,204 @@
+// 3x3 stride-1 convolution with the input patch staged once per 16-channel block ("halo" tiles).
+//
+// The per-tap implicit GEMM (conv_gemm_kernel) gathers, splits and stores a fresh B tile for every
+// 16-deep k-tile: with the channel-blocked K order (VST_GEMM_KBLOCK) the nine k-tiles of one
+// channel block are the nine taps, i.e. the same source pixels shifted -- each input element is
+// gathered, split into its bf16 pieces and written to LDS nine times, with a barrier per tap.
+// Here a block owns a TH x TW output tile (4 rows x 32 columns = 128 pixels) and, per 16-channel
+// block, stages the (TH+2) x (TW+2) source patch ONCE (gather with the reflect / zero border
+// folded in, optional ReLU mask of the data gradient applied, split, one LDS store per piece); the
+// nine taps then read their B fragments from that patch at shifted positions (compile-time LDS
+// offsets) -- one gather + split + store + barrier per 9 k-tiles instead of per k-tile.  The A
+// operand (packed weights) goes straight from memory into each wave's MFMA registers, one tap
+// ahead (the A-direct scheme of conv_gemm_kernel: one wave per 32 weight rows).
+//
+// The k-tile sequence (channel block major, tap minor) and the per-k-tile MFMA sequence are those of
+// conv_gemm_kernel under VST_GEMM_KBLOCK, so the two kernels produce bitwise-identical results
+// (tests/test_gpu_halo.py).  Covers every 3x3 stride-1 conv on the training paths: VGG16 / VGG19
+// convs (zero pad 1, RC/network.py:9-40, AA/vgg19.py:19-37), ReCoNet / AdaAttN residual and decoder
+// convs (reflect pad 1, RC/network.py:72-75,145-150, AA/network.py:9-33), and their data gradients
+// (the transposed gather over dY, zero pad; RC ResidualBlock's over the padded grid, EPI_PADOUT).
+#pragma once
+#include "conv_gemm_kernel.h"
+
+#ifndef VST_HALO
+#define VST_HALO 1
+#endif
+
+namespace vstk {
+
+constexpr int HTH = 4, HTW = 32;                              // output tile: 4 rows x 32 columns
+constexpr int HPH = HTH + 2, HPW = HTW + 2, HPP = HPH * HPW;  // source patch: 6 x 34 = 204 pixels
+
+// PREC 3: bf16x6 (three bf16 pieces per value); 2 / 4: single bf16 / fp16 product (one piece)
+template <int WM, int MINW, int PREC, bool GM>
+__global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) {
+  static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo kernel: bf16x6, bf16 or fp16 products");
+  constexpr int TM = 1, TN = HTH;    // each wave: 32 weight rows x (4 output rows of 32 pixels)
+  constexpr int NTT = WM * 64;
+  constexpr int BM = WM * 32;
+  constexpr int AW = PREC == 3 ? 24 : 16;  // packed A dwords per (k-tile, row) (vst_common.h apack_store)
+  constexpr int NPC = PREC == 3 ? 3 : 1;   // bf16 pieces per value in the patch
+  constexpr int LS = NPC * 8 + 4;          // LDS dwords per patch pixel (+4 pad: conflict-free b128 reads)
+  constexpr int NTASK = 2 * HPP;           // (patch pixel, channel octet)
+  constexpr int TIT = (NTASK + NTT - 1) / NTT;
+  constexpr int OOR = 0x7ffffff0;
+  __shared__ __attribute__((aligned(16))) float Ps[2][HPP][LS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int lo = lane & 31, hi = lane >> 5;
+  // work order: M tile fastest, then pixel tile, then image (XCD-aware: the M tiles of one pixel
+  // tile share its patch through one L2)
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int rest = __builtin_amdgcn_readfirstlane(wk / gy);
+  const int n = __builtin_amdgcn_readfirstlane(rest / gx);
+  const int m0 = __builtin_amdgcn_readfirstlane((wk - rest * gy) * BM);
+  const int tile = __builtin_amdgcn_readfirstlane(rest - n * gx);
+  const int tiles_x = (P.Wo + HTW - 1) / HTW;
+  const int ty = __builtin_amdgcn_readfirstlane(tile / tiles_x);
+  const int oy0 = ty * HTH, ox0 = (tile - ty * tiles_x) * HTW;
+  // forward: source row oy - pad + kh; data gradient (transposed, stride 1): dY row oy + pad - kh
+  const bool tr = P.gmode == GM_TRANSPOSED;
+  const int y0 = oy0 + (tr ? P.pad - 2 : -P.pad), x0 = ox0 + (tr ? P.pad - 2 : -P.pad);
+
+  const int plane = P.Hs * P.Ws;
+  const long plane_l = (long)plane;
+  const float* src_n = P.src + (long)n * P.Cs * plane_l;
+  const uint32_t src_bytes = (uint32_t)P.Cs * (uint32_t)plane * 4u;
+  const __amdgpu_buffer_rsrc_t srd = uniform_rsrc(src_n, src_bytes);
+  const __amdgpu_buffer_rsrc_t gsrd = uniform_rsrc(GM ? P.gmask + (long)n * P.Cs * plane_l : src_n, src_bytes);
+  const float* A = P.wpack + (long)n * P.a_batch_stride;
+  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(A, (uint32_t)((long)P.Kpad / BK * P.Mpad * AW * 4));
+  const int ad_voff = ((wave * 32 + lo) * AW + 4 * hi) * 4;
+
+  // this thread's patch tasks: pixel q (consecutive lanes -> consecutive pixels of a patch row),
+  // channel octet o; the source offset of channel 8o of the block, or OOR (zero / outside)
+  int t_voff[TIT], t_lds[TIT];
+#pragma unroll
+  for (int it = 0; it < TIT; ++it) {
+    const int t = tid + it * NTT;
+    const int o = t >= HPP ? 1 : 0, q = t - o * HPP;
+    const int py = q / HPW, px = q - py * HPW;
+    int y = y0 + py, x = x0 + px;
+    if (P.gmode == GM_REFLECT) {
+      y = abs(y);
+      y = y >= P.Hs ? 2 * P.Hs - 2 - y : y;
+      x = abs(x);
+      x = x >= P.Ws ? 2 * P.Ws - 2 - x : x;
+    }
+    const bool ok = t < NTASK && (unsigned)y < (unsigned)P.Hs && (unsigned)x < (unsigned)P.Ws;
+    t_voff[it] = ok ? ((8 * o) * plane + y * P.Ws + x) * 4 : OOR;
+    t_lds[it] = t < NTASK ? q * LS + 4 * o : -1;
+  }
+  const int cstep = __builtin_amdgcn_readfirstlane(plane * 4);  // bytes between channels
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
+
+  float rv[TIT][8];
+  float rgv[TIT][GM ? 8 : 1];
+  auto load_patch = [&](int cb) {
+    const int cb_off = __builtin_amdgcn_readfirstlane(cb * 16 * plane * 4);
+#pragma unroll
+    for (int it = 0; it < TIT; ++it)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        rv[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
+        if constexpr (GM)
+          rgv[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
+      }
+  };
+  auto store_patch = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < TIT; ++it) {
+      if (NTASK % NTT != 0 && t_lds[it] < 0) continue;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = GM ? (rgv[it][i] > 0.f ? rv[it][i] : 0.f) : rv[it][i];
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][0][0]) + t_lds[it];
+      if constexpr (PREC == 3) {
+        uint32_t h[4], md[4], l[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split3_bf16x2(v[2 * q], v[2 * q + 1], h[q], md[q], l[q]);
+        *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<u32x4*>(d + 8) = u32x4{md[0], md[1], md[2], md[3]};
+        *reinterpret_cast<u32x4*>(d + 16) = u32x4{l[0], l[1], l[2], l[3]};
+      } else {
+        uint32_t h[4], l[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split2<PREC>(v[2 * q], v[2 * q + 1], h[q], l[q]);
+        *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+      }
+    }
+  };
+  // A fragments of k-tile kt (channel block cb, tap t: kt = 9 cb + t under the blocked K order)
+  bf16x8_t arN[TM][3], arC[TM][3];
+  auto load_a = [&](int kt, bf16x8_t (&ar)[TM][3]) {
+    const int a_soff = __builtin_amdgcn_readfirstlane(((kt * P.Mpad + m0) * AW) * 4);
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc)
+      ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
+  };
+
+  const int ncb = P.Cs / 16;
+  load_patch(0);
+  load_a(0, arC);
+  store_patch(0);
+  __syncthreads();
+  for (int cb = 0; cb < ncb; ++cb) {
+    const int buf = cb & 1;
+    if (cb + 1 < ncb) load_patch(cb + 1);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const int ph = tr ? 2 - kh : kh, pw = tr ? 2 - kw : kw;  // (tr is block-uniform)
+      const int kt_next = t < 8 ? 9 * cb + t + 1 : 9 * (cb + 1);
+      if (t < 8 || cb + 1 < ncb) load_a(kt_next, arN);
+      // B fragments of tap t: output row j of the tile reads patch row j + ph, columns lo + pw
+      const float(*Bt)[LS] = &Ps[buf][ph * HPW + pw];
+      if constexpr (PREC == 3)
+        mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC, const_cast<float(*)[LS]>(Bt), 0, lane, HPW);
+      else
+        mfma_single_ktile_ra<TM, TN, PREC, LS>(acc, arC, const_cast<float(*)[LS]>(Bt), 0, lane, HPW);
+#pragma unroll
+      for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+    }
+    if (cb + 1 < ncb) store_patch(buf ^ 1);
+    __syncthreads();
+  }
+
+  int pix[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int oy = oy0 + j, ox = ox0 + lo;
+    pix[j] = (oy < P.Ho && ox < P.Wo) ? oy * P.Wo + ox : -1;
+  }
+  conv_epilogue<TM, TN>(P, acc, n, m0 + wave * 32, pix, hi);
+}
+
+// A-direct block sizes: WM waves of 32 weight rows (64 / 128 / 192 / 256 rows)
+template <int PR, bool GM>
+void launch_halo(int wm, dim3 grid, hipStream_t st, const ConvParams& P) {
+  switch (wm) {
+    case 2: conv_halo_kernel<2, 3, PR, GM><<<grid, 128, 0, st>>>(P); break;
+    case 4: conv_halo_kernel<4, 3, PR, GM><<<grid, 256, 0, st>>>(P); break;
+    case 6: conv_halo_kernel<6, 2, PR, GM><<<grid, 384, 0, st>>>(P); break;
+    default: conv_halo_kernel<8, 2, PR, GM><<<grid, 512, 0, st>>>(P); break;
+  }
+}
+
+template <int PR>
+void launch_halo_prec(bool gm, int wm, dim3 grid, hipStream_t st, const ConvParams& P) {
+  gm ? launch_halo<PR, true>(wm, grid, st, P) : launch_halo<PR, false>(wm, grid, st, P);
+}
+
+extern template void launch_halo_prec<2>(bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_halo_prec<3>(bool, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_halo_prec<4>(bool, int, dim3, hipStream_t, const ConvParams&);
+
+}  // namespace vstk

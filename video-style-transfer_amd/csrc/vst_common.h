@@ -65,10 +65,10 @@ static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // GEMM arithmetic mode: a per-call argument of every GEMM / pack entry (vst_hip.h VST_GEMM_*, plus
 // the VST_GEMM_KBLOCK K-order flag); the library keeps no mode state
-static inline int vst_mode_arith(int mode) { return mode & ~VST_GEMM_KBLOCK; }
+static inline int vst_mode_arith(int mode) { return mode & 7; }
 static inline bool vst_mode_ok(int mode) {
   const int a = vst_mode_arith(mode);
-  return (mode & ~(VST_GEMM_KBLOCK | 7)) == 0 &&
+  return (mode & ~(VST_GEMM_KBLOCK | VST_GEMM_PERTAP | 7)) == 0 &&
          (a == VST_GEMM_F32 || a == VST_GEMM_BF16X3 || a == VST_GEMM_BF16 || a == VST_GEMM_BF16X6 ||
           a == VST_GEMM_F16);
 }
@@ -284,12 +284,12 @@ __device__ __forceinline__ void mfma_bf16x6_ktile(f32x16 (&acc)[TM][TN], float (
 // straight from the packed weights) and B from LDS
 template <int TM, int TN, int LS>
 __device__ __forceinline__ void mfma_bf16x6_ktile_ra(f32x16 (&acc)[TM][TN], const bf16x8_t (&ar)[TM][3],
-                                                     float (*B)[LS], int b0, int lane) {
+                                                     float (*B)[LS], int b0, int lane, int jstride = 32) {
   const int r = lane & 31, h = lane >> 5;
   bf16x8_t bh[TN], bm[TN], bl[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const float* p = &B[b0 + j * 32 + r][4 * h];
+    const float* p = &B[b0 + j * jstride + r][4 * h];
     bh[j] = *reinterpret_cast<const bf16x8_t*>(p);
     bm[j] = *reinterpret_cast<const bf16x8_t*>(p + 8);
     bl[j] = *reinterpret_cast<const bf16x8_t*>(p + 16);
@@ -312,11 +312,11 @@ __device__ __forceinline__ void mfma_bf16x6_ktile_ra(f32x16 (&acc)[TM][TN], cons
 // from the packed weights: the hi piece of each 32-row fragment) and B from LDS
 template <int TM, int TN, int PREC, int LS>
 __device__ __forceinline__ void mfma_single_ktile_ra(f32x16 (&acc)[TM][TN], const bf16x8_t (&ar)[TM][3],
-                                                     float (*B)[LS], int b0, int lane) {
+                                                     float (*B)[LS], int b0, int lane, int jstride = 32) {
   const int r = lane & 31, h = lane >> 5;
   bf16x8_t bh[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bh[j] = *reinterpret_cast<const bf16x8_t*>(&B[b0 + j * 32 + r][4 * h]);
+  for (int j = 0; j < TN; ++j) bh[j] = *reinterpret_cast<const bf16x8_t*>(&B[b0 + j * jstride + r][4 * h]);
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
