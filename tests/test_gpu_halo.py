@@ -87,7 +87,7 @@ def test_halo_forward_bitwise(mode, shape, pad_mode):
     if pad_mode == "zero":
         y = y.clamp_min(0)
     err = float((halo.double() - y).abs().max() / y.abs().max())
-    assert err < (2e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -113,7 +113,7 @@ def test_halo_dgrad_bitwise(mode, shape, masked):
     if masked:
         dx = dx * (dmask > 0).double()
     err = float((halo.double() - dx).abs().max() / dx.abs().max())
-    assert err < (2e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
 
 
 @pytest.mark.parametrize("mode", [BF16X6, F16])
