@@ -137,11 +137,11 @@ def test_halo_padout_dgrad_bitwise(mode, shape):
         res.append(dx)
     torch.cuda.synchronize()
     assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
-    x = torch.zeros(N, Cin, H, W, dtype=torch.float64, requires_grad=True)
+    x = torch.zeros(N, Cin, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
     y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w.double())
     y.backward(dy.double())
     err = float((res[0].double() - x.grad).abs().max() / x.grad.abs().max())
-    assert err < (2e-6 if mode == BF16X6 else 2e-3), err
+    assert err < (5e-6 if mode == BF16X6 else 2e-3), err
 
 
 def test_halo_accumulate_and_fallbacks():
