@@ -64,11 +64,13 @@ def main():
     cols = [(p, lib, m) for p, lib in zip(paths, libs) for m in MODES]
     dev = "cuda"
     st = torch.cuda.current_stream().cuda_stream
-    only = None
+    only = os.environ.get("BENCH_ONLY")  # substring of the shape names to run
     results = {(p, m, s[0]): [] for p in paths for m in MODES for s in SHAPES}
     bufs = {}
     for s in SHAPES:
         name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
+        if only and only not in name:
+            continue
         src = torch.randn(N, Cs, Hs, Ws, device=dev)
         out = torch.empty(N, M, Ho, Wo, device=dev)
         bufs[name] = (src, out)
@@ -101,6 +103,8 @@ def main():
     print(hdr)
     tot = {(p, m): 0.0 for p, _, m in cols}
     for s in SHAPES:
+        if only and only not in s[0]:
+            continue
         line = s[0].ljust(16)
         for p, _, m in cols:
             ms = statistics.median(results[(p, m, s[0])])
