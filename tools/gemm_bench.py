@@ -64,12 +64,13 @@ def main():
     cols = [(p, lib, m) for p, lib in zip(paths, libs) for m in MODES]
     dev = "cuda"
     st = torch.cuda.current_stream().cuda_stream
-    only = os.environ.get("BENCH_ONLY")  # substring of the shape names to run
+    only = os.environ.get("BENCH_ONLY")  # comma-separated substrings of the shape names to run
+    sel = (lambda nm: any(o in nm for o in only.split(","))) if only else (lambda nm: True)
     results = {(p, m, s[0]): [] for p in paths for m in MODES for s in SHAPES}
     bufs = {}
     for s in SHAPES:
         name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
-        if only and only not in name:
+        if not sel(name):
             continue
         src = torch.randn(N, Cs, Hs, Ws, device=dev)
         out = torch.empty(N, M, Ho, Wo, device=dev)
@@ -78,7 +79,7 @@ def main():
         for p, lib, MODE in cols:
             for s in SHAPES:
                 name, N, Cs, Hs, Ws, M, KH, KW, Ho, Wo, gm, stride, pad, up, fl = s
-                if only and only not in name:
+                if not sel(name):
                     continue
                 src, out = bufs[name]
                 mp, kp = ctypes.c_int(), ctypes.c_int()
@@ -103,7 +104,7 @@ def main():
     print(hdr)
     tot = {(p, m): 0.0 for p, _, m in cols}
     for s in SHAPES:
-        if only and only not in s[0]:
+        if not sel(s[0]):
             continue
         line = s[0].ljust(16)
         for p, _, m in cols:

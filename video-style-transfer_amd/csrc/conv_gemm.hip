@@ -348,16 +348,16 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   // 3x3 stride-1 convs in the channel-blocked K order: the halo-tiled kernel (conv_halo_kernel.h),
   // one A-direct wave per 32 weight rows -- 2 / 4 / 6 / 8 waves as the per-tap kernel's blocks
   const int am = vst_mode_arith(mode);
-  const int hwm = M <= 64 ? 2 : (M % 256 == 0 ? 8 : (M % 192 == 0 && M % 128 != 0 ? 6 : 4));
-  // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's rows must divide it)
+  // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
   const int pack_bm = cfg_bm(select_cfg(M)), pack_mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
-  const bool halo = VST_HALO && pack_mpad % (32 * hwm) == 0 && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 && KW == 3 &&
-                    stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
+  const int hcfg = halo_cfg(M, pack_mpad, am == VST_GEMM_BF16X6);
+  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 &&
+                    KW == 3 && stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
                     (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED) &&
                     !(epi & (EPI_AFFINE | EPI_PHASE2)) &&
                     (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
   if (halo) {
-    const int wm = hwm, bm = 32 * wm;
+    const int bm = 32 * halo_wm(hcfg), th = 4 * halo_wn(hcfg);
     P.Mpad = pack_mpad;
     P.K = K;
     P.Kpad = (K + BK - 1) / BK * BK;
@@ -376,13 +376,13 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     P.fd_Cs = make_fastdiv(Cs);
     P.fd_KW = make_fastdiv(KW);
     P.kb = 1;
-    const int tiles = ((Wo + HTW - 1) / HTW) * ((Ho + HTH - 1) / HTH);
+    const int tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
     dim3 grid(tiles, P.Mpad / bm, N);
     hipStream_t st = (hipStream_t)stream;
     const bool gm = gmask != nullptr;
-    if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, wm, grid, st, P);
-    else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, wm, grid, st, P);
-    else launch_halo_prec<2>(gm, wm, grid, st, P);
+    if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, hcfg, grid, st, P);
+    else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, hcfg, grid, st, P);
+    else launch_halo_prec<2>(gm, hcfg, grid, st, P);
     return vst_launch_status();
   }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);

@@ -27,27 +27,33 @@
 
 namespace vstk {
 
-constexpr int HTH = 4, HTW = 32;                              // output tile: 4 rows x 32 columns
-constexpr int HPH = HTH + 2, HPW = HTW + 2, HPP = HPH * HPW;  // source patch: 6 x 34 = 204 pixels
+constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave covers 4 rows of it
 
-// PREC 3: bf16x6 (three bf16 pieces per value); 2 / 4: single bf16 / fp16 product (one piece)
-template <int WM, int MINW, int PREC, bool GM>
-__global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) {
+// Block = WM x WN waves: wave (wm, wn) computes weight rows m0 + 32 wm .. +31 for output rows
+// oy0 + 4 wn .. +3 (TN = 4 fragments of 32 pixels), so the tile is TH = 4 WN rows x 32 columns and
+// the patch (TH + 2) x 34 pixels.  DB: double-buffered patch (the next channel block's stores need
+// no second barrier) or one buffer (half the LDS: more blocks per CU, two barriers per block).
+// PREC 3: bf16x6 (three bf16 pieces per value); 2 / 4: single bf16 / fp16 product (one piece).
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB>
+__global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo kernel: bf16x6, bf16 or fp16 products");
-  constexpr int TM = 1, TN = HTH;    // each wave: 32 weight rows x (4 output rows of 32 pixels)
-  constexpr int NTT = WM * 64;
+  constexpr int TM = 1, TN = 4;
+  constexpr int TH = 4 * WN, HPH = TH + 2, HPW = HTW + 2, HPP = HPH * HPW;
+  constexpr int NTT = WM * WN * 64;
   constexpr int BM = WM * 32;
   constexpr int AW = PREC == 3 ? 24 : 16;  // packed A dwords per (k-tile, row) (vst_common.h apack_store)
   constexpr int NPC = PREC == 3 ? 3 : 1;   // bf16 pieces per value in the patch
   constexpr int LS = NPC * 8 + 4;          // LDS dwords per patch pixel (+4 pad: conflict-free b128 reads)
   constexpr int NTASK = 2 * HPP;           // (patch pixel, channel octet)
   constexpr int TIT = (NTASK + NTT - 1) / NTT;
+  constexpr int NBUF = DB ? 2 : 1;
   constexpr int OOR = 0x7ffffff0;
-  __shared__ __attribute__((aligned(16))) float Ps[2][HPP][LS];
+  __shared__ __attribute__((aligned(16))) float Ps[NBUF][HPP][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int lo = lane & 31, hi = lane >> 5;
+  const int wm = wave % WM, wn = wave / WM;
   // work order: M tile fastest, then pixel tile, then image (XCD-aware: the M tiles of one pixel
   // tile share its patch through one L2)
   const int gx = gridDim.x, gy = gridDim.y;
@@ -58,7 +64,7 @@ __global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) 
   const int tile = __builtin_amdgcn_readfirstlane(rest - n * gx);
   const int tiles_x = (P.Wo + HTW - 1) / HTW;
   const int ty = __builtin_amdgcn_readfirstlane(tile / tiles_x);
-  const int oy0 = ty * HTH, ox0 = (tile - ty * tiles_x) * HTW;
+  const int oy0 = ty * TH, ox0 = (tile - ty * tiles_x) * HTW;
   // forward: source row oy - pad + kh; data gradient (transposed, stride 1): dY row oy + pad - kh
   const bool tr = P.gmode == GM_TRANSPOSED;
   const int y0 = oy0 + (tr ? P.pad - 2 : -P.pad), x0 = ox0 + (tr ? P.pad - 2 : -P.pad);
@@ -71,7 +77,7 @@ __global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) 
   const __amdgpu_buffer_rsrc_t gsrd = uniform_rsrc(GM ? P.gmask + (long)n * P.Cs * plane_l : src_n, src_bytes);
   const float* A = P.wpack + (long)n * P.a_batch_stride;
   const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(A, (uint32_t)((long)P.Kpad / BK * P.Mpad * AW * 4));
-  const int ad_voff = ((wave * 32 + lo) * AW + 4 * hi) * 4;
+  const int ad_voff = ((wm * 32 + lo) * AW + 4 * hi) * 4;
 
   // this thread's patch tasks: pixel q (consecutive lanes -> consecutive pixels of a patch row),
   // channel octet o; the source offset of channel 8o of the block, or OOR (zero / outside)
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) 
   store_patch(0);
   __syncthreads();
   for (int cb = 0; cb < ncb; ++cb) {
-    const int buf = cb & 1;
+    const int buf = DB ? (cb & 1) : 0;
     if (cb + 1 < ncb) load_patch(cb + 1);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -159,8 +165,9 @@ __global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) 
       const int ph = tr ? 2 - kh : kh, pw = tr ? 2 - kw : kw;  // (tr is block-uniform)
       const int kt_next = t < 8 ? 9 * cb + t + 1 : 9 * (cb + 1);
       if (t < 8 || cb + 1 < ncb) load_a(kt_next, arN);
-      // B fragments of tap t: output row j of the tile reads patch row j + ph, columns lo + pw
-      const float(*Bt)[LS] = &Ps[buf][ph * HPW + pw];
+      // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
+      // columns lo + pw
+      const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
       if constexpr (PREC == 3)
         mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC, const_cast<float(*)[LS]>(Bt), 0, lane, HPW);
       else
@@ -168,33 +175,71 @@ __global__ __launch_bounds__(WM * 64, MINW) void conv_halo_kernel(ConvParams P) 
 #pragma unroll
       for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
     }
-    if (cb + 1 < ncb) store_patch(buf ^ 1);
+    if (cb + 1 < ncb) {
+      if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
+      store_patch(DB ? buf ^ 1 : 0);
+    }
     __syncthreads();
   }
 
   int pix[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int oy = oy0 + j, ox = ox0 + lo;
+    const int oy = oy0 + 4 * wn + j, ox = ox0 + lo;
     pix[j] = (oy < P.Ho && ox < P.Wo) ? oy * P.Wo + ox : -1;
   }
-  conv_epilogue<TM, TN>(P, acc, n, m0 + wave * 32, pix, hi);
+  conv_epilogue<TM, TN>(P, acc, n, m0 + wm * 32, pix, hi);
 }
 
-// A-direct block sizes: WM waves of 32 weight rows (64 / 128 / 192 / 256 rows)
+// Block shape per layer width (M = weight rows): WM x WN waves, M tile 32 WM.  The packed A carries
+// vst_conv_pack_dims' Mpad, which the M tile must divide (halo_cfg returns 0 otherwise).
+// Measured per layer shape (tools/gemm_bench.py, one box, bf16x6 / fp16; profiles/r04_halo_shapes.txt):
+//   M = 64  (VGG conv1_x, 256x512): 2x2 one buffer 746 us < 2x2 double 878 < 2x1 902 < per-tap 1071
+//   M = 128 (VGG conv2_x): 4x1 619-664 < 4x2 685 < per-tap 751
+//   M = 192 (ReCoNet residual, 64x128): bf16x6 per-tap 413 / 531 (dgrad) < halo 3x2 436 / 594 and
+//           6x1 439 / 605 -- the per-tap LDS-A tile stays; fp16 halo 134 < per-tap 199
+//   M = 256-multiples (VGG conv3_x / conv4_x): 8x1, 268-274 TF/s vs per-tap 233-245
+#ifndef VST_HALO_M64
+#define VST_HALO_M64 3  // 1: 2x1 double-buffered; 2: 2x2 double-buffered; 3: 2x2 one buffer
+#endif
+#ifndef VST_HALO_M128
+#define VST_HALO_M128 1  // 1: 4x1; 2: 4x2
+#endif
+#ifndef VST_HALO_M192
+#define VST_HALO_M192 0  // 0: per-tap kernel for bf16x6; 1: 6x1; 2: 3x2 (two 96-row M tiles)
+#endif
+enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1 };
+inline int halo_wm(int c) { return c <= H2x2S ? 2 : (c <= H4x2 ? 4 : (c == H6x1 ? 6 : (c == H3x2 ? 3 : 8))); }
+inline int halo_wn(int c) { return (c == H2x2 || c == H2x2S || c == H4x2 || c == H3x2) ? 2 : 1; }
+// 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster there)
+inline int halo_cfg(int M, int pack_mpad, bool bf16x6) {
+  int c;
+  if (M <= 64) c = VST_HALO_M64 == 1 ? H2x1 : (VST_HALO_M64 == 2 ? H2x2 : H2x2S);
+  else if (M % 256 == 0) c = H8x1;
+  else if (M % 192 == 0 && M % 128 != 0) {
+    if (bf16x6 && VST_HALO_M192 == 0) return 0;
+    c = VST_HALO_M192 == 1 ? H6x1 : H3x2;
+  } else c = VST_HALO_M128 == 1 ? H4x1 : H4x2;
+  return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
+}
+
 template <int PR, bool GM>
-void launch_halo(int wm, dim3 grid, hipStream_t st, const ConvParams& P) {
-  switch (wm) {
-    case 2: conv_halo_kernel<2, 3, PR, GM><<<grid, 128, 0, st>>>(P); break;
-    case 4: conv_halo_kernel<4, 3, PR, GM><<<grid, 256, 0, st>>>(P); break;
-    case 6: conv_halo_kernel<6, 2, PR, GM><<<grid, 384, 0, st>>>(P); break;
-    default: conv_halo_kernel<8, 2, PR, GM><<<grid, 512, 0, st>>>(P); break;
+void launch_halo(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
+  switch (c) {
+    case H2x1: conv_halo_kernel<2, 1, 3, PR, GM, true><<<grid, 128, 0, st>>>(P); break;
+    case H2x2: conv_halo_kernel<2, 2, 2, PR, GM, true><<<grid, 256, 0, st>>>(P); break;
+    case H2x2S: conv_halo_kernel<2, 2, 3, PR, GM, false><<<grid, 256, 0, st>>>(P); break;
+    case H4x1: conv_halo_kernel<4, 1, 3, PR, GM, true><<<grid, 256, 0, st>>>(P); break;
+    case H4x2: conv_halo_kernel<4, 2, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
+    case H6x1: conv_halo_kernel<6, 1, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
+    case H3x2: conv_halo_kernel<3, 2, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
+    default: conv_halo_kernel<8, 1, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
   }
 }
 
 template <int PR>
-void launch_halo_prec(bool gm, int wm, dim3 grid, hipStream_t st, const ConvParams& P) {
-  gm ? launch_halo<PR, true>(wm, grid, st, P) : launch_halo<PR, false>(wm, grid, st, P);
+void launch_halo_prec(bool gm, int c, dim3 grid, hipStream_t st, const ConvParams& P) {
+  gm ? launch_halo<PR, true>(c, grid, st, P) : launch_halo<PR, false>(c, grid, st, P);
 }
 
 extern template void launch_halo_prec<2>(bool, int, dim3, hipStream_t, const ConvParams&);
