@@ -206,11 +206,18 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #define VST_HALO_M128 1  // 1: 4x1; 2: 4x2
 #endif
 #ifndef VST_HALO_M192
-#define VST_HALO_M192 0  // 0: per-tap kernel for bf16x6; 1: 6x1; 2: 3x2 (two 96-row M tiles)
+#define VST_HALO_M192 0  // 0: per-tap kernel for bf16x6; 1: 6x1; 2: 3x2 (two 96-row M tiles); 3: 2x4
+                        // one buffer (64-row M tiles, 16-row pixel tiles); 4: 3x1 one buffer; 5: 3x2 one buffer
 #endif
-enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1 };
-inline int halo_wm(int c) { return c <= H2x2S ? 2 : (c <= H4x2 ? 4 : (c == H6x1 ? 6 : (c == H3x2 ? 3 : 8))); }
-inline int halo_wn(int c) { return (c == H2x2 || c == H2x2S || c == H4x2 || c == H3x2) ? 2 : 1; }
+enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S };
+inline int halo_wm(int c) {
+  const int wm[] = {0, 2, 2, 2, 4, 4, 6, 3, 8, 2, 3, 3};
+  return wm[c];
+}
+inline int halo_wn(int c) {
+  const int wn[] = {0, 1, 2, 2, 1, 2, 1, 2, 1, 4, 1, 2};
+  return wn[c];
+}
 // 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster there)
 inline int halo_cfg(int M, int pack_mpad, bool bf16x6) {
   int c;
@@ -218,7 +225,8 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6) {
   else if (M % 256 == 0) c = H8x1;
   else if (M % 192 == 0 && M % 128 != 0) {
     if (bf16x6 && VST_HALO_M192 == 0) return 0;
-    c = VST_HALO_M192 == 1 ? H6x1 : H3x2;
+    const int m192[] = {H3x2, H6x1, H3x2, H2x4S, H3x1S, H3x2S};
+    c = m192[VST_HALO_M192];
   } else c = VST_HALO_M128 == 1 ? H4x1 : H4x2;
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
 }
@@ -233,6 +241,9 @@ void launch_halo(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
     case H4x2: conv_halo_kernel<4, 2, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
     case H6x1: conv_halo_kernel<6, 1, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
     case H3x2: conv_halo_kernel<3, 2, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
+    case H2x4S: conv_halo_kernel<2, 4, 4, PR, GM, false><<<grid, 512, 0, st>>>(P); break;
+    case H3x1S: conv_halo_kernel<3, 1, 4, PR, GM, false><<<grid, 192, 0, st>>>(P); break;
+    case H3x2S: conv_halo_kernel<3, 2, 3, PR, GM, false><<<grid, 384, 0, st>>>(P); break;
     default: conv_halo_kernel<8, 1, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
   }
 }
