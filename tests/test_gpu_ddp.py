@@ -1,0 +1,111 @@
+"""Data parallelism through the product's HIP backward on the GPU box: two ranks on
+cuda:0 (gloo carries the collectives; RCCL needs one GPU per rank), each running the real
+`ReCoNetTrainer.step` / `AdaAttNTrainer.step` on its own shard.  The HIP Functions write weight
+gradients straight into the flat gradient and return None, so this is the path where the
+post-accumulate-grad bucket hooks must still fire (vst/reconet/dist.py): every bucket must be
+all-reduced during backward, both replicas must end identical, and the update must equal one Adam
+step on the mean of the two shards' single-process HIP gradients.  (tests/test_ddp.py covers the
+same host logic on CPU with the oracle's forward; 8-GPU RCCL runs are the driver's.)"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trainer(kind):
+    import oracle
+    from oracle import shapes
+
+    def seeded(m, spec, seed):
+        P = oracle.seeded_params(spec, seed)
+        with torch.no_grad():
+            for n, p in m.named_parameters():
+                p.copy_(P[n])
+        return m.cuda()
+
+    if kind == "reconet":
+        from vst.reconet.network import ReCoNet, Vgg16
+        from vst.reconet.train import ReCoNetTrainer
+        from vst.synthetic import style_image
+
+        return ReCoNetTrainer(seeded(ReCoNet(), shapes.reconet(), 1), seeded(Vgg16(), shapes.vgg16(), 2),
+                              style_image(3, 32, 64).cuda())
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+
+    return AdaAttNTrainer(seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), 1),
+                          seeded(VGG19(), shapes.vgg19(), 2), activation="cosine")
+
+
+def _batch(kind, rank):
+    from vst.reconet.dist import shard_seed
+    from vst.synthetic import content_style_batch, frame_pair_batch
+
+    if kind == "reconet":
+        img1, img2, flow, mask = frame_pair_batch(shard_seed(40, rank), 1, 32, 64)
+        return torch.stack([img1, img2]).cuda(), flow.cuda(), mask.cuda()
+    c1, c2, s = content_style_batch(shard_seed(50, rank), 1, 32, 64)
+    return (torch.stack([c1, c2, s]).cuda(),)
+
+
+def _worker(rank, world, port, outdir, kind):
+    sys.path[:0] = [REPO, os.path.join(REPO, "video-style-transfer_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = _trainer(kind)
+    tr.step(*_batch(kind, rank))
+    torch.cuda.synchronize()
+    st = tr.dp.stats()
+    np.save(os.path.join(outdir, f"p{rank}.npy"), tr.flat.p.cpu().numpy())
+    np.save(os.path.join(outdir, f"g{rank}.npy"), tr.flat.g.cpu().numpy())
+    np.save(os.path.join(outdir, f"s{rank}.npy"), np.array([st["buckets"], st["launched_in_backward"]]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["reconet", "adaattn"])
+def test_hip_dp_step_equals_adam_on_mean_shard_gradient(tmp_path, kind):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
+    assert np.array_equal(p0, p1), "replicas diverged"
+    nb, in_bwd = np.load(tmp_path / "s0.npy")
+    assert nb > 1 and in_bwd == nb, f"{in_bwd} of {nb} buckets all-reduced during backward"
+    # the two shards' gradients in ONE process, no process group (the reference's per-shard step)
+    gs = []
+    for r in range(world):
+        tr = _trainer(kind)
+        tr.flat.zero_grad()
+        out = tr.losses(*_batch(kind, r))
+        out["loss"].backward()
+        torch.cuda.synchronize()
+        gs.append(tr.flat.g.clone())
+    gsum = (gs[0] + gs[1]).cpu().numpy()
+    g_dp = np.load(tmp_path / "g0.npy")
+    assert np.abs(g_dp - gsum).max() <= 1e-6 * np.abs(gsum).max()
+    ref = _trainer(kind)
+    ref.flat.g.copy_(gs[0] + gs[1])
+    ref.flat.adam(1, ref.lr, ref.betas, ref.eps, 1.0 / world)
+    expect = ref.flat.p.cpu().numpy()
+    d = float(np.abs(p0 - expect).max())
+    print(f"{kind}: {nb} buckets, all in backward; |p_dp - adam(mean shard grad)| max {d:.2e}")
+    assert d < 1e-6
+    assert not np.allclose(gs[0].cpu().numpy(), gs[1].cpu().numpy())

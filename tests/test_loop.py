@@ -47,3 +47,33 @@ def test_fit_epochs_batches_and_checkpoints(tmp_path):
     for e in (1, 2):
         sd = torch.load(tmp_path / f"m_epoch_{e}.pth", weights_only=True)
         assert sorted(sd) == ["bias", "weight"]
+
+
+class _StubAdaAttN:
+    """an AdaAttN-style trainer: consumes (content1, content2, style) triples through step_batch"""
+
+    def __init__(self):
+        self.model = torch.nn.Conv2d(3, 3, 1)
+        self.seen = []
+
+    def step_batch(self, batch):
+        c1, c2, s = batch
+        self.seen.append(tuple(torch.stack([c1, c2, s]).shape))
+        n = float(len(self.seen))
+        return {"loss": torch.tensor(n), "loss_gs": torch.tensor(n / 4), "loss_lf": torch.tensor(n / 4),
+                "loss_is": torch.tensor(n / 2)}
+
+
+def test_fit_adaattn_triples_and_reference_checkpoint_name(tmp_path):
+    from vst.reconet.loop import AA_VIDEO_CHECKPOINT
+
+    B, H, W = 4, 8, 16
+    triple = tuple(torch.zeros(B, 3, H, W) for _ in range(3))
+    tr = _StubAdaAttN()
+    log = StepLog(every=2, units_per_step=B)
+    ck = str(tmp_path / AA_VIDEO_CHECKPOINT.replace("./models/", "").format(epoch="{epoch}", batch=B))
+    fit(tr, [triple] * 3, epochs=1, log=log, checkpoint=ck)
+    assert tr.seen == [(3, B, 3, H, W)] * 3
+    assert [r["steps"] for r in log.records] == [2, 1]
+    assert [r["loss_is"] for r in log.records] == [0.75, 1.5]
+    assert (tmp_path / "AdaAttN-video_epoch_1_batchSize_4.pth").exists()

@@ -350,7 +350,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   const int am = vst_mode_arith(mode);
   // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
   const int pack_bm = cfg_bm(select_cfg(M)), pack_mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
-  const int hcfg = halo_cfg(M, pack_mpad, am == VST_GEMM_BF16X6);
+  const int hcfg = halo_cfg(M, pack_mpad, am == VST_GEMM_BF16X6, (epi & EPI_PADOUT) != 0);
   const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 &&
                     KW == 3 && stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
                     (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED) &&

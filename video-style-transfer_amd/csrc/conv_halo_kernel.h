@@ -29,6 +29,43 @@ namespace vstk {
 
 constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave covers 4 rows of it
 
+// One tap of a wave's 32 x 128 tile: the B fragments of output row j (LDS pixel rows jstride apart)
+// stream through a two-deep register ring -- fragment j+1's reads are issued before fragment j's
+// MFMAs -- instead of all TN fragments up front (24 fewer live VGPRs: the 4-wave-per-SIMD budget)
+template <int TN, int PREC, int LS>
+__device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&ar)[1][3], const float (*B)[LS],
+                                         int lane, int jstride) {
+  constexpr int NPC = PREC == 3 ? 3 : 1;
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8_t b[2][3];
+  auto load = [&](int j, bf16x8_t (&d)[3]) {
+    const float* p = &B[j * jstride + r][4 * h];
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc) d[pc] = *reinterpret_cast<const bf16x8_t*>(p + 8 * pc);
+  };
+  load(0, b[0]);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if (j + 1 < TN) load(j + 1, b[(j + 1) & 1]);
+    const bf16x8_t(&c)[3] = b[j & 1];
+    f32x16 a = acc[0][j];
+    if constexpr (PREC == 3) {
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][2], c[0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][1], c[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[2], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][1], c[0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[0], a, 0, 0, 0);
+    } else if constexpr (PREC == 4) {
+      a = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, ar[0][0]), __builtin_bit_cast(f16x8_t, c[0]),
+                                                 a, 0, 0, 0);
+    } else {
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[0], a, 0, 0, 0);
+    }
+    acc[0][j] = a;
+  }
+}
+
 // Block = WM x WN waves: wave (wm, wn) computes weight rows m0 + 32 wm .. +31 for output rows
 // oy0 + 4 wn .. +3 (TN = 4 fragments of 32 pixels), so the tile is TH = 4 WN rows x 32 columns and
 // the patch (TH + 2) x 34 pixels.  DB: double-buffered patch (the next channel block's stores need
@@ -168,10 +205,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
       // columns lo + pw
       const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
-      if constexpr (PREC == 3)
-        mfma_bf16x6_ktile_ra<TM, TN, LS>(acc, arC, const_cast<float(*)[LS]>(Bt), 0, lane, HPW);
-      else
-        mfma_single_ktile_ra<TM, TN, PREC, LS>(acc, arC, const_cast<float(*)[LS]>(Bt), 0, lane, HPW);
+      halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
 #pragma unroll
       for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
     }
@@ -196,56 +230,62 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 // Measured per layer shape (tools/gemm_bench.py, one box, bf16x6 / fp16; profiles/r04_halo_shapes.txt):
 //   M = 64  (VGG conv1_x, 256x512): 2x2 one buffer 746 us < 2x2 double 878 < 2x1 902 < per-tap 1071
 //   M = 128 (VGG conv2_x): 4x1 619-664 < 4x2 685 < per-tap 751
-//   M = 192 (ReCoNet residual, 64x128): bf16x6 per-tap 413 / 531 (dgrad) < halo 3x2 436 / 594 and
-//           6x1 439 / 605 -- the per-tap LDS-A tile stays; fp16 halo 134 < per-tap 199
+//   M = 192 (ReCoNet residual, 64x128): 2x4 one buffer 391 us (fp16 115) < per-tap 447 (LDS-A tile)
+//           < 3x2 415-428, 6x1 428, 3x1 448; the padded-grid data gradient stays per-tap (bf16x6)
 //   M = 256-multiples (VGG conv3_x / conv4_x): 8x1, 268-274 TF/s vs per-tap 233-245
 #ifndef VST_HALO_M64
-#define VST_HALO_M64 3  // 1: 2x1 double-buffered; 2: 2x2 double-buffered; 3: 2x2 one buffer
+#define VST_HALO_M64 3  // block shape of 64-row layers (HaloCfg below)
 #endif
 #ifndef VST_HALO_M128
-#define VST_HALO_M128 1  // 1: 4x1; 2: 4x2
+#define VST_HALO_M128 4
 #endif
 #ifndef VST_HALO_M192
-#define VST_HALO_M192 0  // 0: per-tap kernel for bf16x6; 1: 6x1; 2: 3x2 (two 96-row M tiles); 3: 2x4
-                        // one buffer (64-row M tiles, 16-row pixel tiles); 4: 3x1 one buffer; 5: 3x2 one buffer
+#define VST_HALO_M192 9
 #endif
-enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S };
-inline int halo_wm(int c) {
-  const int wm[] = {0, 2, 2, 2, 4, 4, 6, 3, 8, 2, 3, 3};
-  return wm[c];
-}
-inline int halo_wn(int c) {
-  const int wn[] = {0, 1, 2, 2, 1, 2, 1, 2, 1, 4, 1, 2};
-  return wn[c];
-}
-// 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster there)
-inline int halo_cfg(int M, int pack_mpad, bool bf16x6) {
+#ifndef VST_HALO_M256
+#define VST_HALO_M256 8  // 256-row multiples
+#endif
+#ifndef VST_HALO_SMINW
+#define VST_HALO_SMINW 4  // waves per SIMD the one-buffer tiles' registers must allow
+#endif
+// WM x WN waves (S: one patch buffer)
+enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S, H4x2S };
+constexpr int halo_wm_c(int c) { return c == H2x1 || c == H2x2 || c == H2x2S || c == H2x4S ? 2
+                                      : c == H4x1 || c == H4x2 || c == H4x2S ? 4 : c == H6x1 ? 6 : c == H8x1 ? 8 : 3; }
+constexpr int halo_wn_c(int c) { return c == H2x4S ? 4 : (c == H2x2 || c == H2x2S || c == H4x2 || c == H3x2 || c == H3x2S || c == H4x2S) ? 2 : 1; }
+constexpr bool halo_db_c(int c) { return !(c == H2x2S || c == H2x4S || c == H3x1S || c == H3x2S || c == H4x2S); }
+inline int halo_wm(int c) { return halo_wm_c(c); }
+inline int halo_wn(int c) { return halo_wn_c(c); }
+// 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster
+// there: the bf16x6 residual data gradient over the padded grid, whose 130-column rows waste a
+// fifth of a 32-column tile grid)
+inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
   int c;
-  if (M <= 64) c = VST_HALO_M64 == 1 ? H2x1 : (VST_HALO_M64 == 2 ? H2x2 : H2x2S);
-  else if (M % 256 == 0) c = H8x1;
+  if (M <= 64) c = VST_HALO_M64;
+  else if (M % 256 == 0) c = VST_HALO_M256;
   else if (M % 192 == 0 && M % 128 != 0) {
-    if (bf16x6 && VST_HALO_M192 == 0) return 0;
-    const int m192[] = {H3x2, H6x1, H3x2, H2x4S, H3x1S, H3x2S};
-    c = m192[VST_HALO_M192];
-  } else c = VST_HALO_M128 == 1 ? H4x1 : H4x2;
+    if (bf16x6 && padout) return 0;
+    c = VST_HALO_M192;
+  } else c = VST_HALO_M128;
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
 }
 
+template <int C, int PR, bool GM>
+void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
+  constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
+  // waves per SIMD the registers must allow: 4 for the one-buffer tiles (their LDS admits 16 waves per
+  // CU), 3 for 4-wave double-buffered ones, 2 for the 6- and 8-wave double-buffered ones
+  constexpr int MINW = !halo_db_c(C) ? VST_HALO_SMINW : (WM * WN <= 4 ? 3 : 2);
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C)><<<grid, WM * WN * 64, 0, st>>>(P);
+}
+
+// only the block shapes the build's selection can reach are instantiated
 template <int PR, bool GM>
 void launch_halo(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
-  switch (c) {
-    case H2x1: conv_halo_kernel<2, 1, 3, PR, GM, true><<<grid, 128, 0, st>>>(P); break;
-    case H2x2: conv_halo_kernel<2, 2, 2, PR, GM, true><<<grid, 256, 0, st>>>(P); break;
-    case H2x2S: conv_halo_kernel<2, 2, 3, PR, GM, false><<<grid, 256, 0, st>>>(P); break;
-    case H4x1: conv_halo_kernel<4, 1, 3, PR, GM, true><<<grid, 256, 0, st>>>(P); break;
-    case H4x2: conv_halo_kernel<4, 2, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
-    case H6x1: conv_halo_kernel<6, 1, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
-    case H3x2: conv_halo_kernel<3, 2, 2, PR, GM, true><<<grid, 384, 0, st>>>(P); break;
-    case H2x4S: conv_halo_kernel<2, 4, 4, PR, GM, false><<<grid, 512, 0, st>>>(P); break;
-    case H3x1S: conv_halo_kernel<3, 1, 4, PR, GM, false><<<grid, 192, 0, st>>>(P); break;
-    case H3x2S: conv_halo_kernel<3, 2, 3, PR, GM, false><<<grid, 384, 0, st>>>(P); break;
-    default: conv_halo_kernel<8, 1, 2, PR, GM, true><<<grid, 512, 0, st>>>(P); break;
-  }
+  if (c == VST_HALO_M64) launch_halo_c<VST_HALO_M64, PR, GM>(grid, st, P);
+  else if (c == VST_HALO_M128) launch_halo_c<VST_HALO_M128, PR, GM>(grid, st, P);
+  else if (c == VST_HALO_M192) launch_halo_c<VST_HALO_M192, PR, GM>(grid, st, P);
+  else launch_halo_c<VST_HALO_M256, PR, GM>(grid, st, P);
 }
 
 template <int PR>

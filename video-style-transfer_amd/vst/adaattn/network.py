@@ -6,8 +6,9 @@ reference checkpoints load unchanged.  `nn.Conv2d` modules are parameter contain
 forward and backward runs libvst_hip.so kernels through `vst.ops` / `vst.adaattn.attention`:
   * reflection pad is folded into the conv gather, conv + bias + ReLU is one kernel,
   * the decoder's `interpolate(x5) + x4` and `cat([interpolate(x), x3])` write one buffer,
-  * the 1x1 f/g/h convs are MFMA GEMMs, the attention products run on the GEMM kernels with the
-    attention matrix materialised per image (see attention.py).
+  * the 1x1 f/g/h convs are MFMA GEMMs; the cosine attention never forms the Nc x Ns matrix (its
+    two moments are an exact re-association over the style positions) and the softmax attention
+    forms it in blocks of query rows (see attention.py).
 """
 import numpy as np
 import torch
@@ -52,7 +53,8 @@ class ConvReLU(nn.Module):
 
 
 class ConvTanh(nn.Module):
-    """AA/network.py:36-46: (tanh(conv(x)) + 1) / 2 * 255 (not on the training path)."""
+    """AA/network.py:36-46: (tanh(conv(x)) + 1) / 2 * 255 (defined, not used by StylizingNetwork):
+    the conv kernel, then the tanh-image kernel (forward and backward on the device)."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride):
         super().__init__()
@@ -60,7 +62,7 @@ class ConvTanh(nn.Module):
         self.tanh = nn.Tanh()
 
     def forward(self, x):
-        raise NotImplementedError("ConvTanh is defined but unused by the reference's StylizingNetwork")
+        return ops.tanh_image(self.conv.run(x), image=True)
 
 
 class ConvReluInterpolate(nn.Module):
@@ -73,9 +75,18 @@ class ConvReluInterpolate(nn.Module):
         self.scale_factor = scale_factor
 
     def forward(self, x):
-        if self.scale_factor != 2:
-            raise NotImplementedError("only scale_factor=2 bilinear upsampling is on the reference path")
-        return ops.upsample2x(self.conv.run(x, act="relu"))
+        y = self.conv.run(x, act="relu")
+        if self.scale_factor == 2:
+            return ops.upsample2x(y)
+        # F.interpolate(scale_factor=s, bilinear, align_corners=False) maps output pixel i to source
+        # (i + 0.5) / s - 0.5 with the output floor(H s) pixels tall; the size-based resize kernel maps
+        # with H / Ho, the same thing whenever H s is a whole number
+        H, W = y.shape[2:]
+        s = float(self.scale_factor)
+        Ho, Wo = int(np.floor(H * s)), int(np.floor(W * s))
+        if Ho != H * s or Wo != W * s or Ho < 1 or Wo < 1:
+            raise NotImplementedError(f"scale_factor {s} on a {H}x{W} map: the output size is not H*s x W*s exactly")
+        return ops.resize(y, (Ho, Wo))
 
 
 class Decoder(nn.Module):
@@ -97,7 +108,7 @@ class Decoder(nn.Module):
         self.conv8 = Conv(64, 3, kernel_size=3, stride=1)
 
     def forward(self, x5, x4, x3):
-        with ops.gemm_scope("stylizer"):
+        with ops.gemm_scope("stylizer"), ops.gemm_scope("dec"):  # channel-blocked K order (ops.gemm_role)
             return self._forward(x5, x4, x3)
 
     def _forward(self, x5, x4, x3):

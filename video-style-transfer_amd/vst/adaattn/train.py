@@ -189,6 +189,15 @@ class AdaAttNTrainer:
     def step(self, c1, c2=None, s=None):
         return self._update(self.losses, c1, c2, s)
 
+    def step_batch(self, batch):
+        """One step on a loader batch (content1, content2, style) (AA/train_video.py:78-81): the three
+        encodings as one VGG19 pass of 3B (a [3, B, 3, H, W] buffer); an already stacked buffer is
+        used as is."""
+        if isinstance(batch, torch.Tensor):
+            return self.step(batch)
+        c1, c2, s = batch
+        return self.step(torch.stack([c1, c2, s]))
+
     def backward(self, loss):
         """loss.backward() seeded as a fresh trainer's first step seeds it (the policy's initial loss
         scale, `ops.loss_scale()`: 1 except under fp16); returns the factor that unscales the

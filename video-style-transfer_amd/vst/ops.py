@@ -37,9 +37,10 @@ def _check(t, name, ndim=None):
 
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3, "f16": 4}
 KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
-# where the channel-blocked K order applies (VST_KBLOCK): "res" (default) the loss networks, every
-# data gradient and the stylizer's residual-block forwards; "1" not inside the stylizer forward at
-# all; "2" everywhere (diagnostic: fails the ragged golden step, tools/policy_check.py); "0" off
+# where the channel-blocked K order applies (VST_KBLOCK): "res" (default) the loss networks, the
+# ReCoNet stylizer's residual blocks and the AdaAttN decoder (scope "stylizer.dec": no InstanceNorm
+# there, and its 3x3 convs then run on the halo-tiled kernel); "1" nowhere inside a stylizer; "2"
+# everywhere (diagnostic: fails the ragged golden step, tools/policy_check.py); "0" off
 _KB = os.environ.get("VST_KBLOCK", "res")
 KBLOCK_ON = _KB != "0"
 KBLOCK_STYLIZER = _KB == "2"
@@ -221,7 +222,8 @@ def gemm_role(role):
     # (margin 2.7; residual blocks alone: 0.000 -- tools/policy_check.py, VST_KBLOCK=2 / res)
     sc = _SCOPE[0]
     in_stylizer = sc is not None and sc.split(".")[0] == "stylizer"
-    if KBLOCK_ON and (KBLOCK_STYLIZER or not in_stylizer or (KBLOCK_RES and sc.startswith("stylizer.res"))):
+    if KBLOCK_ON and (KBLOCK_STYLIZER or not in_stylizer or
+                      (KBLOCK_RES and (sc.startswith("stylizer.res") or sc.startswith("stylizer.dec")))):
         m |= KBLOCK
     _CUR[0] = m
     return m
@@ -1033,6 +1035,24 @@ def resize_bilinear(x, size, chscale=None, binarize=False, out=None, addend=None
     lib.vst_resize_bilinear(ptr(x), optr, N * C, C, H, W, Ho, Wo, ptr(chscale), int(binarize),
                             obs if obs != C * Ho * Wo else 0, ptr(addend), stream())
     return out
+
+
+class ResizeFn(Function):
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) with its adjoint (gather form)."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        ctx.x_shape = x.shape
+        return resize_bilinear(x.contiguous(), size)
+
+    @staticmethod
+    def backward(ctx, g):
+        return resize_bilinear_bwd(g.contiguous(), ctx.x_shape), None
+
+
+def resize(x, size):
+    """Differentiable bilinear resize (align_corners=False) to `size` = (Ho, Wo)."""
+    return ResizeFn.apply(x, tuple(int(v) for v in size))
 
 
 def resize_bilinear_bwd(gout, x_shape):

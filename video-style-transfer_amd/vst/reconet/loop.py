@@ -1,17 +1,22 @@
-"""The reference's epoch loop (RC/train_single/train_candy.py:58-170) around a trainer step,
-without a host synchronisation per step.
+"""The reference's epoch loops (RC/train_single/train_candy.py:58-170, AA/train_video.py:64-138)
+around a trainer step, without a host synchronisation per step.
 
 The reference reads six `.item()` loss terms every step for its tqdm postfix
 (train_candy.py:155-166) -- six device->host syncs that stall the launch queue.  `StepLog` keeps
 the steps' 0-d device scalars as they are (no kernel, no sync), and every `every` steps reads them
 all in ONE transfer and writes one JSONL line: the mean of every term over the window and the
-window's wall-clock throughput.  `fit` is the loop: per batch `trainer.step`, per epoch a
-`state_dict` checkpoint under the reference's file-name pattern (train_candy.py:168-170).
+window's wall-clock throughput (AA/train_video.py:124-134 reads four `.item()` per step the same
+way).  `fit` is the loop: per batch `trainer.step_batch` (the trainer unpacks its loader's batch as
+the reference's loop does), per epoch a `state_dict` checkpoint under the reference's file-name
+pattern (train_candy.py:168-170, train_video.py:137-138: `AA_VIDEO_CHECKPOINT`).
 """
 import json
 import time
 
 import torch
+
+# AA/train_video.py:138
+AA_VIDEO_CHECKPOINT = "./models/AdaAttN-video_epoch_{epoch}_batchSize_{batch}.pth"
 
 
 class StepLog:
@@ -57,15 +62,19 @@ class StepLog:
 
 
 def fit(trainer, loader, epochs, epoch_start=1, log=None, checkpoint=None):
-    """train_candy.py:62-170: for each epoch, one trainer step per batch of the loader
-    (FramePairLoader: (img1, img2, flow, mask) on the device; ImageLoader: images), the terms to
-    `log` (StepLog) without a per-step sync, and `torch.save(model.state_dict(), checkpoint.format(
-    epoch=e))` at the end of each epoch when `checkpoint` is given (the reference's pattern, e.g.
-    "./models/Flow_input_1_epoch_{epoch}_batchSize_2.pth")."""
+    """train_candy.py:62-170 / train_video.py:64-138: for each epoch, one trainer step per batch of
+    the loader (ReCoNet: FramePairLoader (img1, img2, flow, mask) or ImageLoader images; AdaAttN:
+    (content1, content2, style) triples), the terms to `log` (StepLog) without a per-step sync, and
+    `torch.save(model.state_dict(), checkpoint.format(epoch=e))` at the end of each epoch when
+    `checkpoint` is given (the reference's patterns, e.g.
+    "./models/Flow_input_1_epoch_{epoch}_batchSize_2.pth", AA_VIDEO_CHECKPOINT with its batch
+    filled in)."""
     for epoch in range(epoch_start, epochs + 1):
         trainer.model.train()
         for batch in loader:
-            if getattr(trainer, "single", False):
+            if hasattr(trainer, "step_batch"):
+                out = trainer.step_batch(batch)
+            elif getattr(trainer, "single", False):
                 out = trainer.step(batch)
             else:
                 img1, img2, flow, mask = batch

@@ -174,6 +174,14 @@ class ReCoNetTrainer:
         loss.backward(torch.full((), s, device=loss.device))
         return 1.0 / s
 
+    def step_batch(self, batch):
+        """One step on a loader batch: FramePairLoader's (img1, img2, flow, mask) or, for the
+        single-image trainer, ImageLoader's images (train_candy.py:77-78, train_coco2014.py:65)."""
+        if self.single:
+            return self.step(batch)
+        img1, img2, flow, mask = batch
+        return self.step(torch.stack([img1, img2]), flow, mask)
+
     def step(self, frames, flow=None, mask=None):
         """One training step (train_candy.py:77-152): losses, backward, gradient exchange, Adam.
         `step_count` counts calls; under the fp16 policy Adam's own count lives in `scaler` and does
