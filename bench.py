@@ -293,20 +293,23 @@ def full_size_parity_adaattn(args, dev, first):
     return res
 
 
-def pmc_traffic(model, family="conv_gemm_kernel"):
-    """HBM bytes per launch of the roofline kernel from the committed PMC summary of the same
+def pmc_traffic(model, family=("conv_halo_kernel", "conv_gemm_kernel")):
+    """HBM bytes per launch of the roofline kernel family from the committed PMC summary of the same
     workload (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/pmc_traffic.py; counters cannot
-    be read from inside the timed run).  None if no summary is committed."""
+    be read from inside the timed run): the launch-weighted mean over the family's kernels.  None if
+    no summary is committed."""
     import glob
 
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_traffic_{model}.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    fam = d["families"].get(family)
-    if fam is None:
+    fams = [d["families"][f] for f in ((family,) if isinstance(family, str) else family) if f in d["families"]]
+    if not fams:
         return None, None
-    return fam["bytes_per_launch"], os.path.relpath(files[-1], REPO) + " (" + d["method"] + ")"
+    launches = sum(f.get("launches", 1) for f in fams)
+    total = sum(f["bytes_per_launch"] * f.get("launches", 1) for f in fams)
+    return total / launches, os.path.relpath(files[-1], REPO) + " (" + d["method"] + ")"
 
 
 def vgg19_subbench(dev, reps=3, B=8, H=256, W=512):
@@ -717,7 +720,8 @@ def main():
                        "global_batch": B * world, "height": H, "width": W, "parallelism": f"dp{world}"},
             "frames_per_s": 2 * value,
             "loss_last_step": loss,
-            "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (conv fwd + dgrad implicit GEMM, all tile variants)",
+            "roofline": {"bound": "mfma", "kernel": "conv fwd + dgrad implicit GEMM (conv_halo_kernel: 3x3 stride-1 "
+                                                           "convs; conv_gemm_kernel: the rest), all tile variants",
                          "achieved": achieved, "peak": ks["peak_tflops"], "unit": "TFLOP/s",
                          "frac": achieved / ks["peak_tflops"], "traffic": traffic,
                          "peak_note": "algorithmic fp32-operand TFLOP/s vs the MFMA peak of the arithmetic launched "

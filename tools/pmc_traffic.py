@@ -17,7 +17,8 @@ FETCH_CORRECTION = 2.0
 PASS_ARGS = {"reconet": "bench.py --steps 2 --warmup 2 --prof-steps 0 (headline policy)",
              "adaattn": "bench.py --model adaattn --steps 2 --warmup 2 --prof-steps 0",
              "adaattn_c5": "bench.py --model adaattn --batch 8 --height 512 --width 1024 --steps 2 --warmup 2 "
-                           "--prof-steps 0 (config 5 shape, its default f16 policy)"}
+                           "--prof-steps 0 (config 5 shape, its default f16 policy)",
+             "reconet_f32": "bench.py --gemm f32 --steps 2 --warmup 2 --prof-steps 0 (strict fp32 MFMA policy)"}
 
 
 def load(model, counter):

@@ -228,10 +228,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 // Block shape per layer width (M = weight rows): WM x WN waves, M tile 32 WM.  The packed A carries
 // vst_conv_pack_dims' Mpad, which the M tile must divide (halo_cfg returns 0 otherwise).
 // Measured per layer shape (tools/gemm_bench.py, one box, bf16x6 / fp16; profiles/r04_halo_shapes.txt):
-//   M = 64  (VGG conv1_x, 256x512): 2x2 one buffer 746 us < 2x2 double 878 < 2x1 902 < per-tap 1071
+//   M = 64  (VGG conv1_x, 256x512): 2x2 one buffer 746-758 us < 2x2 double 878 < 2x1 902 < per-tap 1071
 //   M = 128 (VGG conv2_x): 4x1 619-664 < 4x2 685 < per-tap 751
-//   M = 192 (ReCoNet residual, 64x128): 2x4 one buffer 391 us (fp16 115) < per-tap 447 (LDS-A tile)
-//           < 3x2 415-428, 6x1 428, 3x1 448; the padded-grid data gradient stays per-tap (bf16x6)
+//   M = 192 (ReCoNet residual, 64x128): 2x4 one buffer 354-391 us (fp16 110-118) < per-tap 413-452
+//           (LDS-A tile) < 3x2 415-428, 6x1 428, 3x1 448; the padded-grid data gradient stays
+//           per-tap (bf16x6)
+//   2x4 one-buffer everywhere: 128-row layers 839 us, 256-row 695-770; 4x2 one-buffer: 932-1172 --
+//   both slower than 4x1 / 8x1 (profiles/r04_halo_shapes.txt)
 //   M = 256-multiples (VGG conv3_x / conv4_x): 8x1, 268-274 TF/s vs per-tap 233-245
 #ifndef VST_HALO_M64
 #define VST_HALO_M64 3  // block shape of 64-row layers (HaloCfg below)
@@ -244,9 +247,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #endif
 #ifndef VST_HALO_M256
 #define VST_HALO_M256 8  // 256-row multiples
-#endif
-#ifndef VST_HALO_SMINW
-#define VST_HALO_SMINW 4  // waves per SIMD the one-buffer tiles' registers must allow
 #endif
 // WM x WN waves (S: one patch buffer)
 enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S, H4x2S };
@@ -273,9 +273,12 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
 template <int C, int PR, bool GM>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
-  // waves per SIMD the registers must allow: 4 for the one-buffer tiles (their LDS admits 16 waves per
-  // CU), 3 for 4-wave double-buffered ones, 2 for the 6- and 8-wave double-buffered ones
-  constexpr int MINW = !halo_db_c(C) ? VST_HALO_SMINW : (WM * WN <= 4 ? 3 : 2);
+  // waves per SIMD the registers must allow: one-buffer tiles 4 for the single-product modes (their
+  // LDS admits 16 waves per CU) but 3 for bf16x6, whose three-piece fragments spill at the 128-VGPR
+  // budget (measured: the spilling 2x2 tile 1088 us vs 758 us at 3 waves per SIMD on the 64-row VGG
+  // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
+  // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
+  constexpr int MINW = !halo_db_c(C) ? (PR == 3 ? 3 : 4) : (WM * WN <= 4 ? 3 : 2);
   conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C)><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
