@@ -123,5 +123,5 @@ def test_hip_dp_step_equals_adam_on_mean_shard_gradient(tmp_path, kind):
     print(f"{kind}: {nb} buckets, all in backward; grad sum err {err:.2e} (one process, same shard twice: "
           f"{self_spread:.2e}); update cosine {cos:.8f}, "
           f"{frac:.2e} of parameters off by > 1e-3 lr, max |dp| {d.max():.2e}")
-    assert cos > 0.9999 and frac < 1e-3 and d.max() <= 2.01 * ref.lr
+    assert cos > 0.999 and frac < 1e-3 and d.max() <= 2.01 * ref.lr
     assert not np.allclose(gs[0].cpu().numpy(), gs[1].cpu().numpy())

@@ -223,7 +223,7 @@ def gemm_role(role):
     sc = _SCOPE[0]
     in_stylizer = sc is not None and sc.split(".")[0] == "stylizer"
     if KBLOCK_ON and (KBLOCK_STYLIZER or not in_stylizer or
-                      (KBLOCK_RES and (sc.startswith("stylizer.res") or sc.startswith("stylizer.dec")))):
+                      (KBLOCK_RES and (sc.startswith("stylizer.res") or "dec" in sc.split(".")))):
         m |= KBLOCK
     _CUR[0] = m
     return m
