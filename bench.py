@@ -684,7 +684,9 @@ def main():
         value = B * world * args.steps / elapsed
         achieved = ks["tflops"]
         c5 = args.model == "adaattn" and (H, W) == (512, 1024)
-        traffic, traffic_src = pmc_traffic("adaattn_c5" if c5 else args.model)
+        # the counter summary of this very workload and policy (the strict-f32 line has its own)
+        tag = "adaattn_c5" if c5 else (f"{args.model}_f32" if args.gemm == "f32" else args.model)
+        traffic, traffic_src = pmc_traffic(tag)
         if args.model == "reconet":
             metric = "training frame-pairs/sec at 256\u00d7512, ReCoNet+VGG19 loss, 1/2/4/8 GPUs"
             workload = (f"config{args.config}: ReCoNet {'train_candy step, full loss incl. FTL/OTL warp' if args.config == 3 else 'train_coco2014 step (content + Gram style, no temporal) on the 2B frames'}"

@@ -208,3 +208,53 @@ def test_pack_matrix_row_form_matches_flat_form(mode, transpose):
     _lib.lib.vst_pack_matrix(x.data_ptr(), b.data_ptr() + 4, B, M, K, transpose, Mpad, Kpad, M * K, mode, st)
     torch.cuda.synchronize()
     assert torch.equal(C(a).view(torch.int32), C(b[1:]).view(torch.int32))
+
+
+def _buf(t, misalign):
+    """t on the device, 16-byte aligned (vector kernels) or offset by one float (flat fallback)"""
+    if not misalign:
+        return G(t.contiguous())
+    b = torch.empty(t.numel() + 1, device=DEV)
+    v = b[1:].view(t.shape)
+    v.copy_(G(t))
+    return v
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("misalign", [False, True])
+def test_adaattn_elementwise_vec_and_flat(misalign):
+    """square_concat, adaattn_out, adaattn_out_bwd_scaled, plane_norm (AA/network.py:205-220): the
+    division-free float4 forms (aligned) and the flat forms (misaligned) against torch fp32."""
+    from vst._lib import lib
+
+    g = torch.Generator().manual_seed(11)
+    N, dv, P = 3, 8, 36
+    per = dv * P
+    V = torch.randn(N, per, generator=g)
+    M = torch.randn(N, per, generator=g)
+    E2 = M * M + torch.rand(N, per, generator=g) * 2 - 0.2  # some variances below the 1e-6 clamp
+    MV = torch.cat([M, E2], 1)
+    cn = torch.randn(N, per, generator=g)
+    dout = torch.randn(N, per, generator=g)
+    w = torch.rand(N, P, generator=g) + 0.5
+    Vd, MVd, cnd, doutd, wd = (_buf(t, misalign) for t in (V, MV, cn, dout, w))
+    VV2, out, dMV = (_buf(torch.zeros(s), misalign) for s in ((N, 2 * per), (N, per), (N, 2 * per)))
+    lib.vst_square_concat(Vd.data_ptr(), VV2.data_ptr(), N, per, _st())
+    lib.vst_adaattn_out(MVd.data_ptr(), cnd.data_ptr(), out.data_ptr(), N, per, _st())
+    lib.vst_adaattn_out_bwd_scaled(doutd.data_ptr(), MVd.data_ptr(), cnd.data_ptr(), wd.data_ptr(), dMV.data_ptr(), N,
+                                   per, P, _st())
+    xs = torch.randn(5, 64 * 20, generator=g)
+    xsd, nrm = _buf(xs, misalign), _buf(torch.zeros(5), misalign)
+    lib.vst_plane_norm(xsd.data_ptr(), nrm.data_ptr(), 5, 64 * 20, _st())
+    torch.cuda.synchronize()
+    assert torch.equal(C(VV2), torch.cat([V, V * V], 1))
+    var = E2 - M * M
+    assert rel_err(C(out).numpy(), (torch.sqrt(torch.clamp(var, min=1e-6)) * cn + M).numpy()) < 1e-6
+    dvar = torch.where(var >= 1e-6, dout * cn * 0.5 / torch.sqrt(var.clamp_min(1e-30)), torch.zeros_like(var))
+    s = w.repeat(1, dv)
+    ref = torch.cat([(dout - 2 * M * dvar) * s, dvar * s], 1)
+    assert rel_err(C(dMV).numpy(), ref.numpy()) < 1e-5
+    assert rel_err(C(nrm).numpy(), xs.double().norm(dim=1).float().numpy()) < 1e-6

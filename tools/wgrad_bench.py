@@ -27,7 +27,13 @@ SHAPES = [
     # the nearest-x2 layers through the phase-stacked source-grid GEMM (vst_conv_wgrad_up2)
     ("deconv1_p", 16, 192, 64, 128, 96, 3, 1, 0, 1, 2),
     ("deconv2_p", 16, 96, 128, 256, 48, 3, 1, 0, 1, 2),
+    # AdaAttN decoder at config 5 (B = 8 pairs -> 16 images, 512x1024 input; AA/network.py:63-99)
+    ("aadec1", 16, 512, 64, 128, 512, 3, 1, 0, 1, 1),
+    ("aadec3", 16, 256, 128, 256, 256, 3, 1, 0, 1, 1),
+    ("aadec5", 16, 128, 256, 512, 128, 3, 1, 0, 1, 1),
+    ("aadec7", 16, 64, 512, 1024, 64, 3, 1, 0, 1, 1),
 ]
+ONLY = os.environ.get("BENCH_ONLY")
 
 
 def load(path):
@@ -41,6 +47,9 @@ def load(path):
 
 
 def main():
+    global SHAPES
+    if ONLY:
+        SHAPES = [s for s in SHAPES if any(o in s[0] for o in ONLY.split(","))]
     paths = sys.argv[1:] or [LIB_PATH]
     libs = [load(p) for p in paths]
     st = torch.cuda.current_stream().cuda_stream

@@ -265,6 +265,81 @@ __global__ void adaattn_out_bwd_scaled_kernel(const float* __restrict__ dout, co
   dMV[n * 2 * per + per + t] = dvar * s;
 }
 
+// Division-free forms of the four kernels above (one float4 per thread, image n on blockIdx.y, the
+// column-scaled backward's channel on blockIdx.z): the flat forms decode (n, t) with a 64-bit
+// division per element (and t % P in 64 bits), which made them VALU-bound under the HBM rate.
+// Used when per (and P) is a multiple of 4 and the pointers are 16-byte aligned.
+__global__ void square_concat_vec_kernel(const float4* __restrict__ V, float4* __restrict__ VV2, long per4) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per4) return;
+  const long n = blockIdx.y;
+  const float4 v = V[n * per4 + t];
+  VV2[n * 2 * per4 + t] = v;
+  VV2[n * 2 * per4 + per4 + t] = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
+}
+
+__global__ void adaattn_out_vec_kernel(const float4* __restrict__ MV, const float4* __restrict__ cn,
+                                       float4* __restrict__ out, long per4) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per4) return;
+  const long n = blockIdx.y;
+  const float4 m = MV[n * 2 * per4 + t], e2 = MV[n * 2 * per4 + per4 + t], c = cn[n * per4 + t];
+  float4 o;
+  o.x = sqrtf(fmaxf(e2.x - m.x * m.x, 1e-6f)) * c.x + m.x;
+  o.y = sqrtf(fmaxf(e2.y - m.y * m.y, 1e-6f)) * c.y + m.y;
+  o.z = sqrtf(fmaxf(e2.z - m.z * m.z, 1e-6f)) * c.z + m.z;
+  o.w = sqrtf(fmaxf(e2.w - m.w * m.w, 1e-6f)) * c.w + m.w;
+  out[n * per4 + t] = o;
+}
+
+// grid (ceil(P4 / 256), dv, N): element (n, channel c, column p) of the dv x P plane stack
+__global__ void adaattn_out_bwd_scaled_vec_kernel(const float4* __restrict__ dout, const float4* __restrict__ MV,
+                                                  const float4* __restrict__ cn, const float4* __restrict__ w,
+                                                  float4* __restrict__ dMV, int P4, long per4) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P4) return;
+  const long n = blockIdx.z, t = (long)blockIdx.y * P4 + p;
+  const float4 m = MV[n * 2 * per4 + t], e2 = MV[n * 2 * per4 + per4 + t], g = dout[n * per4 + t];
+  const float4 c = cn[n * per4 + t], sc = w[n * P4 + p];
+  float4 d0, d1;
+  auto one = [](float m_, float e2_, float g_, float c_, float s_, float& a, float& b) {
+    const float var = e2_ - m_ * m_;
+    const float dvar = var >= 1e-6f ? g_ * c_ * 0.5f / sqrtf(var) : 0.f;
+    a = (g_ - 2.0f * m_ * dvar) * s_;
+    b = dvar * s_;
+  };
+  one(m.x, e2.x, g.x, c.x, sc.x, d0.x, d1.x);
+  one(m.y, e2.y, g.y, c.y, sc.y, d0.y, d1.y);
+  one(m.z, e2.z, g.z, c.z, sc.z, d0.z, d1.z);
+  one(m.w, e2.w, g.w, c.w, sc.w, d0.w, d1.w);
+  dMV[n * 2 * per4 + t] = d0;
+  dMV[n * 2 * per4 + per4 + t] = d1;
+}
+
+// per-plane L2 norm with two float4 loads in flight per thread (fp64 accumulation as the flat form)
+__global__ void plane_norm_vec_kernel(const float4* __restrict__ x, float* __restrict__ out, int HW4) {
+  __shared__ double sh[RT / 64];
+  const float4* xp = x + (long)blockIdx.x * HW4;
+  double s = 0.0;
+  int i = threadIdx.x;
+  for (; i + RT < HW4; i += 2 * RT) {
+    const float4 a = xp[i], b = xp[i + RT];
+    s += ((double)a.x * a.x + (double)a.y * a.y) + ((double)a.z * a.z + (double)a.w * a.w) +
+         (((double)b.x * b.x + (double)b.y * b.y) + ((double)b.z * b.z + (double)b.w * b.w));
+  }
+  if (i < HW4) {
+    const float4 a = xp[i];
+    s += ((double)a.x * a.x + (double)a.y * a.y) + ((double)a.z * a.z + (double)a.w * a.w);
+  }
+  const double t = block_sum_d(s, sh);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)sqrt(t);
+}
+
+static bool al16(const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr,
+                 const void* e = nullptr) {
+  return ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c) | ((uintptr_t)d) | ((uintptr_t)e)) & 15) == 0;
+}
+
 // per-plane mean and unbiased std (torch .mean / .std over (H, W))
 __global__ void plane_meanstd_kernel(const float* __restrict__ x, float* __restrict__ mean, float* __restrict__ std_,
                                      int HW) {
@@ -453,6 +528,11 @@ int vst_norm_grad_add(float* x, const float* s, const float* nrm, const float* y
 
 int vst_square_concat(const float* V, float* VV2, int N, long per, void* stream) {
   VST_CHECK_ARG(V && VV2 && N > 0 && per > 0);
+  if (per % 4 == 0 && N <= 65535 && al16(V, VV2)) {
+    dim3 g(ceil_div(per / 4, 256), N);
+    square_concat_vec_kernel<<<g, 256, 0, (hipStream_t)stream>>>((const float4*)V, (float4*)VV2, per / 4);
+    return vst_launch_status();
+  }
   square_concat_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(V, VV2, N, per);
   return vst_launch_status();
 }
@@ -465,6 +545,12 @@ int vst_square_concat_bwd(const float* dVV2, const float* V, float* dV, int N, l
 
 int vst_adaattn_out(const float* MV, const float* cn, float* out, int N, long per, void* stream) {
   VST_CHECK_ARG(MV && cn && out && N > 0 && per > 0);
+  if (per % 4 == 0 && N <= 65535 && al16(MV, cn, out)) {
+    dim3 g(ceil_div(per / 4, 256), N);
+    adaattn_out_vec_kernel<<<g, 256, 0, (hipStream_t)stream>>>((const float4*)MV, (const float4*)cn, (float4*)out,
+                                                               per / 4);
+    return vst_launch_status();
+  }
   adaattn_out_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(MV, cn, out, N, per);
   return vst_launch_status();
 }
@@ -479,6 +565,12 @@ int vst_adaattn_out_bwd(const float* dout, const float* MV, const float* cn, flo
 int vst_adaattn_out_bwd_scaled(const float* dout, const float* MV, const float* cn, const float* colscale, float* dMV,
                                int N, long per, int P, void* stream) {
   VST_CHECK_ARG(dout && MV && cn && colscale && dMV && N > 0 && per > 0 && P > 0 && per % P == 0);
+  if (P % 4 == 0 && per / P <= 65535 && N <= 65535 && al16(dout, MV, cn, colscale, dMV)) {
+    dim3 g(ceil_div(P / 4, 256), per / P, N);
+    adaattn_out_bwd_scaled_vec_kernel<<<g, 256, 0, (hipStream_t)stream>>>(
+        (const float4*)dout, (const float4*)MV, (const float4*)cn, (const float4*)colscale, (float4*)dMV, P / 4, per / 4);
+    return vst_launch_status();
+  }
   adaattn_out_bwd_scaled_kernel<<<ceil_div((long)N * per, 256), 256, 0, (hipStream_t)stream>>>(dout, MV, cn, colscale,
                                                                                             dMV, N, per, P);
   return vst_launch_status();
@@ -499,6 +591,10 @@ int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, 
 
 int vst_plane_norm(const float* x, float* out, long NC, int HW, void* stream) {
   VST_CHECK_ARG(x && out && NC > 0 && HW > 0);
+  if (HW % 4 == 0 && al16(x)) {
+    plane_norm_vec_kernel<<<NC, RT, 0, (hipStream_t)stream>>>((const float4*)x, out, HW / 4);
+    return vst_launch_status();
+  }
   plane_norm_kernel<<<NC, RT, 0, (hipStream_t)stream>>>(x, out, HW);
   return vst_launch_status();
 }

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   }
 }
 
-enum { W32 = 0, W64, W96, W128, W192, W64N, W96N };  // *N: 256-column variants (row-tiled kernel only)
+enum { W32 = 0, W64, W96, W128, W192, W64N, W96N, W128N };  // *N: 256-column variants (row-tiled kernel only)
 static int wsel(int M) {
   if (M <= 32) return W32;
   if (M <= 64) return W64;
@@ -840,14 +840,24 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
     case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W128N:
+      if constexpr (PR == 2 || PR == 4) wgrad2_kernel<2, 2, 2, 4, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P);
+      break;
     default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
   }
 }
 
-// two k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
+// k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
+#ifndef VST_WKD_SP
+#define VST_WKD_SP 2
+#endif
+// 128 x 256 blocks (each wave 64 x 128) for the single-product modes' 128-row tiles
+#ifndef VST_WG128N
+#define VST_WG128N 0
+#endif
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
-  launch_wg2_pk<PR, GMD, (PR == 2 || PR == 4) ? 2 : 1>(c, g, st, P);
+  launch_wg2_pk<PR, GMD, (PR == 2 || PR == 4) ? VST_WKD_SP : 1>(c, g, st, P);
 }
 
 template <int GMD>
@@ -901,6 +911,9 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     // the slab layout and the workspace size do not change.
     int cw = c;
     if ((c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
+    const int am = vst_mode_arith(mode);
+    if (VST_WG128N && c == W128 && (am == VST_GEMM_BF16 || am == VST_GEMM_F16) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0)
+      cw = W128N;
     dim3 g(Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
     if (gmode == 0) launch_wg2<0>(cw, g, mode, st, Q);
     else if (gmode == 2) launch_wg2<2>(cw, g, mode, st, Q);
