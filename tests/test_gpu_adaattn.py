@@ -381,7 +381,9 @@ DEAD, DEAD_ABS = 1e-6, 1e-5
 def own_norm_margins(policy, got_norms, ref_norms):
     """{tensor: margin} (<= 1 passes) against the policy's per-tensor own-norm bar (above)"""
     gmax = max(ref_norms.values())
-    bar = max(2 * U[policy] * DEPTH, 2e-3)  # (bf16x3: floor at the fp32-class golden bar's scale)
+    # bf16x3: its 2^-16 products leave the attention's E2 - M^2 cancellation (AA/network.py:209-211)
+    # as the dominant error -- measured 4.0e-3 on adaattn.0.g.bias at 64x128 -- so it is held to 1e-2
+    bar = max(2 * U[policy] * DEPTH, 1e-2 if policy == "bf16x3" else 0.0)
     out = {}
     for n, rn in ref_norms.items():
         gn = got_norms[n]
