@@ -71,7 +71,13 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // the patch (TH + 2) x 34 pixels.  DB: double-buffered patch (the next channel block's stores need
 // no second barrier) or one buffer (half the LDS: more blocks per CU, two barriers per block).
 // PREC 3: bf16x6 (three bf16 pieces per value); 2 / 4: single bf16 / fp16 product (one piece).
-template <int WM, int WN, int MINW, int PREC, bool GM, bool DB>
+// KC: 16-channel blocks per stage (one barrier per KC blocks; their patch loads in flight across KC x 9
+// taps).  The single-product modes do one MFMA per fragment pair, so a one-block stage (36 MFMAs per
+// wave) does not cover a first-touch gather of the next patch from HBM (config 5: 67 % of wave time
+// waiting on memory at KC = 1, profiles/r04_mfma_busy_adaattn_c5.json).  Measured, it does not pay:
+// fp16 VGG + residual shapes 2.38 ms at KC = 1, 2.58 ms at 2, 2.61 ms at 4 (the larger stage halves the
+// blocks per CU; profiles/r04_halo_kc.txt), so VST_HALO_KC stays 1 (KC > 1 kept for the record).
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo kernel: bf16x6, bf16 or fp16 products");
   constexpr int TM = 1, TN = 4;
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   constexpr int TIT = (NTASK + NTT - 1) / NTT;
   constexpr int NBUF = DB ? 2 : 1;
   constexpr int OOR = 0x7ffffff0;
-  __shared__ __attribute__((aligned(16))) float Ps[NBUF][HPP][LS];
+  __shared__ __attribute__((aligned(16))) float Ps[NBUF][KC][HPP][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -143,27 +149,34 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
 
-  float rv[TIT][8];
-  float rgv[TIT][GM ? 8 : 1];
-  auto load_patch = [&](int cb) {
-    const int cb_off = __builtin_amdgcn_readfirstlane(cb * 16 * plane * 4);
+  float rv[KC][TIT][8];
+  float rgv[KC][TIT][GM ? 8 : 1];
+  // stage s = channel blocks KC s .. KC s + KC - 1 (Cs / 16 is a multiple of KC: the launcher checks)
+  auto load_patch = [&](int st) {
 #pragma unroll
-    for (int it = 0; it < TIT; ++it)
+    for (int kc = 0; kc < KC; ++kc) {
+      const int cb_off = __builtin_amdgcn_readfirstlane((st * KC + kc) * 16 * plane * 4);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        rv[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
-        if constexpr (GM)
-          rgv[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
-      }
+      for (int it = 0; it < TIT; ++it)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          rv[kc][it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
+          if constexpr (GM)
+            rgv[kc][it][i] =
+                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
+        }
+    }
   };
   auto store_patch = [&](int buf) {
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
     for (int it = 0; it < TIT; ++it) {
       if (NTASK % NTT != 0 && t_lds[it] < 0) continue;
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = GM ? (rgv[it][i] > 0.f ? rv[it][i] : 0.f) : rv[it][i];
-      uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][0][0]) + t_lds[it];
+      for (int i = 0; i < 8; ++i) v[i] = GM ? (rgv[kc][it][i] > 0.f ? rv[kc][it][i] : 0.f) : rv[kc][it][i];
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][kc][0][0]) + t_lds[it];
       if constexpr (PREC == 3) {
         uint32_t h[4], md[4], l[4];
 #pragma unroll
@@ -188,28 +201,32 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  const int ncb = P.Cs / 16;
+  const int nst = P.Cs / (16 * KC);
   load_patch(0);
   load_a(0, arC);
   store_patch(0);
   __syncthreads();
-  for (int cb = 0; cb < ncb; ++cb) {
-    const int buf = DB ? (cb & 1) : 0;
-    if (cb + 1 < ncb) load_patch(cb + 1);
+  for (int st = 0; st < nst; ++st) {
+    const int buf = DB ? (st & 1) : 0;
+    if (st + 1 < nst) load_patch(st + 1);
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int kh = t / 3, kw = t % 3;
-      const int ph = tr ? 2 - kh : kh, pw = tr ? 2 - kw : kw;  // (tr is block-uniform)
-      const int kt_next = t < 8 ? 9 * cb + t + 1 : 9 * (cb + 1);
-      if (t < 8 || cb + 1 < ncb) load_a(kt_next, arN);
-      // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
-      // columns lo + pw
-      const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
-      halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
+    for (int kc = 0; kc < KC; ++kc) {
+      const int cb = st * KC + kc;
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int ph = tr ? 2 - kh : kh, pw = tr ? 2 - kw : kw;  // (tr is block-uniform)
+        const int kt_next = t < 8 ? 9 * cb + t + 1 : 9 * (cb + 1);
+        if (t < 8 || cb + 1 < nst * KC) load_a(kt_next, arN);
+        // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
+        // columns lo + pw
+        const float(*Bt)[LS] = &Ps[buf][kc][(4 * wn + ph) * HPW + pw];
+        halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
+#pragma unroll
+        for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+      }
     }
-    if (cb + 1 < ncb) {
+    if (st + 1 < nst) {
       if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
       store_patch(DB ? buf ^ 1 : 0);
     }
@@ -270,16 +287,27 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
 }
 
+#ifndef VST_HALO_KC
+#define VST_HALO_KC 1  // channel blocks per stage for the single-product modes (measured above)
+#endif
 template <int C, int PR, bool GM>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
+  // (the one-buffer tiles already sit at their 128-VGPR budget with one block's staging registers)
+  constexpr int KC = (PR == 3 || !halo_db_c(C)) ? 1 : VST_HALO_KC;
   // waves per SIMD the registers must allow: one-buffer tiles 4 for the single-product modes (their
   // LDS admits 16 waves per CU) but 3 for bf16x6, whose three-piece fragments spill at the 128-VGPR
   // budget (measured: the spilling 2x2 tile 1088 us vs 758 us at 3 waves per SIMD on the 64-row VGG
   // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
   // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
   constexpr int MINW = !halo_db_c(C) ? (PR == 3 ? 3 : 4) : (WM * WN <= 4 ? 3 : 2);
-  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C)><<<grid, WM * WN * 64, 0, st>>>(P);
+  if constexpr (KC > 1) {
+    if ((P.Cs / 16) % KC != 0) {  // (a channel count that does not fill whole stages)
+      conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), 1><<<grid, WM * WN * 64, 0, st>>>(P);
+      return;
+    }
+  }
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 // only the block shapes the build's selection can reach are instantiated

@@ -553,6 +553,48 @@ def grad_sink(p):
     return g
 
 
+WGRAD_SIDE = os.environ.get("VST_WGRAD_SIDE", "1") != "0"  # A/B: weight gradients on a second stream
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def join_side_streams():
+    """The current stream waits for every weight gradient queued on the side streams (called at the
+    end of each backward pass and by the data-parallel bucket launch before it reads the flat
+    gradient)."""
+    for dev, s in _SIDE.items():
+        torch.cuda.current_stream(dev).wait_stream(s)
+
+
+def wgrad_into_sink(compute, sink, *used):
+    """Run `compute()` -- a weight-gradient GEMM accumulating into the leaf gradient `sink` -- on a
+    second HIP stream of the device.  A layer's weight gradient is read only by the optimizer, its
+    data gradient by the next layer back, so the wgrad GEMMs (latency-bound, about a third
+    MFMA-busy: profiles/r04_mfma_busy_*.json) run beside the MFMA-bound data-gradient GEMMs of the
+    layers before them instead of in series.  Ordering: the side stream first waits for the current
+    stream (the inputs `used` and the zeroed sink are ready), `used` are recorded on it so the
+    caching allocator keeps them until it is done, and a final callback of the backward pass makes
+    the caller's stream wait for it (so `.grad` and the optimizer see the finished gradients).
+    Gradients returned to autograd (no sink) stay on the current stream."""
+    if not (WGRAD_SIDE and sink is not None and sink.is_cuda):
+        return compute()
+    dev = sink.device
+    side = _side_stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        compute()
+    for t in used:
+        t.record_stream(side)
+    torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+    return sink
+
+
 class Conv2dFn(Function):
     """[nearest x`up` upsample] -> (reflect|zero) pad -> Conv2d(ks, stride) [+bias] [-> ReLU | ReCoNet tanh].
     Replaces RC/network.py:72-75 (ConvLayer), 114-120 (UpsampleConvLayer), 83-85 (ConvTanh) and the
@@ -643,9 +685,10 @@ class Conv2dFn(Function):
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
             if rowsplit_wgrad_ok(w.shape[0], w.shape[1], ks, stride, pad_mode, up, x.shape[3]) and pad == ks // 2:
-                dw = conv_wgrad_rowsplit(gz, x, w.shape, out=sink)
+                dw = wgrad_into_sink(lambda: conv_wgrad_rowsplit(gz, x, w.shape, out=sink), sink, gz, x)
             else:
-                dw = conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up, out=sink)
+                dw = wgrad_into_sink(lambda: conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up, out=sink),
+                                     sink, gz, x)
             dw = None if sink is not None else dw
         if ctx.has_bias and ctx.needs_input_grad[2]:
             sink = grad_sink(ctx.params[1])
@@ -1263,7 +1306,7 @@ class ConvTranspose2dFn(Function):
             dx = conv_gemm(gy, packed_weight(w, False), Cin, ks, H, W, GM_ZERO, stride, pad, 1)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
-            dw = conv_wgrad(x, gy, w.shape, ks, stride, pad, "zero", 1, out=sink)
+            dw = wgrad_into_sink(lambda: conv_wgrad(x, gy, w.shape, ks, stride, pad, "zero", 1, out=sink), sink, x, gy)
             dw = None if sink is not None else dw
         if ctx.has_bias and ctx.needs_input_grad[2]:
             sink = grad_sink(ctx.params[1])

@@ -18,7 +18,8 @@ module is consumed first is needed, and a parameter the graph never reaches (unu
 keeps its bucket back for `finish()`.  A hook that fires for a parameter whose bucket was already
 launched (a second backward in the same step) raises instead of reducing a half-written slice.
 Hooks fire in the same order on every rank (same graph), so the collectives are issued in the same
-order everywhere.
+order everywhere.  Weight gradients that the HIP backward queued on its side stream
+(ops.wgrad_into_sink) are joined into the current stream before each launch.
 """
 import torch
 import torch.distributed as dist
@@ -110,6 +111,10 @@ class GradBuckets:
     def _launch(self, b):
         lo, hi = self.buckets[b]
         self.launched[b] = True
+        if self.flat.g.is_cuda:
+            from ..ops import join_side_streams  # weight gradients queued on the side stream
+
+            join_side_streams()
         self.works.append(dist.all_reduce(self.flat.g[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def finish(self):
