@@ -58,6 +58,13 @@ const char* vst_build_id(void);
  * results are bitwise those of the per-tap kernel.  VST_GEMM_PERTAP or-ed into a GEMM call's mode
  * selects the per-tap kernel instead (an explicit per-call choice for A/B measurement and the
  * equivalence test; pack entries ignore it).
+ * A bf16x6 / bf16 halo launch whose grid would not fill the chip (fewer than 512 blocks: AdaAttN
+ * config 4's decoder, VGG19 conv4 / conv5) is split over the 16-channel blocks (split-K; fp16 launches
+ * stay unsplit): the slices' raw sums go to a per-stream
+ * scratch buffer the library holds, and a reduce kernel adds them in slice order (deterministic)
+ * and applies the epilogue -- equal to the unsplit result up to fp32 summation order.
+ * VST_GEMM_NOSPLIT or-ed into the mode keeps such a launch unsplit (the bitwise test against the
+ * per-tap kernel).
  * An unknown mode returns VST_EINVAL (-1). */
 #define VST_GEMM_F32 0
 #define VST_GEMM_BF16X3 1
@@ -66,6 +73,7 @@ const char* vst_build_id(void);
 #define VST_GEMM_F16 4
 #define VST_GEMM_KBLOCK 16
 #define VST_GEMM_PERTAP 32
+#define VST_GEMM_NOSPLIT 64
 
 /* ---- convolution (implicit GEMM on MFMA, arithmetic per the `mode` argument) ---------------
  * Replaces: ReflectionPad2d + Conv2d (RC/network.py:68-75), nearest x2 interpolate + pad + conv

@@ -6,7 +6,10 @@ in the same order with the same MFMA sequence, so their outputs must be BITWISE 
 border rule (reflect / zero forward, transposed data gradient with and without the gathered ReLU
 mask, the padded-grid data gradient with its border side buffer), epilogue and ragged tile edge.
 The shapes are the training paths' 3x3 layers at reduced size (VGG16 / VGG19 64..512 channels,
-ReCoNet residual 192, AdaAttN decoder 256 / 128 / 64) plus ragged grids."""
+ReCoNet residual 192, AdaAttN decoder 256 / 128 / 64) plus ragged grids.  These small grids would be
+split over the channel blocks (split-K: fewer than 512 blocks); the bitwise comparisons keep the
+halo launch unsplit (VST_GEMM_NOSPLIT), and the split results are held to the unsplit ones within
+fp32 summation-order rounding and to fp64."""
 import ctypes
 
 import numpy as np
@@ -19,7 +22,7 @@ from vst._lib import lib
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 BF16, BF16X6, F16 = 2, 3, 4
-KBLOCK, PERTAP = 16, 32
+KBLOCK, PERTAP, NOSPLIT = 16, 32, 64
 GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
 EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM = 1, 2, 8, 16
 
@@ -77,7 +80,7 @@ def test_halo_forward_bitwise(mode, shape, pad_mode):
     wp = _pack(w, m)
     gm = GM_REFLECT if pad_mode == "reflect" else GM_ZERO
     epi = EPI_BIAS | (EPI_RELU if pad_mode == "zero" else 0)
-    halo = _conv(x, wp, Cout, H, W, gm, 1, m, epi, bias=b)
+    halo = _conv(x, wp, Cout, H, W, gm, 1, m | NOSPLIT, epi, bias=b)
     ref = _conv(x, wp, Cout, H, W, gm, 1, m | PERTAP, epi, bias=b)
     torch.cuda.synchronize()
     assert torch.equal(halo, ref), float((halo - ref).abs().max())
@@ -104,7 +107,7 @@ def test_halo_dgrad_bitwise(mode, shape, masked):
     gmask = _rand(N, Cout, H, W, seed=6) if masked else None
     dmask = _rand(N, Cin, H, W, seed=7) if masked else None
     epi = EPI_MASK if masked else 0
-    halo = _conv(dy, wp, Cin, H, W, GM_TRANSPOSED, 1, m, epi, mask=dmask, gmask=gmask)
+    halo = _conv(dy, wp, Cin, H, W, GM_TRANSPOSED, 1, m | NOSPLIT, epi, mask=dmask, gmask=gmask)
     ref = _conv(dy, wp, Cin, H, W, GM_TRANSPOSED, 1, m | PERTAP, epi, mask=dmask, gmask=gmask)
     torch.cuda.synchronize()
     assert torch.equal(halo, ref), float((halo - ref).abs().max())
@@ -128,7 +131,7 @@ def test_halo_padout_dgrad_bitwise(mode, shape):
     wp = _pack(w, m, transposed=True)
     st = torch.cuda.current_stream().cuda_stream
     res = []
-    for mm in (m, m | PERTAP):
+    for mm in (m | NOSPLIT, m | PERTAP, m):
         dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
         border = torch.zeros(N, Cin, H + 2, W + 2, device=DEV)
         lib.vst_conv_dgrad_padout(dy.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N, Cout, H, W,
@@ -137,6 +140,7 @@ def test_halo_padout_dgrad_bitwise(mode, shape):
         res.append(dx)
     torch.cuda.synchronize()
     assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    assert float((res[2] - res[0]).abs().max() / res[0].abs().max()) < 1e-5  # split-K (bf16x6): summation order
     x = torch.zeros(N, Cin, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
     y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w.double())
     y.backward(dy.double())
@@ -152,7 +156,7 @@ def test_halo_accumulate_and_fallbacks():
     m = BF16X6 | KBLOCK
     wp = _pack(w, m)
     base = _rand(1, 64, 10, 40, seed=12)
-    a = _conv(x, wp, 64, 10, 40, GM_ZERO, 1, m, EPI_ACCUM, out=base.clone())
+    a = _conv(x, wp, 64, 10, 40, GM_ZERO, 1, m | NOSPLIT, EPI_ACCUM, out=base.clone())
     b = _conv(x, wp, 64, 10, 40, GM_ZERO, 1, m | PERTAP, EPI_ACCUM, out=base.clone())
     assert torch.equal(a, b)
     for cout in (3, 96):
@@ -160,3 +164,39 @@ def test_halo_accumulate_and_fallbacks():
         y = _conv(x, _pack(w2, m), cout, 10, 40, GM_REFLECT, 1, m)
         ref = F.conv2d(F.pad(x.double(), (1, 1, 1, 1), mode="reflect"), w2.double())
         assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-6
+
+
+@pytest.mark.parametrize("mode", [BF16X6, BF16])  # (fp16 launches are never split)
+@pytest.mark.parametrize("shape", [(4, 192, 64, 128, 192), (2, 192, 20, 36, 192), (1, 128, 16, 64, 128),
+                                   (1, 256, 8, 16, 128)])
+@pytest.mark.parametrize("epi", ["bias_relu", "mask", "accum"])
+def test_halo_split_k(mode, shape, epi):
+    """Split-K (the grid under 512 blocks; ReCoNet's residual layer at a quarter batch first): the
+    slices' sums added in order then the epilogue, against the unsplit launch (same k-tiles, other
+    fp32 summation order) and fp64."""
+    N, Cin, H, W, Cout = shape
+    x = _rand(N, Cin, H, W, seed=21, scale=3.0)
+    w = _rand(Cout, Cin, 3, 3, seed=22, scale=0.05)
+    b = _rand(Cout, seed=23)
+    mask = _rand(N, Cout, H, W, seed=24)
+    base = _rand(N, Cout, H, W, seed=25)
+    m = mode | KBLOCK
+    wp = _pack(w, m)
+    e = {"bias_relu": EPI_BIAS | EPI_RELU, "mask": EPI_MASK, "accum": EPI_ACCUM}[epi]
+    kw = dict(bias=b) if epi == "bias_relu" else dict(mask=mask) if epi == "mask" else {}
+    outs = [_conv(x, wp, Cout, H, W, GM_REFLECT, 1, mm, e, out=base.clone() if epi == "accum" else None, **kw)
+            for mm in (m, m | NOSPLIT)]
+    torch.cuda.synchronize()
+    split, whole = outs
+    assert not torch.isnan(split).any()
+    y = F.conv2d(F.pad(x.double(), (1, 1, 1, 1), mode="reflect"), w.double())
+    if epi == "bias_relu":
+        y = (y + b.double().view(1, -1, 1, 1)).clamp_min(0)
+    elif epi == "mask":
+        y = y * (mask > 0).double()
+    else:
+        y = y + base.double()
+    scale = float(y.abs().max())
+    assert float((split - whole).abs().max()) / scale < 1e-5  # fp32 summation order over K = 9 Cin
+    err = float((split.double() - y).abs().max()) / scale
+    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err

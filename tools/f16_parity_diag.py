@@ -58,7 +58,7 @@ def top(d, k=6):
     return sorted(((v, n) for n, v in d.items()), reverse=True)[:k]
 
 
-def step_vs_oracle(policy, B, H, W, seeds=(61, 62, 63)):
+def step_vs_oracle(policy, B, H, W, seeds=(61, 62, 63), k=6):
     from vst import ops
     from vst.adaattn.train import AdaAttNTrainer
     from vst.synthetic import content_style_batch
@@ -85,7 +85,7 @@ def step_vs_oracle(policy, B, H, W, seeds=(61, 62, 63)):
     b = torch.cat([P[n].grad.reshape(-1).double() / (ref[n] + 1e-30) for n in P])
     return {"size": [B, H, W], "oracle_s": round(t_oracle, 1),
             "loss_rel": {k: abs(out[k].item() - L[k].item()) / abs(L[k].item()) for k in ("loss", "loss_gs", "loss_lf", "loss_is")},
-            "worst_own": top(live), "dead": top(dead, 3), "cosine": float(a @ b / (a.norm() * b.norm()))}
+            "worst_own": top(live, k), "dead": top(dead, 3), "cosine": float(a @ b / (a.norm() * b.norm()))}
 
 
 def step_vs_golden(policy):

@@ -42,6 +42,11 @@ conv("deconv1", 16, 192, 64, 128, 96, 3, up=2)
 conv("deconv2", 16, 96, 128, 256, 48, 3, up=2)
 conv("conv2", 16, 48, 256, 512, 96, 3, stride=2)
 conv("conv3", 16, 96, 128, 256, 192, 3, stride=2)
+# AdaAttN config 4 (4 triples at 256x512: 8 content images) decoder 3x3 layers and VGG19 conv4 / conv5
+conv("aa4_dec256", 8, 256, 32, 64, 256, 3)
+conv("aa4_dec128", 8, 128, 64, 128, 128, 3)
+conv("aa4_vgg4", 12, 512, 32, 64, 512, 3, pad_mode="zero")
+conv("aa4_vgg5", 12, 512, 16, 32, 512, 3, pad_mode="zero")
 # VGG conv1_1 over the kw-unfolded input (3 channels x 3 kw, padded to 16): K = 48, output-bound
 # (KW = 1 with pad 1 shifts the columns by one -- same cost as the real pad_x = 0 launch)
 SHAPES.append(("vgg1_1u.fwd", 16, 16, 256, 512, 64, 3, 1, 256, 512, 1, 1, 1, 1, 2.0 * 16 * 64 * 256 * 512 * 48))

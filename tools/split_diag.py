@@ -1,0 +1,81 @@
+"""Halo split-K vs the unsplit launch (VST_GEMM_NOSPLIT) over the shapes of the AdaAttN mid-size test
+(B=1, 128x256: VGG19 and decoder layers) for every gather mode and epilogue the training step uses:
+max |split - unsplit| / max |unsplit| per case.   python tools/split_diag.py   (GPU)"""
+import ctypes
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "video-style-transfer_amd")]
+from vst._lib import lib  # noqa: E402
+
+DEV = "cuda"
+KBLOCK, NOSPLIT = 16, 64
+GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM = 1, 2, 8, 16
+
+
+def dims(M, K):
+    mp, kp = ctypes.c_int(), ctypes.c_int()
+    lib.vst_conv_pack_dims(M, K, ctypes.byref(mp), ctypes.byref(kp))
+    return mp.value, kp.value
+
+
+def pack(w, mode, transposed):
+    Cout, Cin = w.shape[:2]
+    M = Cin if transposed else Cout
+    Mpad, Kpad = dims(M, 9 * (Cout if transposed else Cin))
+    p = torch.empty(Mpad * Kpad * 3 // 2 if (mode & 7) == 3 else Mpad * Kpad, device=DEV)
+    lib.vst_pack_weight(w.data_ptr(), p.data_ptr(), Cout, Cin, 3, 3, int(transposed), 0, Mpad, Kpad, mode,
+                        torch.cuda.current_stream().cuda_stream)
+    return p
+
+
+def conv(src, wp, M, gmode, mode, epi, bias=None, mask=None, gmask=None):
+    N, Cs, H, W = src.shape
+    out = torch.full((N, M, H, W), float("nan"), device=DEV)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    rc = lib.vst_conv_gemm_padx(src.data_ptr(), wp.data_ptr(), P(bias), P(mask), out.data_ptr(), N, Cs, H, W, M, 9 * Cs,
+                                H, W, 3, 3, gmode, 1, 1, 1, 1, epi, 0, None, P(gmask), mode,
+                                torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    return out
+
+
+def main():
+    g = torch.Generator().manual_seed(0)
+    R = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)  # noqa: E731
+    shapes = [(1, 512, 16, 32, 512), (3, 512, 16, 32, 512), (1, 512, 32, 64, 512), (1, 256, 32, 64, 256),
+              (2, 256, 16, 32, 256), (1, 128, 64, 128, 128), (1, 64, 128, 256, 64), (2, 512, 8, 16, 256),
+              (2, 256, 32, 64, 128), (2, 128, 64, 128, 64)]
+    worst = 0.0
+    for mode in (4, 3, 2):
+        for (N, Cin, H, W, Cout) in shapes:
+            x = R(N, Cin, H, W, sc=3.0)
+            w = R(Cout, Cin, 3, 3, sc=0.05)
+            b = R(Cout)
+            m = mode | KBLOCK
+            cases = []
+            wf = pack(w, m, False)
+            cases.append(("fwd reflect bias", lambda mm: conv(x, wf, Cout, GM_REFLECT, mm, EPI_BIAS, bias=b)))
+            cases.append(("fwd zero bias relu", lambda mm: conv(x, wf, Cout, GM_ZERO, mm, EPI_BIAS | EPI_RELU, bias=b)))
+            dy = R(N, Cout, H, W)
+            wt = pack(w, m, True)
+            gm, dm = R(N, Cout, H, W), R(N, Cin, H, W)
+            cases.append(("dgrad", lambda mm: conv(dy, wt, Cin, GM_TRANSPOSED, mm, 0)))
+            cases.append(("dgrad gmask mask", lambda mm: conv(dy, wt, Cin, GM_TRANSPOSED, mm, EPI_MASK, mask=dm, gmask=gm)))
+            for name, fn in cases:
+                a, u = fn(m), fn(m | NOSPLIT)
+                torch.cuda.synchronize()
+                nan = bool(torch.isnan(a).any())
+                d = float((a - u).abs().max() / u.abs().max())
+                worst = max(worst, d)
+                flag = "  <-- " if d > 1e-5 or nan else ""
+                print(f"mode {mode} {(N, Cin, H, W, Cout)} {name:18s} rel {d:.2e} nan {nan}{flag}", flush=True)
+    print("worst", worst)
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,8 @@
 // the MFMAs of tile t; one barrier per k-tile.
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "conv_gemm_kernel.h"
 #include "conv_halo_kernel.h"
@@ -25,6 +27,78 @@
 using namespace vstk;
 
 namespace {
+
+// Split-K scratch of the halo kernel: one device buffer per stream (kernels of one stream run in
+// order, so a buffer is never shared by two splits in flight), grown on demand -- the sizes of a
+// training step are fixed, so it reaches its final size in the first step.  At most
+// VST_SPLITK_MAX_BYTES per stream; a split that would need more runs unsplit.
+#ifndef VST_SPLITK_MAX_BYTES
+#define VST_SPLITK_MAX_BYTES (512l << 20)
+#endif
+float* splitk_scratch(hipStream_t st, size_t bytes) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, std::pair<float*, size_t>> bufs;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = bufs[st];
+  if (b.second < bytes) {
+    if (b.first) {
+      if (hipStreamSynchronize(st) != hipSuccess || hipFree(b.first) != hipSuccess) return nullptr;
+      b = {nullptr, 0};
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    b = {(float*)p, bytes};
+  }
+  return b.first;
+}
+
+// sum of the split-K slices part[s][n][m][p] (s in order: deterministic), then the conv epilogue.
+// Grid: x = pixel chunks of 4 x 256, y = n * M + m.
+template <bool VEC>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvParams P, int N) {
+  const int row = blockIdx.y, n = row / P.M, m = row - n * P.M;
+  const int HWo = P.Ho * P.Wo;
+  const long slice = (long)N * P.M * HWo;
+  const float* src = P.part + (long)row * HWo;
+  const int p0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p0 >= HWo) return;
+  float v[4];
+  if constexpr (VEC) {
+    float4 a = *reinterpret_cast<const float4*>(src + p0);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+    for (int s = 1; s < P.ksplit; ++s) {
+      const float4 b = *reinterpret_cast<const float4*>(src + s * slice + p0);
+      v[0] += b.x, v[1] += b.y, v[2] += b.z, v[3] += b.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = 0.f;
+      if (p0 + i < HWo)
+        for (int s = 0; s < P.ksplit; ++s) v[i] += src[s * slice + p0 + i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (p0 + i < HWo) conv_epilogue_elem(P, n, m, p0 + i, v[i]);
+}
+
+// slices for a halo launch of `wgs` blocks over `nblk` 16-channel blocks: none when the grid
+// already fills the chip; otherwise the fewest equal slices (>= 3 blocks each) that reach two
+// blocks per CU, at most four per CU
+#ifndef VST_HALO_SPLIT
+#define VST_HALO_SPLIT 1
+#endif
+int halo_ksplit(long wgs, int nblk) {
+  if (!VST_HALO_SPLIT || wgs >= 512) return 1;
+  int best = 1;
+  for (int s : {2, 3, 4, 6, 8}) {
+    if (nblk % s || nblk / s < 3 || wgs * s > 1024) continue;
+    best = s;
+    if (wgs * s >= 512) break;
+  }
+  return best;
+}
 
 // ---------------------------------------------------------------------------------------------
 // fwd:        A[k = (kh*KW+kw)*Cin + ci][m = co]
@@ -377,12 +451,32 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     P.fd_KW = make_fastdiv(KW);
     P.kb = 1;
     const int tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
-    dim3 grid(tiles, P.Mpad / bm, N);
     hipStream_t st = (hipStream_t)stream;
+    // split-K when the grid is too small for the chip (AdaAttN config 4's decoder and VGG19 conv4 /
+    // conv5 layers: 128-384 blocks).  Not under fp16: every split launch matches its unsplit launch
+    // to <= 3e-6 (tools/split_diag.py), but the fp16 AdaAttN step amplifies that summation-order change
+    // in its attention-parameter gradients past its own parity bars
+    const bool kc1 = am == VST_GEMM_BF16X6 || VST_HALO_KC == 1 || !halo_db_c(hcfg);
+    int S = (kc1 && am != VST_GEMM_F16 && !(mode & VST_GEMM_NOSPLIT)) ? halo_ksplit((long)tiles * (P.Mpad / bm) * N, Cs / 16) : 1;
+    const size_t part_bytes = (size_t)S * N * M * Ho * Wo * sizeof(float);
+    if (S > 1 && part_bytes <= (size_t)VST_SPLITK_MAX_BYTES) {
+      P.part = splitk_scratch(st, part_bytes);
+      if (!P.part) return (int)hipErrorOutOfMemory;
+      P.ksplit = S;
+    } else {
+      S = 1;
+    }
+    dim3 grid(tiles, P.Mpad / bm, N * S);
     const bool gm = gmask != nullptr;
     if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, hcfg, grid, st, P);
     else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, hcfg, grid, st, P);
     else launch_halo_prec<2>(gm, hcfg, grid, st, P);
+    if (S > 1) {
+      const int HWo = Ho * Wo;
+      dim3 rgrid((HWo + 1023) / 1024, N * M);
+      if (HWo % 4 == 0) splitk_reduce_kernel<true><<<rgrid, 256, 0, st>>>(P, N);
+      else splitk_reduce_kernel<false><<<rgrid, 256, 0, st>>>(P, N);
+    }
     return vst_launch_status();
   }
   int bm = cfg_bm(cfg), bn = cfg_bn(cfg);

@@ -55,6 +55,11 @@ struct ConvParams {
   int ph_H, ph_W, ph_pad;
   FastDiv fd_Wo, fd_Cs, fd_KW;
   int kb;  // channel-blocked K order (VST_GEMM_KBLOCK, vst_common.h kdecode)
+  // split-K of the halo kernel (conv_halo_kernel.h): blockIdx.z = n * ksplit + s, slice s sums its
+  // share of the 16-channel blocks into part[s][n][M][Ho Wo] (raw accumulators); the reduce kernel
+  // adds the slices in order and applies the epilogue
+  int ksplit = 1;
+  float* part = nullptr;
 };
 
 enum { GM_REFLECT = 0, GM_ZERO = 1, GM_TRANSPOSED = 2, GM_CLAMP = 3 };
@@ -181,6 +186,35 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 
       }
     }
   }
+}
+
+// conv_epilogue for one output element (row m, output pixel pp of image n) given its accumulated
+// value: the paths the halo kernel can take (no EPI_AFFINE, no EPI_PHASE2), for the split-K reduce.
+__device__ __forceinline__ void conv_epilogue_elem(const ConvParams& P, int n, int m, int pp, float v) {
+  const int HWo = P.Ho * P.Wo;
+  if (P.epi & EPI_PADOUT) {
+    const int I = (int)fdiv((uint32_t)pp, P.fd_Wo), J = pp - I * P.Wo;
+    const int y = I - P.ph_pad, x = J - P.ph_pad;
+    if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W) {
+      const long o = ((long)n * P.M + m) * P.ph_H * P.ph_W + (long)y * P.ph_W + x;
+      P.out[o] = ((P.epi & EPI_MASK) && !(P.mask[o] > 0.f)) ? 0.f : v;
+    } else {
+      const int Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
+      P.ph_border[(((long)n * P.M + m) * Hp + I) * Wp + J] = v;
+    }
+    return;
+  }
+  if (P.epi & EPI_BIAS) v += P.bias[m];
+  if (P.epi & EPI_RELU) v = fmaxf(v, 0.f);
+  const long o = ((long)n * P.M + m) * HWo + pp;
+  if (P.epi & EPI_TANH) {
+    const float t = tanhf(v / 255.0f);
+    if (P.aux) P.aux[o] = t;
+    v = t * 150.0f + 127.5f;
+  }
+  if (P.epi & EPI_MASK) v = P.mask[o] > 0.f ? v : 0.f;
+  if (P.epi & EPI_ACCUM) v += P.out[o];
+  P.out[o] = v;
 }
 
 // float4 slot (row*4 + quad) of A-tile element idx: 8 consecutive lanes take 8 consecutive rows of

@@ -102,9 +102,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   const int gx = gridDim.x, gy = gridDim.y;
   const int wk = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   const int rest = __builtin_amdgcn_readfirstlane(wk / gy);
-  const int n = __builtin_amdgcn_readfirstlane(rest / gx);
+  const int nz = __builtin_amdgcn_readfirstlane(rest / gx);
   const int m0 = __builtin_amdgcn_readfirstlane((wk - rest * gy) * BM);
-  const int tile = __builtin_amdgcn_readfirstlane(rest - n * gx);
+  const int tile = __builtin_amdgcn_readfirstlane(rest - nz * gx);
+  // split-K: image n, slice s of the channel blocks (ConvParams::ksplit)
+  const int n = __builtin_amdgcn_readfirstlane(nz / P.ksplit), ks = nz - n * P.ksplit;
   const int tiles_x = (P.Wo + HTW - 1) / HTW;
   const int ty = __builtin_amdgcn_readfirstlane(tile / tiles_x);
   const int oy0 = ty * TH, ox0 = (tile - ty * tiles_x) * HTW;
@@ -201,13 +203,15 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  const int nst = P.Cs / (16 * KC);
-  load_patch(0);
-  load_a(0, arC);
+  const int nst_all = P.Cs / (16 * KC);
+  const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
+  const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
+  load_patch(st0);
+  load_a(9 * KC * st0, arC);
   store_patch(0);
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = DB ? (st & 1) : 0;
+  for (int st = st0; st < nst; ++st) {
+    const int buf = DB ? ((st - st0) & 1) : 0;
     if (st + 1 < nst) load_patch(st + 1);
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
@@ -238,6 +242,20 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   for (int j = 0; j < TN; ++j) {
     const int oy = oy0 + 4 * wn + j, ox = ox0 + lo;
     pix[j] = (oy < P.Ho && ox < P.Wo) ? oy * P.Wo + ox : -1;
+  }
+  if (P.ksplit > 1) {  // raw partial sums of this slice: part[ks][n][m][pixel]
+    const long HWo = (long)P.Ho * P.Wo;
+    float* pt = P.part + (long)(ks * (gridDim.z / P.ksplit) + n) * P.M * HWo;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (pix[j] < 0) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (m < P.M) pt[m * HWo + pix[j]] = acc[0][j][r];
+      }
+    }
+    return;
   }
   conv_epilogue<TM, TN>(P, acc, n, m0 + wm * 32, pix, hi);
 }
@@ -276,12 +294,15 @@ inline int halo_wn(int c) { return halo_wn_c(c); }
 // 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster
 // there: the bf16x6 residual data gradient over the padded grid, whose 130-column rows waste a
 // fifth of a 32-column tile grid)
+#ifndef VST_HALO_X6_PADOUT
+#define VST_HALO_X6_PADOUT 0  // 1: the bf16x6 residual padded-grid dgrad on the halo kernel (config 3: 47.61 vs 47.23 ms per-tap)
+#endif
 inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
   int c;
   if (M <= 64) c = VST_HALO_M64;
   else if (M % 256 == 0) c = VST_HALO_M256;
   else if (M % 192 == 0 && M % 128 != 0) {
-    if (bf16x6 && padout) return 0;
+    if (bf16x6 && padout && !VST_HALO_X6_PADOUT) return 0;
     c = VST_HALO_M192;
   } else c = VST_HALO_M128;
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;

@@ -68,7 +68,7 @@ static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int vst_mode_arith(int mode) { return mode & 7; }
 static inline bool vst_mode_ok(int mode) {
   const int a = vst_mode_arith(mode);
-  return (mode & ~(VST_GEMM_KBLOCK | VST_GEMM_PERTAP | 7)) == 0 &&
+  return (mode & ~(VST_GEMM_KBLOCK | VST_GEMM_PERTAP | VST_GEMM_NOSPLIT | 7)) == 0 &&
          (a == VST_GEMM_F32 || a == VST_GEMM_BF16X3 || a == VST_GEMM_BF16 || a == VST_GEMM_BF16X6 ||
           a == VST_GEMM_F16);
 }

@@ -13,7 +13,9 @@ import re
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvst_hip.so")
+# VST_LIB_PATH: a library built from the same sources with other compile-time choices (csrc/Makefile
+# VARIANT_FLAGS), for A/B step measurements only (tools/gpu_r04_*.sh)
+LIB_PATH = os.environ.get("VST_LIB_PATH") or os.path.join(_HERE, "libvst_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "vst_hip.h")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
