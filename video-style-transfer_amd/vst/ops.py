@@ -248,7 +248,7 @@ def pack_dims(M, K):
 # frozen (requires_grad=False) weights: packs cached per weight OBJECT (weak keys, so a freed
 # tensor's entry dies with it and a new tensor at a recycled address never hits a stale pack),
 # validated against the tensor's version counter (in-place updates / load_state_dict re-pack).
-_PACK_CACHE = {}  # id(w) -> (weakref(w), {key: pack})
+_PACK_CACHE = {}  # id(w) -> (weakref(w), {key: (pack, event after the pack, stream it was packed on)})
 
 
 def _cache_entry(w):
@@ -265,7 +265,14 @@ def packed_weight(w, transposed, split_kh=False, kwu=False):
     if not w.requires_grad:
         hit = _cache_entry(w).get(key)
         if hit is not None:
-            return hit
+            out, done, made_on = hit
+            if done is not None and made_on != stream():
+                # packed on another stream (the side stream's content pass shares the loss net's
+                # packs): wait for the pack, and keep the buffer from reuse until this stream is done
+                cur = torch.cuda.current_stream(out.device)
+                cur.wait_event(done)
+                out.record_stream(cur)
+            return out
     Cout, Cin, KH, KW = w.shape
     if kwu:
         Cu = kwu_channels(Cout if transposed else Cin, KW)
@@ -283,7 +290,11 @@ def packed_weight(w, transposed, split_kh=False, kwu=False):
                             stream())
     if not w.requires_grad:
         entry = {k: v for k, v in _cache_entry(w).items() if k[0] == key[0] and k[1] == key[1]}
-        entry[key] = out
+        done = None
+        if out.is_cuda:
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(out.device))
+        entry[key] = (out, done, stream() if out.is_cuda else None)
         wid = id(w)
         _PACK_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _PACK_CACHE.pop(wid, None)), entry)
     return out
@@ -593,6 +604,53 @@ def wgrad_into_sink(compute, sink, *used):
         t.record_stream(side)
     torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
     return sink
+
+
+CONTENT_SIDE = os.environ.get("VST_CONTENT_SIDE", "1") != "0"  # A/B: input-only targets on the side stream
+
+
+class _SideBranch:
+    """`with side_branch(*inputs) as side:` runs its body (no-grad work that depends on `inputs`
+    only) on the device's side stream, beside what the current stream does next; `side.produced(*t)`
+    names the tensors the body made (their memory is then recorded on the current stream, which
+    reads and frees them), `side.join()` makes the current stream wait for the body before it reads
+    them.  On CPU tensors (or with VST_CONTENT_SIDE=0) the body runs in line."""
+
+    def __init__(self, inputs):
+        ts = [t for t in inputs if isinstance(t, torch.Tensor)]
+        self.on = CONTENT_SIDE and bool(ts) and ts[0].is_cuda
+        self.inputs, self.ctx, self.made = ts, None, []
+        if self.on:
+            dev = ts[0].device
+            self.main, self.side = torch.cuda.current_stream(dev), _side_stream(dev)
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            for t in self.inputs:
+                t.record_stream(self.side)
+            self.ctx = torch.cuda.stream(self.side)
+            self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+            self.ctx = None
+        return False
+
+    def produced(self, *ts):
+        self.made = [t for t in ts if isinstance(t, torch.Tensor)]
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in self.made:
+                t.record_stream(self.main)
+
+
+def side_branch(*inputs):
+    return _SideBranch(inputs)
 
 
 class Conv2dFn(Function):

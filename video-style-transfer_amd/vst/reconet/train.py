@@ -119,17 +119,22 @@ class ReCoNetTrainer:
             x, nf = frames.reshape(2 * B, C, H, W), 2
             if self.temporal and (flow is None or mask is None):
                 raise ValueError("the temporal terms need flow and mask")
+        # the content targets (normalized frames, their VGG features, the warped frame) depend on
+        # the inputs only: computed on the side stream beside the stylizer's forward
+        with ops.side_branch(x, flow) as side:
+            with torch.no_grad():
+                i_n = ops.VggNormalizeFn.apply(x if C == 3 else x[:, C - 3:].contiguous())
+                # the content loss reads relu3_3 only (train_candy.py:126-128): the content pass stops
+                # after slice 3 when the loss net supports it
+                upto = getattr(self.vgg, "features_upto", None)
+                cf = upto(i_n, 3) if upto is not None else self.vgg(i_n)
+                warped_i = ops.warp(i_n[:B], flow) if "OTL" in self.terms else None
+            side.produced(i_n, *cf, warped_i)
         mout = self.model(x)
         fmap, styled = mout[-2], mout[-1]
         s_n = ops.VggNormalizeFn.apply(styled)
-        with torch.no_grad():
-            i_n = ops.VggNormalizeFn.apply(x if C == 3 else x[:, C - 3:].contiguous())
         sf = self.vgg(s_n)
-        with torch.no_grad():
-            # the content loss reads relu3_3 only (train_candy.py:126-128): the content pass stops
-            # after slice 3 when the loss net supports it
-            upto = getattr(self.vgg, "features_upto", None)
-            cf = upto(i_n, 3) if upto is not None else self.vgg(i_n)
+        side.join()
         out = {}
         if "FTL" in self.terms:
             Hf, Wf = fmap.shape[2:]
@@ -139,8 +144,6 @@ class ReCoNetTrainer:
             out["FTL"] = ops.feature_temporal_loss(fmap[B:], warped_f, fmask, w["LAMBDA_F"])
         if "OTL" in self.terms:
             warped_s = ops.warp(s_n[:B], flow)
-            with torch.no_grad():
-                warped_i = ops.warp(i_n[:B], flow)
             out["OTL"] = ops.output_temporal_loss(s_n[B:], warped_s, i_n[B:], warped_i, mask, w["LAMBDA_O"])
         # mean over the nf*B batch x nf = the reference's sum of nf per-frame means
         out["CL"] = ops.mse(sf[2], cf[2], nf * w["ALPHA"])
