@@ -137,6 +137,14 @@ class AdaAttNTrainer:
         # frames' and the style's, the AdaAttnNoConv loss targets frame 1's (the first half of the
         # content batch) and the style's (the first half when the style side is doubled)
         down = _down_sampled(fc12, fs2)
+        # the local-feature targets (AdaAttnNoConv over frame 1's and the style's data features) depend
+        # on the data only: computed on the side stream beside the stylizer and its VGG pass
+        l1, ls = list(fc1.values()), list(fs.values())
+        args = [(l1[i], ls[i], down[0][i][:B], down[1][i][:B]) for i in (2, 3, 4)]
+        with ops.side_branch(*[t for a in args for t in a]) as side:
+            with torch.no_grad():
+                targets = [self.noconv[i](*args[i]) for i in range(3)]
+            side.produced(*targets)
         fcs = self.vgg(self.model(fc12, fs2, down=down))  # cs1 ++ cs2
         halves = {k: _halves(v, B) for k, v in fcs.items()}
         fcs1 = {k: h[0] for k, h in halves.items()}
@@ -145,13 +153,10 @@ class AdaAttNTrainer:
         for k in FEATURES[1:]:
             t = global_stylized_loss(fcs1[k], fs[k], weight=w["LAMBDA_G"])
             gs = t if gs is None else gs + t
-        l1, ls = list(fc1.values()), list(fs.values())
+        side.join()
         lf = None
         for i in range(3):
-            idx = i + 2
-            with torch.no_grad():
-                target = self.noconv[i](l1[idx], ls[idx], down[0][idx][:B], down[1][idx][:B])
-            t = local_feature_loss(fcs1[FEATURES[idx]], target, weight=w["LAMBDA_L"])
+            t = local_feature_loss(fcs1[FEATURES[i + 2]], targets[i], weight=w["LAMBDA_L"])
             lf = t if lf is None else lf + t
         isl = None
         for k in FEATURES[1:4]:
