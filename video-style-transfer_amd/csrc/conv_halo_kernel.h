@@ -266,8 +266,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 //   M = 64  (VGG conv1_x, 256x512): 2x2 one buffer 746-758 us < 2x2 double 878 < 2x1 902 < per-tap 1071
 //   M = 128 (VGG conv2_x): 4x1 619-664 < 4x2 685 < per-tap 751
 //   M = 192 (ReCoNet residual, 64x128): 2x4 one buffer 354-391 us (fp16 110-118) < per-tap 413-452
-//           (LDS-A tile) < 3x2 415-428, 6x1 428, 3x1 448; the padded-grid data gradient stays
-//           per-tap (bf16x6)
+//           (LDS-A tile) < 3x2 415-428, 6x1 428, 3x1 448; re-measured on one box:
+//           2x2 one buffer 339 us (fp16 121) < 2x4 one buffer 363 (125) < 3x1 one buffer 379 (121);
+//           the padded-grid data gradient 474 us on 2x2 one buffer (544 on 2x4): config 3 46.12 ms
+//           with it on the halo kernel vs 46.61 per-tap (profiles/r04_halo_m192.txt)
 //   2x4 one-buffer everywhere: 128-row layers 839 us, 256-row 695-770; 4x2 one-buffer: 932-1172 --
 //   both slower than 4x1 / 8x1 (profiles/r04_halo_shapes.txt)
 //   M = 256-multiples (VGG conv3_x / conv4_x): 8x1, 268-274 TF/s vs per-tap 233-245
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #define VST_HALO_M128 4
 #endif
 #ifndef VST_HALO_M192
-#define VST_HALO_M192 9
+#define VST_HALO_M192 3
 #endif
 #ifndef VST_HALO_M256
 #define VST_HALO_M256 8  // 256-row multiples
@@ -291,11 +293,11 @@ constexpr int halo_wn_c(int c) { return c == H2x4S ? 4 : (c == H2x2 || c == H2x2
 constexpr bool halo_db_c(int c) { return !(c == H2x2S || c == H2x4S || c == H3x1S || c == H3x2S || c == H4x2S); }
 inline int halo_wm(int c) { return halo_wm_c(c); }
 inline int halo_wn(int c) { return halo_wn_c(c); }
-// 0: the per-tap kernel (the M tile would not divide the pack's Mpad, or the shape measured faster
-// there: the bf16x6 residual data gradient over the padded grid, whose 130-column rows waste a
-// fifth of a 32-column tile grid)
+// 0: the per-tap kernel (the M tile would not divide the pack's Mpad; or, with VST_HALO_X6_PADOUT 0,
+// the bf16x6 residual data gradient over the padded grid, whose 66 x 130 grid wastes a fifth of a
+// 32-column tile grid -- slower than per-tap on the 2x4 block, faster on the 2x2 one)
 #ifndef VST_HALO_X6_PADOUT
-#define VST_HALO_X6_PADOUT 0  // 1: the bf16x6 residual padded-grid dgrad on the halo kernel (config 3: 47.61 vs 47.23 ms per-tap)
+#define VST_HALO_X6_PADOUT 1  // the bf16x6 residual padded-grid dgrad on the halo kernel (measured above)
 #endif
 inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
   int c;
