@@ -672,10 +672,18 @@ def main():
         step()
     # headline: K uninstrumented steps
     elapsed, out = timed(step, args.steps, world, dev, mark=True)
-    # roofline: a second run of the same step with HIP events around every conv_gemm launch
+    # roofline: a second run of the same step with HIP events around every conv_gemm launch, the side
+    # streams off so that each launch has the chip to itself: its duration is
+    # the kernel's, not shared with a concurrent weight-gradient GEMM (the timed region above runs them
+    # on; tools/gpu_r04_close.sh profiles with the same switches so the rocprofv3 averages compare)
     timer = kprof.KernelTimer()
-    with timer:
-        prof_elapsed, _ = timed(step, args.prof_steps, world, dev)
+    side = (ops.WGRAD_SIDE, ops.CONTENT_SIDE)
+    ops.WGRAD_SIDE = ops.CONTENT_SIDE = False
+    try:
+        with timer:
+            prof_elapsed, _ = timed(step, args.prof_steps, world, dev)
+    finally:
+        ops.WGRAD_SIDE, ops.CONTENT_SIDE = side
     ks = timer.summary()
     loss = float(out["loss"].item()) if "loss" in out else None
 
@@ -735,7 +743,7 @@ def main():
                          "algo_bytes_per_launch": ks["bytes"] / max(ks["launches"], 1),
                          "launches": ks["launches"], "avg_launch_us": ks["avg_us"],
                          "algo_gflop_per_launch": ks["flops"] / max(ks["launches"], 1) / 1e9,
-                         "measured_over": f"{args.prof_steps} instrumented steps after the timed region "
+                         "measured_over": f"{args.prof_steps} instrumented steps after the timed region, side streams off "
                                           f"({1e3 * prof_elapsed / max(args.prof_steps, 1):.2f} ms/step instrumented)",
                          "share_of_step": ks["total_ms"] / max(1e3 * prof_elapsed, 1e-9)},
         }

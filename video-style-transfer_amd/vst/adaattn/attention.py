@@ -96,7 +96,7 @@ def _ones(n, like):
     key = (like.device, n)
     v = _ONES.get(key)
     if v is None:
-        v = torch.ones(n, device=like.device, dtype=torch.float32)
+        v = ops.persistent(torch.ones(n, device=like.device, dtype=torch.float32))
         _ONES[key] = v
     return v
 
@@ -462,6 +462,6 @@ def instance_norm_plain(x, eps=1e-5):
     key = (x.device, C)
     wb = _AFFINE_ID.get(key)
     if wb is None:
-        wb = (torch.ones(C, device=x.device), torch.zeros(C, device=x.device))
+        wb = (torch.ones(C, device=x.device), ops.persistent(torch.zeros(C, device=x.device)))
         _AFFINE_ID[key] = wb
     return ops.instance_norm(x, wb[0], wb[1], eps=eps)

@@ -653,6 +653,15 @@ def side_branch(*inputs):
     return _SideBranch(inputs)
 
 
+def persistent(t):
+    """A lazily created constant kept in a module-level cache (read afterwards from either stream):
+    its fill kernels complete before it is handed out, so a first use on the side stream cannot race
+    the current stream's reads (one synchronisation per constant, on first creation only)."""
+    if t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
+    return t
+
+
 class Conv2dFn(Function):
     """[nearest x`up` upsample] -> (reflect|zero) pad -> Conv2d(ks, stride) [+bias] [-> ReLU | ReCoNet tanh].
     Replaces RC/network.py:72-75 (ConvLayer), 114-120 (UpsampleConvLayer), 83-85 (ConvTanh) and the
