@@ -566,6 +566,8 @@ def grad_sink(p):
 
 WGRAD_SIDE = os.environ.get("VST_WGRAD_SIDE", "1") != "0"  # A/B: weight gradients on a second stream
 _SIDE = {}
+_SIDE_SINKS = set()  # data_ptr of the gradients accumulated on a side stream since the last join
+FIRST_INLINE = os.environ.get("VST_FIRST_INLINE", "1") != "0"  # A/B: no-data-gradient layers' wgrad in line
 
 
 def _side_stream(dev):
@@ -581,9 +583,10 @@ def join_side_streams():
     gradient)."""
     for dev, s in _SIDE.items():
         torch.cuda.current_stream(dev).wait_stream(s)
+    _SIDE_SINKS.clear()
 
 
-def wgrad_into_sink(compute, sink, *used):
+def wgrad_into_sink(compute, sink, *used, overlap=True):
     """Run `compute()` -- a weight-gradient GEMM accumulating into the leaf gradient `sink` -- on a
     second HIP stream of the device.  A layer's weight gradient is read only by the optimizer, its
     data gradient by the next layer back, so the wgrad GEMMs (latency-bound, about a third
@@ -592,9 +595,14 @@ def wgrad_into_sink(compute, sink, *used):
     stream (the inputs `used` and the zeroed sink are ready), `used` are recorded on it so the
     caching allocator keeps them until it is done, and a final callback of the backward pass makes
     the caller's stream wait for it (so `.grad` and the optimizer see the finished gradients).
-    Gradients returned to autograd (no sink) stay on the current stream."""
+    Gradients returned to autograd (no sink) stay on the current stream, and so does the weight
+    gradient of a layer with no data gradient (`overlap=False`: the network's first conv), which then
+    runs beside the previous layer's weight gradient still on the side stream."""
     if not (WGRAD_SIDE and sink is not None and sink.is_cuda):
         return compute()
+    if FIRST_INLINE and not overlap and sink.data_ptr() not in _SIDE_SINKS:  # (else: keep the sink's writes in order)
+        return compute()
+    _SIDE_SINKS.add(sink.data_ptr())
     dev = sink.device
     side = _side_stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -752,10 +760,11 @@ class Conv2dFn(Function):
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
             if rowsplit_wgrad_ok(w.shape[0], w.shape[1], ks, stride, pad_mode, up, x.shape[3]) and pad == ks // 2:
-                dw = wgrad_into_sink(lambda: conv_wgrad_rowsplit(gz, x, w.shape, out=sink), sink, gz, x)
+                dw = wgrad_into_sink(lambda: conv_wgrad_rowsplit(gz, x, w.shape, out=sink), sink, gz, x,
+                                     overlap=ctx.needs_input_grad[0])
             else:
                 dw = wgrad_into_sink(lambda: conv_wgrad(gz, x, w.shape, ks, stride, pad, pad_mode, up, out=sink),
-                                     sink, gz, x)
+                                     sink, gz, x, overlap=ctx.needs_input_grad[0])
             dw = None if sink is not None else dw
         if ctx.has_bias and ctx.needs_input_grad[2]:
             sink = grad_sink(ctx.params[1])
