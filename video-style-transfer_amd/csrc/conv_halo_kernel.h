@@ -77,7 +77,7 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // waiting on memory at KC = 1, profiles/r04_mfma_busy_adaattn_c5.json).  Measured, it does not pay:
 // fp16 VGG + residual shapes 2.38 ms at KC = 1, 2.58 ms at 2, 2.61 ms at 4 (the larger stage halves the
 // blocks per CU; profiles/r04_halo_kc.txt), so VST_HALO_KC stays 1 (KC > 1 kept for the record).
-template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1>
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1, int PD = 1>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo kernel: bf16x6, bf16 or fp16 products");
   constexpr int TM = 1, TN = 4;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   float rv[KC][TIT][8];
   float rgv[KC][TIT][GM ? 8 : 1];
   // stage s = channel blocks KC s .. KC s + KC - 1 (Cs / 16 is a multiple of KC: the launcher checks)
-  auto load_patch = [&](int st) {
+  auto load_into = [&](int st, auto& R, auto& G) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int cb_off = __builtin_amdgcn_readfirstlane((st * KC + kc) * 16 * plane * 4);
@@ -162,14 +162,14 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       for (int it = 0; it < TIT; ++it)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          rv[kc][it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
+          R[kc][it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
           if constexpr (GM)
-            rgv[kc][it][i] =
+            G[kc][it][i] =
                 __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
         }
     }
   };
-  auto store_patch = [&](int buf) {
+  auto store_from = [&](int buf, auto& R, auto& G) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       if (NTASK % NTT != 0 && t_lds[it] < 0) continue;
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = GM ? (rgv[kc][it][i] > 0.f ? rv[kc][it][i] : 0.f) : rv[kc][it][i];
+      for (int i = 0; i < 8; ++i) v[i] = GM ? (G[kc][it][i] > 0.f ? R[kc][it][i] : 0.f) : R[kc][it][i];
       uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][kc][0][0]) + t_lds[it];
       if constexpr (PREC == 3) {
         uint32_t h[4], md[4], l[4];
@@ -206,13 +206,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   const int nst_all = P.Cs / (16 * KC);
   const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
   const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
-  load_patch(st0);
-  load_a(9 * KC * st0, arC);
-  store_patch(0);
-  __syncthreads();
-  for (int st = st0; st < nst; ++st) {
-    const int buf = DB ? ((st - st0) & 1) : 0;
-    if (st + 1 < nst) load_patch(st + 1);
+  // the nine taps of every channel block of stage st, B fragments from patch buffer buf
+  auto taps = [&](int st, int buf) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int cb = st * KC + kc;
@@ -230,11 +225,41 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
         for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
       }
     }
-    if (st + 1 < nst) {
-      if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
-      store_patch(DB ? buf ^ 1 : 0);
-    }
+  };
+  load_into(st0, rv, rgv);
+  load_a(9 * KC * st0, arC);
+  store_from(0, rv, rgv);
+  if constexpr (PD == 1) {
     __syncthreads();
+    for (int st = st0; st < nst; ++st) {
+      const int buf = DB ? ((st - st0) & 1) : 0;
+      if (st + 1 < nst) load_into(st + 1, rv, rgv);
+      taps(st, buf);
+      if (st + 1 < nst) {
+        if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
+        store_from(DB ? buf ^ 1 : 0, rv, rgv);
+      }
+      __syncthreads();
+    }
+  } else {
+    // two patches in flight: stage st + 2's loads are issued before stage st's taps, into the
+    // register set stage st + 1 is not stored from (the two sets alternate, loop unrolled by two)
+    static_assert(PD == 2 && DB, "depth-2 patch prefetch: double-buffered tiles");
+    float rvN[KC][TIT][8];
+    float rgvN[KC][TIT][GM ? 8 : 1];
+    if (st0 + 1 < nst) load_into(st0 + 1, rv, rgv);
+    __syncthreads();
+    auto stage = [&](int st, auto& Rs, auto& Gs, auto& Rl, auto& Gl) {
+      const int buf = (st - st0) & 1;
+      if (st + 2 < nst) load_into(st + 2, Rl, Gl);
+      taps(st, buf);
+      if (st + 1 < nst) store_from(buf ^ 1, Rs, Gs);
+      __syncthreads();
+    };
+    for (int st = st0; st < nst; st += 2) {
+      stage(st, rv, rgv, rvN, rgvN);
+      if (st + 1 < nst) stage(st + 1, rvN, rgvN, rv, rgv);
+    }
   }
 
   int pix[TN];
@@ -313,6 +338,12 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
 #ifndef VST_HALO_KC
 #define VST_HALO_KC 1  // channel blocks per stage for the single-product modes (measured above)
 #endif
+#ifndef VST_HALO_SMINW_SP
+#define VST_HALO_SMINW_SP 4  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
+#endif
+#ifndef VST_HALO_PD
+#define VST_HALO_PD 2  // patches in flight for the single-product double-buffered tiles
+#endif
 template <int C, int PR, bool GM>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
@@ -323,14 +354,20 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // budget (measured: the spilling 2x2 tile 1088 us vs 758 us at 3 waves per SIMD on the 64-row VGG
   // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
   // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
-  constexpr int MINW = !halo_db_c(C) ? (PR == 3 ? 3 : 4) : (WM * WN <= 4 ? 3 : 2);
+  constexpr int MINW = !halo_db_c(C) ? (PR == 3 ? 3 : VST_HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
   if constexpr (KC > 1) {
     if ((P.Cs / 16) % KC != 0) {  // (a channel count that does not fill whole stages)
       conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), 1><<<grid, WM * WN * 64, 0, st>>>(P);
       return;
     }
   }
-  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC><<<grid, WM * WN * 64, 0, st>>>(P);
+  // depth-2 patch prefetch for the 8-wave single-product tiles (config 5: the fp16 tiles wait on the
+  // next patch's gather; fp16 shapes, one box: AdaAttN decoder 256-row 69 -> 53 us, VGG conv4 150 ->
+  // 144, conv5 123 -> 89; config 5 145.07 -> 141.5 ms, profiles/r04_halo_pd.txt).  Not on the 4-wave
+  // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
+  // bf16x6 (MFMA-bound, registers spoken for)
+  constexpr int PD = (PR != 3 && halo_db_c(C) && KC == 1 && WM * WN >= 8) ? VST_HALO_PD : 1;
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC, PD><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 // only the block shapes the build's selection can reach are instantiated
