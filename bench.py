@@ -10,6 +10,17 @@ Adam — config 3 of BASELINE.json.  `--config 2` runs the reference's no-tempor
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL all-reduce)
 
+`python bench.py --gpus N` with N > 1 outside torchrun starts the N ranks itself: before any GPU
+call it runs `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port P bench.py <same arguments>` as a child process and relays rank 0's JSON line (exit
+code = the child's).  Under torchrun, `--gpus` must equal WORLD_SIZE.  `--dry-run` replaces the
+training step with a CPU stand-in (gloo gradient all-reduce) to test that launcher on a machine
+without GPUs.
+
+Inputs: every step trains on its own synthetic batch, numpy PCG64 seeded 1234 + step on rank 0
+([1234 + step, rank] on the others), all generated and staged in HBM before the
+timed region.
+
 GEMM arithmetic (`--gemm`, vst.ops.POLICIES): the headline runs `bf16x6` -- every conv / Gram
 product on three-way split bf16 MFMAs, per-product error ~2^-24 (fp32-class; the reference's
 golden steps pass at the f32 bar under it, tests/test_gpu_parity.py) at 2500/6 = 417 TFLOP/s
@@ -42,7 +53,10 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (GPUs of this node); > 1 outside torchrun: bench.py launches them itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU stand-in step over gloo (tests the multi-rank launcher and timing without GPUs)")
     ap.add_argument("--steps", type=int, default=150)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--prof-steps", type=int, default=10, help="instrumented steps for the roofline line")
@@ -357,9 +371,8 @@ def vgg19_subbench(dev, reps=3, B=8, H=256, W=512):
 def build_reconet(args, dev, rank):
     from vst import ops
     from vst.reconet import network as N
-    from vst.reconet.dist import shard_seed
     from vst.reconet.train import ReCoNetTrainer
-    from vst.synthetic import frame_pair_batch, style_image
+    from vst.synthetic import frame_pair_parts, style_image
 
     model = N.ReCoNet().to(dev)
     vgg = N.Vgg16().to(dev)
@@ -368,16 +381,17 @@ def build_reconet(args, dev, rank):
     script = "train_coco2014" if args.config == 2 else "train_candy"
     trainer = ReCoNetTrainer.for_script(script, model, vgg, style)
 
-    def hip_mask(f01, f10):
-        return ops.flow_warp_mask(f01.to(dev), f10.to(dev))
+    def stage(parts):
+        img1, img2, f01, f10, motion = (t.to(dev) for t in parts)
+        frames = torch.stack([img1, img2]).contiguous()
+        if trainer.single:  # config 2: the 2B frames of the B pairs as single images
+            return (frames.reshape(2 * B, 3, H, W),)
+        # occlusion mask on the device (RC/utilities.py:60-90) x the motion stand-in
+        mask = torch.stack([ops.flow_warp_mask(f01[b], f10[b]) for b in range(B)]) * motion
+        return frames, f10.contiguous(), mask.contiguous()
 
-    img1, img2, flow, mask = frame_pair_batch(shard_seed(1234, rank), B, H, W, mask_fn=hip_mask, device=dev)
-    frames = torch.stack([img1, img2]).contiguous()
-    del img1, img2
-    if trainer.single:  # config 2: the 2B frames of the B pairs as single images
-        frames = frames.reshape(2 * B, 3, H, W)
-        return lambda: trainer.step(frames)
-    return lambda: trainer.step(frames, flow, mask)
+    batches = per_step_batches(args, rank, lambda seed: frame_pair_parts(seed, B, H, W), stage)
+    return cycle_steps(trainer.step, batches)
 
 
 def full_size_parity(args, dev, first):
@@ -437,16 +451,48 @@ def build_adaattn(args, dev, rank):
     from vst.adaattn.network import StylizingNetwork
     from vst.adaattn.train import AdaAttNTrainer
     from vst.adaattn.vgg19 import VGG19
-    from vst.reconet.dist import shard_seed
     from vst.synthetic import content_style_batch
 
     model = StylizingNetwork("cosine").to(dev)
     vgg = VGG19().to(dev)
     trainer = AdaAttNTrainer(model, vgg, activation="cosine")
-    c1, c2, s = content_style_batch(shard_seed(1234, rank), args.batch, args.height, args.width, device=dev)
-    triple = torch.stack([c1, c2, s]).contiguous()
-    del c1, c2, s
-    return lambda: trainer.step(triple)
+    B, H, W = args.batch, args.height, args.width
+    batches = per_step_batches(args, rank, lambda seed: content_style_batch(seed, B, H, W),
+                               lambda cs: (torch.stack([c.to(dev) for c in cs]).contiguous(),))
+    return cycle_steps(trainer.step, batches)
+
+
+def per_step_batches(args, rank, draw, stage):
+    """One synthetic batch per step (warm-up, timed and instrumented steps), seeded
+    vst.reconet.dist.step_seed(step, rank) = 1234 + step on rank 0; drawn on host
+    threads (numpy releases the GIL in its fills), staged in HBM before the timed region."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from vst.reconet.dist import step_seed
+
+    n = args.warmup + args.steps + args.prof_steps
+    ranks_here = max(int(os.environ.get("LOCAL_WORLD_SIZE", "1")), 1)
+    workers = max(1, min(8, (os.cpu_count() or 1) // ranks_here))
+    t0 = time.perf_counter()
+    out = []
+    with ThreadPoolExecutor(workers) as ex:
+        for c0 in range(0, n, 2 * workers):  # bounded host memory: 2 x workers batches in flight
+            for parts in ex.map(lambda i: draw(step_seed(i, rank)), range(c0, min(n, c0 + 2 * workers))):
+                out.append(stage(parts))
+    print(f"[bench] {n} per-step batches staged in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    return out
+
+
+def cycle_steps(step_fn, batches):
+    """step() trains on batch i of the per-step list at its i-th call (wrapping after the last)."""
+    it = {"i": 0}
+
+    def step():
+        b = batches[it["i"] % len(batches)]
+        it["i"] += 1
+        return step_fn(*b)
+
+    return step
 
 
 def build_reconet_infer(args, dev, rank):
@@ -615,25 +661,30 @@ def arithmetic_label(ops, ks):
     """dtype string: fp32 operands/accumulation + the product arithmetic actually launched."""
     names = sorted({ops.gemm_mode_name(m) for m in ks["by_mode"]}) or ops.policy_modes()
     desc = {"f32": "f32 MFMA", "bf16x6": "bf16x6 split MFMA (~2^-24/product)", "bf16x3": "bf16x3 split MFMA (~2^-16)",
-            "bf16": "bf16 MFMA (~2^-8)", "f16": f"fp16 MFMA (~2^-11, static loss scale {ops.loss_scale():g})"}
+            "bf16": "bf16 MFMA (~2^-8)", "f16": f"fp16 MFMA (~2^-11, dynamic loss scale from {ops.loss_scale():g})"}
     base = names[0] if names in (["bf16"], ["f16"]) else "f32"
     return f"{base} ({' + '.join(desc[n] for n in names)})"
 
 
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def timed(step, steps, world, dev, mark=False):
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
     if mark:  # rocprofv3 marker dispatch: the counter passes select the dispatches after it
         from vst._lib import lib, stream
 
         lib.vst_marker(stream())
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     out = None
     for _ in range(steps):
         out = step()
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -642,15 +693,87 @@ def timed(step, steps, world, dev, mark=False):
     return float(elapsed.item()), out
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without a torchrun environment: run the N ranks as a child
+    torch.distributed.run (one process per GPU, RCCL over xGMI), relay rank 0's JSON line, return the
+    child's exit code.  Called before anything touches the GPU (this process never initialises HIP)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for line in proc.stdout:  # rank 0 prints the JSON line; anything else goes to stderr
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+def dry_run(args, world, rank):
+    """CPU stand-in for the training step (no GPU): a fixed matmul chain per frame pair plus the
+    step's one gradient all-reduce (15.05 MB, ReCoNet's flat gradient) over gloo, timed exactly as
+    the real line (barrier, max over ranks).  Exercises the launcher, the rank environment and the
+    line's aggregation; its `value` says nothing about MI355X."""
+    dev = torch.device("cpu")
+    B = args.batch
+    g = torch.Generator().manual_seed(rank)
+    a = torch.randn(256, 256, generator=g)
+    grad = torch.zeros(3763011)
+
+    def step():
+        for _ in range(B):
+            a.copy_(torch.tanh(a @ a) * 0.5)
+        if world > 1:
+            dist.all_reduce(grad)
+        return {}
+
+    for _ in range(args.warmup):
+        step()
+    elapsed, _ = timed(step, args.steps, world, dev)
+    if rank != 0:
+        return None
+    value = B * world * args.steps / elapsed
+    result = {"metric": "dry run (CPU stand-in step; launcher test)", "value": value, "unit": "frame-pairs/s",
+              "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "f32", "data": "none (dry run)",
+              "config": {"workload": "dry run", "global_batch": B * world, "parallelism": f"dp{world}"},
+              "elapsed_s": elapsed}
+    print(json.dumps(result), flush=True)
+    return result
+
+
 def main():
     args = parse()
     if args.batch is None:
         args.batch = {"reconet": 8, "adaattn": 4, "reconet_infer": 16, "dataprep": 8}[args.model]
     if args.model == "reconet_infer" and (args.height, args.width) == (256, 512):
         args.height, args.width = 360, 640  # RC/utilities.py:121 (inference frame size)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:
+            sys.exit(launch_ranks(args))  # N ranks as a child torchrun; nothing here touched the GPU
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+            sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        res = dry_run(args, world, rank)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return res
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

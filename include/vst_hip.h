@@ -60,9 +60,10 @@ const char* vst_build_id(void);
  * equivalence test; pack entries ignore it).
  * A bf16x6 / bf16 halo launch whose grid would not fill the chip (fewer than 512 blocks: AdaAttN
  * config 4's decoder, VGG19 conv4 / conv5) is split over the 16-channel blocks (split-K; fp16 launches
- * stay unsplit): the slices' raw sums go to a per-stream
- * scratch buffer the library holds, and a reduce kernel adds them in slice order (deterministic)
- * and applies the epilogue -- equal to the unsplit result up to fp32 summation order.
+ * stay unsplit): the slices' raw sums go to the CALLER's `workspace` (vst_conv_splitk_workspace bytes,
+ * 16-byte aligned), and a reduce kernel on the same stream adds them in slice order (deterministic)
+ * and applies the epilogue -- equal to the unsplit result up to fp32 summation order.  A launch given
+ * a smaller (or NULL) workspace runs unsplit, so ws_bytes = 0 is always valid.
  * VST_GEMM_NOSPLIT or-ed into the mode keeps such a launch unsplit (the bitwise test against the
  * per-tap kernel).
  * An unknown mode returns VST_EINVAL (-1). */
@@ -94,10 +95,18 @@ int vst_pack_weight(const float* w, float* packed, int Cout, int Cin, int KH, in
  * epi bits: 1 bias, 2 relu, 4 reconet-tanh (aux: tanh value, may be NULL), 8 mask (out *= mask>0),
  * 16 accumulate into out.  a_batch_stride > 0: per-image A (Gram backward).
  * gmask (may be NULL, same shape as src): gathered values are zeroed where gmask <= 0 — the
- * ReLU backward of the layer that produced src, fused into the dgrad gather. */
+ * ReLU backward of the layer that produced src, fused into the dgrad gather.
+ * workspace / ws_bytes: split-K scratch (see VST_GEMM_NOSPLIT above); NULL / 0 runs unsplit. */
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                   int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, int mode, void* stream);
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* workspace, long ws_bytes,
+                  int mode, void* stream);
+/* Bytes of split-K workspace the conv GEMM launch with these arguments uses (0: it never splits).
+ * The geometry is vst_conv_gemm_padx's (Cs = source channels, M = output rows, Ho x Wo = output
+ * grid); for vst_conv_dgrad_padout pass (N, Cout, Cin, H + 2 pad, W + 2 pad, KS, KS, gmode 2, stride 1,
+ * pad 0, pad_x 0, up 1, epi 128 | (mask ? 8 : 0), 0, mode).  Pure host arithmetic, no GPU call. */
+long vst_conv_splitk_workspace(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
+                               int pad_x, int up, int epi, long a_batch_stride, int mode);
 /* row-split forward epilogue: out[n][co][y][x] = epi(bias + sum_kh P[n][co*KH+kh][y+kh][x]) where P
  * [N][Cout*KH][H+KH-1][W] came from vst_conv_gemm(KH=1, KW=K, split_kh pack) over the padded rows
  * (RC/network.py:169 deconv3 = ConvTanh(48, 3, 9): 27 GEMM rows instead of 3 padded to 32) */
@@ -138,7 +147,7 @@ int vst_pack_weight_kwu(const float* w, float* packed, int Cout, int Cin, int K,
 int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                        int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
                        int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
-                       int mode, void* stream);
+                       void* workspace, long ws_bytes, int mode, void* stream);
 int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, const float* mask, float* dx, float* border, int N,
                               int Cu, int Ho, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
 /* data gradient of a zero-padded stride-1 KxK conv with few input channels (VGG conv1_1, 64 -> 3):
@@ -153,7 +162,8 @@ int vst_tapsum(const float* P, float* dx, int N, int C, int H, int W, int K, int
  * mask (optional, dx-shaped; the same pointer to vst_fold_border): dx is written only where
  * mask > 0 (the ReLU backward of a conv+ReLU producing this conv's input, fused). */
 int vst_conv_dgrad_padout(const float* dy, const float* wpack, const float* mask, float* dx, float* border, int N,
-                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream);
+                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* workspace,
+                          long ws_bytes, int mode, void* stream);
 /* Reflect-pad dgrad without the padded grid (ConvLayer / UpsampleConvLayer backward,
  * RC/network.py:72-75,114-120): core = vst_conv_gemm on the unpadded grid (up=1: GM_TRANSPOSED,
  * pad=KS/2; up=2: GM_ZERO stride 2, pad KS-1-KS/2, KS+1 taps with the weights of
@@ -233,10 +243,11 @@ int vst_maxpool2x2_bwd_add(const float* x, const float* gy, const float* addend,
  * warp_bwd scatters with float atomics into gx (zero it first or accumulate). */
 int vst_warp_fwd(const float* x, const float* flo, float* out, int B, int C, int H, int W, void* stream);
 int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, int H, int W, void* stream);
-/* warp backward in gather form (no float atomics on the gradient): the bilinear taps are inverted
- * per image into per-source-pixel lists in `workspace` (vst_warp_bwd_workspace bytes), then each
- * source pixel sums its entries over all channels; gx is overwritten (accumulate=0) or added to.
- * Sources hit by more than 8 taps (strongly converging flow) take an atomic pass for the excess. */
+/* warp backward in gather form (no float atomics on the gradient, deterministic): the bilinear taps
+ * are inverted per image into per-source-pixel lists (CSR: a count pass, a scan, a fill pass) in
+ * `workspace` (vst_warp_bwd_workspace bytes, 16-B aligned), then each source pixel sums its entries
+ * over all channels in increasing output-pixel order -- bitwise reproducible run to run; gx is
+ * overwritten (accumulate=0) or added to. */
 long vst_warp_bwd_workspace(int B, int H, int W);
 int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* workspace, int B, int C, int H, int W,
                         int accumulate, void* stream);
@@ -324,7 +335,7 @@ int vst_plane_meanstd_bwd(const float* x, const float* mean, const float* std_, 
 int vst_plane_norm(const float* x, float* out, long NC, int HW, void* stream);
 int vst_plane_norm_grad(float* x, const float* s, const float* nrm, const float* y, long NC, int HW, void* stream);
 /* image_similarity_loss (AA/lossfn.py:25-53) on precomputed C x C products and norms;
- * partial[n][i] = sum_j |Dn_c - Dn_cs|_ij / hw (N*C floats); backward w.r.t. the stylised side (dun zeroed first) */
+ * partial[n][i] = sum_j |Dn_c - Dn_cs|_ij / hw (N*C floats); backward w.r.t. the stylised side (dG, dun, dvn fully written, fixed summation order) */
 int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
                 const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream);
 int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,

@@ -18,7 +18,7 @@ def test_header_parses_and_lists_entry_points():
                  "vst_build_id"):
         assert name in protos, name
     assert protos["vst_conv_gemm"][0] == "int"
-    assert len(protos["vst_conv_gemm"][1]) == 25
+    assert len(protos["vst_conv_gemm"][1]) == 27
     # the C ABI is stateless: no global GEMM-mode setter; every GEMM / pack entry takes `mode`
     assert not [n for n in protos if "set_gemm_mode" in n or "get_gemm_mode" in n]
     for name in ("vst_pack_weight", "vst_conv_gemm", "vst_conv_gemm_padx", "vst_pack_weight_phase2", "vst_conv_dgrad_s2",
@@ -45,7 +45,10 @@ def test_host_side_argument_validation_without_gpu():
     """Entry points validate arguments before touching the device: bad calls fail with VST_EINVAL."""
     lib = _lib.lib.load()
     assert lib.vst_conv_gemm(None, None, None, None, None, 1, 3, 8, 8, 4, 27, 8, 8, 3, 3, 0, 1, 1, 1, 0, 0, None, None,
-                             0, None) == -1
+                             None, 0, 0, None) == -1
+    # split-K workspace is the caller's: a positive size with a NULL pointer is refused
+    assert lib.vst_conv_gemm(1, 1, None, None, 1, 1, 16, 8, 8, 64, 144, 8, 8, 3, 3, 0, 1, 1, 1, 0, 0, None, None,
+                             None, 1024, 19, None) == -1
     mp, kp = ctypes.c_int(), ctypes.c_int()
     assert lib.vst_conv_pack_dims(48, 243, ctypes.byref(mp), ctypes.byref(kp)) == 0
     assert (mp.value, kp.value) == (64, 256)

@@ -35,7 +35,7 @@ def _pack(w, mode, st):
 def _conv(x, wp, out, Cout, mode, st):
     N, Cin, H, W = x.shape
     lib.vst_conv_gemm(x.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cin, H, W, Cout, 9 * Cin, H, W, 3, 3,
-                      GM_ZERO, 1, 1, 1, 0, 0, None, None, mode, st.cuda_stream)
+                      GM_ZERO, 1, 1, 1, 0, 0, None, None, None, 0, mode, st.cuda_stream)
 
 
 def _err(y, ref):

@@ -24,7 +24,7 @@ DEV = "cuda"
 BF16, BF16X6, F16 = 2, 3, 4
 KBLOCK, PERTAP, NOSPLIT = 16, 32, 64
 GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
-EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM = 1, 2, 8, 16
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM, EPI_PADOUT = 1, 2, 8, 16, 128
 
 
 def _dims(M, K):
@@ -44,14 +44,25 @@ def _pack(w, mode, transposed=False):
     return p
 
 
-def _conv(src, wp, M, Ho, Wo, gmode, pad, mode, epi=0, bias=None, mask=None, gmask=None, out=None):
+def _ws_bytes(N, Cs, M, Ho, Wo, gmode, pad, epi, mode):
+    return lib.vst_conv_splitk_workspace(N, Cs, M, Ho, Wo, 3, 3, gmode, 1, pad, pad, 1, epi, 0, mode)
+
+
+def _conv(src, wp, M, Ho, Wo, gmode, pad, mode, epi=0, bias=None, mask=None, gmask=None, out=None, ws=True,
+          stream=None):
+    """ws: supply the split-K workspace the library asks for (caller-owned, from torch's allocator)."""
     N, Cs, Hs, Ws = src.shape
     if out is None:
         out = torch.full((N, M, Ho, Wo), float("nan"), device=DEV)
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    nb = _ws_bytes(N, Cs, M, Ho, Wo, gmode, pad, epi, mode) if ws else 0
+    wsb = torch.empty((nb + 3) // 4, device=DEV) if nb else None
+    st = stream if stream is not None else torch.cuda.current_stream()
     lib.vst_conv_gemm_padx(src.data_ptr(), wp.data_ptr(), P(bias), P(mask), out.data_ptr(), N, Cs, Hs, Ws, M, 9 * Cs,
-                           Ho, Wo, 3, 3, gmode, 1, pad, pad, 1, epi, 0, None, P(gmask), mode,
-                           torch.cuda.current_stream().cuda_stream)
+                           Ho, Wo, 3, 3, gmode, 1, pad, pad, 1, epi, 0, None, P(gmask), P(wsb), nb, mode,
+                           st.cuda_stream)
+    if wsb is not None:
+        wsb.record_stream(st)
     return out
 
 
@@ -134,8 +145,10 @@ def test_halo_padout_dgrad_bitwise(mode, shape):
     for mm in (m | NOSPLIT, m | PERTAP, m):
         dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
         border = torch.zeros(N, Cin, H + 2, W + 2, device=DEV)
+        nb = lib.vst_conv_splitk_workspace(N, Cout, Cin, H + 2, W + 2, 3, 3, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT, 0, mm)
+        ws = torch.empty((nb + 3) // 4, device=DEV) if nb else None
         lib.vst_conv_dgrad_padout(dy.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N, Cout, H, W,
-                                  Cin, H, W, 3, 1, mm, st)
+                                  Cin, H, W, 3, 1, None if ws is None else ws.data_ptr(), nb, mm, st)
         lib.vst_fold_border(border.data_ptr(), None, dx.data_ptr(), N * Cin, H, W, 1, st)
         res.append(dx)
     torch.cuda.synchronize()
@@ -184,10 +197,16 @@ def test_halo_split_k(mode, shape, epi):
     wp = _pack(w, m)
     e = {"bias_relu": EPI_BIAS | EPI_RELU, "mask": EPI_MASK, "accum": EPI_ACCUM}[epi]
     kw = dict(bias=b) if epi == "bias_relu" else dict(mask=mask) if epi == "mask" else {}
-    outs = [_conv(x, wp, Cout, H, W, GM_REFLECT, 1, mm, e, out=base.clone() if epi == "accum" else None, **kw)
-            for mm in (m, m | NOSPLIT)]
+    # the split is planned (the library asks for workspace) except for the full-size residual layer
+    nb = _ws_bytes(N, Cin, Cout, H, W, GM_REFLECT, 1, e, m)
+    assert (nb > 0) == (N * H * W < 4 * 64 * 128), nb
+    assert _ws_bytes(N, Cin, Cout, H, W, GM_REFLECT, 1, e, m | NOSPLIT) == 0
+    outs = [_conv(x, wp, Cout, H, W, GM_REFLECT, 1, mm, e, out=base.clone() if epi == "accum" else None, ws=w_, **kw)
+            for mm, w_ in ((m, True), (m | NOSPLIT, True), (m, False))]
     torch.cuda.synchronize()
-    split, whole = outs
+    split, whole, nows = outs
+    # no workspace given: the same launch runs unsplit, bitwise the NOSPLIT result
+    assert torch.equal(nows, whole)
     assert not torch.isnan(split).any()
     y = F.conv2d(F.pad(x.double(), (1, 1, 1, 1), mode="reflect"), w.double())
     if epi == "bias_relu":
@@ -200,3 +219,47 @@ def test_halo_split_k(mode, shape, epi):
     assert float((split - whole).abs().max()) / scale < 1e-5  # fp32 summation order over K = 9 Cin
     err = float((split.double() - y).abs().max()) / scale
     assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+
+
+@pytest.mark.parametrize("threads", [False, True])
+def test_split_k_two_streams(threads):
+    """Split-K launches on two streams at once (issued from one or two host threads), each with its
+    own caller-owned workspace: every result equals its stream's own unsplit (NOSPLIT) launch up to fp32
+    summation order, and repeated launches are bitwise reproducible (no shared library scratch)."""
+    import threading
+
+    shapes = [(2, 192, 20, 36, 192), (1, 256, 8, 16, 128)]
+    m = BF16X6 | KBLOCK
+    jobs = []
+    for i, (N, Cin, H, W, Cout) in enumerate(shapes):
+        x = _rand(N, Cin, H, W, seed=40 + i, scale=3.0)
+        w = _rand(Cout, Cin, 3, 3, seed=50 + i, scale=0.05)
+        assert _ws_bytes(N, Cin, Cout, H, W, GM_REFLECT, 1, 0, m) > 0
+        jobs.append((x, _pack(w, m), Cout, H, W))
+    streams = [torch.cuda.Stream() for _ in jobs]
+    torch.cuda.synchronize()
+    ref = [_conv(x, wp, C, H, W, GM_REFLECT, 1, m | NOSPLIT) for x, wp, C, H, W in jobs]
+    reps = 20
+    outs = [[None] * reps for _ in jobs]
+
+    def issue(i):
+        x, wp, C, H, W = jobs[i]
+        with torch.cuda.stream(streams[i]):
+            for r in range(reps):
+                outs[i][r] = _conv(x, wp, C, H, W, GM_REFLECT, 1, m, stream=streams[i])
+
+    if threads:
+        ts = [threading.Thread(target=issue, args=(i,)) for i in range(len(jobs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    else:
+        for i in range(len(jobs)):
+            issue(i)
+    torch.cuda.synchronize()
+    for i in range(len(jobs)):
+        scale = float(ref[i].abs().max())
+        assert float((outs[i][0] - ref[i]).abs().max()) / scale < 1e-5
+        for r in range(1, reps):
+            assert torch.equal(outs[i][r], outs[i][0])

@@ -92,8 +92,11 @@ def main():
                 # packed A floats per mode (bf16x6 blocks are 96 B per 16 k, the others 64 B)
                 pf = kp.value * mp.value * 3 // 2 if (MODE & 15) == 3 else kp.value * mp.value
                 wp = torch.randn(pf, device=dev) * 0.05
+                nb = lib.vst_conv_splitk_workspace(N, Cs, M, Ho, Wo, KH, KW, gm, stride, pad, pad, up, 0, 0, MODE)
+                wsb = torch.empty((nb + 3) // 4, device=dev) if nb else None
                 args = (src.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cs, Hs, Ws, M, KH * KW * Cs, Ho, Wo,
-                        KH, KW, gm, stride, pad, up, 0, 0, None, None, MODE, st)
+                        KH, KW, gm, stride, pad, up, 0, 0, None, None, None if wsb is None else wsb.data_ptr(), nb,
+                        MODE, st)
                 for _ in range(2):
                     assert lib.vst_conv_gemm(*args) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -37,8 +37,10 @@ def conv(src, wp, M, gmode, mode, epi, bias=None, mask=None, gmask=None):
     N, Cs, H, W = src.shape
     out = torch.full((N, M, H, W), float("nan"), device=DEV)
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    nb = lib.vst_conv_splitk_workspace(N, Cs, M, H, W, 3, 3, gmode, 1, 1, 1, 1, epi, 0, mode)
+    ws = torch.empty((nb + 3) // 4, device=DEV) if nb else None
     rc = lib.vst_conv_gemm_padx(src.data_ptr(), wp.data_ptr(), P(bias), P(mask), out.data_ptr(), N, Cs, H, W, M, 9 * Cs,
-                                H, W, 3, 3, gmode, 1, 1, 1, 1, epi, 0, None, P(gmask), mode,
+                                H, W, 3, 3, gmode, 1, 1, 1, 1, epi, 0, None, P(gmask), P(ws), nb, mode,
                                 torch.cuda.current_stream().cuda_stream)
     assert rc == 0, rc
     return out

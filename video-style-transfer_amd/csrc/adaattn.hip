@@ -458,11 +458,31 @@ __global__ void simloss_bwd_kernel(const float* __restrict__ Gc, const float* __
     // D = 1 - G/den: dG = -dD/den; d(den) = dD * G / den^2
     dG[o + (long)i * C + j] = -dD / den;
     const float dden = dD * G / (den * den);
-    atomicAdd(&dun[n * C + i], dden * vj);
     dvacc += (double)dden * uns[n * C + i];
   }
   const double dv = block_sum_d(dvacc, sh);
   if (threadIdx.x == 0) dvn[n * C + j] = (float)dv;
+}
+
+// the row half of the same adjoint, one block per row (i, n): dun_i = sum_j d(den_ij) v_j with
+// d(den_ij) = dD_ij G_ij / den_ij^2 = -dG_ij G_ij / den_ij (dG from simloss_bwd_kernel), summed in a
+// fixed order (was a float atomic per (i, j): run-to-run reproducible now)
+__global__ void simloss_bwd_rows_kernel(const float* __restrict__ Gs, const float* __restrict__ uns,
+                                        const float* __restrict__ vns, const float* __restrict__ dG,
+                                        float* __restrict__ dun, int C) {
+  __shared__ double sh[RT / 64];
+  const int i = blockIdx.x, n = blockIdx.y;
+  const long o = (long)n * C * C + (long)i * C;
+  const float ui = uns[n * C + i];
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < C; j += RT) {
+    const float vj = vns[n * C + j];
+    const float den = ui * vj + 1e-6f;
+    const float dden = -dG[o + j] * Gs[o + j] / den;
+    acc += (double)(dden * vj);
+  }
+  const double tot = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) dun[n * C + i] = (float)tot;
 }
 
 // x[plane][i] += s[plane] / nrm[plane] * y[plane][i]   (gradient through per-plane L2 norms)
@@ -615,7 +635,7 @@ int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float
   return vst_launch_status();
 }
 
-// dun must be zeroed (atomic accumulation); dG, dvn fully written
+// dG, dun, dvn fully written (deterministic: no atomics)
 int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const float* Gs, const float* uns,
                     const float* vns, const float* colc, const float* cols, const float* gout, float weight, float* dG,
                     float* dun, float* dvn, int N, int C, int HW, void* stream) {
@@ -623,6 +643,7 @@ int vst_simloss_bwd(const float* Gc, const float* unc, const float* vnc, const f
   dim3 g(C, N);
   simloss_bwd_kernel<<<g, RT, 0, (hipStream_t)stream>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, gout, weight, dG, dun,
                                                         dvn, C, 1.0f / HW);
+  simloss_bwd_rows_kernel<<<dim3(C, N), RT, 0, (hipStream_t)stream>>>(Gs, uns, vns, dG, dun, C);
   return vst_launch_status();
 }
 

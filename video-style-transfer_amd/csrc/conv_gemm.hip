@@ -14,10 +14,9 @@
 // Tile: 4 waves (256 threads); each wave owns TM x TN 32x32 accumulators (WM x WN waves).
 // LDS: A[BK][BM] and B[BK][BN], double buffered; global->register prefetch of tile t+1 overlaps
 // the MFMAs of tile t; one barrier per k-tile.
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
-#include <unordered_map>
 
 #include "conv_gemm_kernel.h"
 #include "conv_halo_kernel.h"
@@ -27,30 +26,6 @@
 using namespace vstk;
 
 namespace {
-
-// Split-K scratch of the halo kernel: one device buffer per stream (kernels of one stream run in
-// order, so a buffer is never shared by two splits in flight), grown on demand -- the sizes of a
-// training step are fixed, so it reaches its final size in the first step.  At most
-// VST_SPLITK_MAX_BYTES per stream; a split that would need more runs unsplit.
-#ifndef VST_SPLITK_MAX_BYTES
-#define VST_SPLITK_MAX_BYTES (512l << 20)
-#endif
-float* splitk_scratch(hipStream_t st, size_t bytes) {
-  static std::mutex mu;
-  static std::unordered_map<hipStream_t, std::pair<float*, size_t>> bufs;
-  std::lock_guard<std::mutex> lock(mu);
-  auto& b = bufs[st];
-  if (b.second < bytes) {
-    if (b.first) {
-      if (hipStreamSynchronize(st) != hipSuccess || hipFree(b.first) != hipSuccess) return nullptr;
-      b = {nullptr, 0};
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    b = {(float*)p, bytes};
-  }
-  return b.first;
-}
 
 // sum of the split-K slices part[s][n][m][p] (s in order: deterministic), then the conv epilogue.
 // Grid: x = pixel chunks of 4 x 256, y = n * M + m.
@@ -370,13 +345,51 @@ static long apack_floats(int M, int K, int mode) {
   return vst_mode_arith(mode) == VST_GEMM_BF16X6 ? f * 3 / 2 : f;
 }
 
+// Halo-kernel plan of a conv GEMM launch (shared by the launch and vst_conv_splitk_workspace, so the
+// workspace a caller is told to supply is exactly what the launch will use): the halo block config
+// (0 = the per-tap kernel runs) and the split-K slice count S (1 = unsplit).
+struct HaloPlan {
+  int hcfg, S, tiles, mpad;
+};
+static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
+                          int pad_x, int up, int epi, long a_batch_stride, int mode) {
+  HaloPlan hp{0, 1, 0, 0};
+  const int am = vst_mode_arith(mode);
+  // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
+  const int pack_bm = cfg_bm(select_cfg(M));
+  hp.mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
+  const int hcfg = halo_cfg(M, hp.mpad, am == VST_GEMM_BF16X6, (epi & EPI_PADOUT) != 0);
+  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 &&
+                    KW == 3 && stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
+                    (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED) &&
+                    !(epi & (EPI_AFFINE | EPI_PHASE2)) &&
+                    (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
+  if (!halo) return hp;
+  hp.hcfg = hcfg;
+  const int bm = 32 * halo_wm(hcfg), th = 4 * halo_wn(hcfg);
+  hp.tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
+  // split-K when the grid is too small for the chip (AdaAttN config 4's decoder and VGG19 conv4 /
+  // conv5 layers: 128-384 blocks).  Not under fp16: every split launch matches its unsplit launch
+  // to <= 3e-6 (tools/split_diag.py), but the fp16 AdaAttN step amplifies that summation-order change
+  // in its attention-parameter gradients past its own parity bars
+  const bool kc1 = am == VST_GEMM_BF16X6 || VST_HALO_KC == 1 || !halo_db_c(hcfg);
+  if (kc1 && am != VST_GEMM_F16 && !(mode & VST_GEMM_NOSPLIT))
+    hp.S = halo_ksplit((long)hp.tiles * (hp.mpad / bm) * N, Cs / 16);
+  return hp;
+}
+
+// bytes of split-K workspace a planned launch needs (0: unsplit)
+static long splitk_bytes(const HaloPlan& hp, int N, int M, int Ho, int Wo) {
+  return hp.S > 1 ? (long)hp.S * N * M * Ho * Wo * (long)sizeof(float) : 0;
+}
+
 static int conv_gemm_launch(const float* src, const float* wpack, const float* bias, const float* mask, float* out,
                             int N, int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode,
                             int stride, int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux,
                             const float* gmask, int mode, void* stream, const float* ep_ra = nullptr,
                             const float* ep_rb = nullptr, const float* ep_rd = nullptr,
                             const float* ep_cg = nullptr, float* ph_border = nullptr, int ph_H = 0, int ph_W = 0,
-                            int ph_pad = 0) {
+                            int ph_pad = 0, void* workspace = nullptr, long ws_bytes = 0) {
   ConvParams P;
   P.ph_border = ph_border;
   P.ph_H = ph_H;
@@ -422,17 +435,10 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   // 3x3 stride-1 convs in the channel-blocked K order: the halo-tiled kernel (conv_halo_kernel.h),
   // one A-direct wave per 32 weight rows -- 2 / 4 / 6 / 8 waves as the per-tap kernel's blocks
   const int am = vst_mode_arith(mode);
-  // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
-  const int pack_bm = cfg_bm(select_cfg(M)), pack_mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
-  const int hcfg = halo_cfg(M, pack_mpad, am == VST_GEMM_BF16X6, (epi & EPI_PADOUT) != 0);
-  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 &&
-                    KW == 3 && stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
-                    (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED) &&
-                    !(epi & (EPI_AFFINE | EPI_PHASE2)) &&
-                    (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
-  if (halo) {
-    const int bm = 32 * halo_wm(hcfg), th = 4 * halo_wn(hcfg);
-    P.Mpad = pack_mpad;
+  const HaloPlan hp = halo_plan(N, Cs, M, Ho, Wo, KH, KW, gmode, stride, pad, pad_x, up, epi, a_batch_stride, mode);
+  if (hp.hcfg) {
+    const int hcfg = hp.hcfg, bm = 32 * halo_wm(hcfg);
+    P.Mpad = hp.mpad;
     P.K = K;
     P.Kpad = (K + BK - 1) / BK * BK;
     P.Ho = Ho;
@@ -450,23 +456,17 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     P.fd_Cs = make_fastdiv(Cs);
     P.fd_KW = make_fastdiv(KW);
     P.kb = 1;
-    const int tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
     hipStream_t st = (hipStream_t)stream;
-    // split-K when the grid is too small for the chip (AdaAttN config 4's decoder and VGG19 conv4 /
-    // conv5 layers: 128-384 blocks).  Not under fp16: every split launch matches its unsplit launch
-    // to <= 3e-6 (tools/split_diag.py), but the fp16 AdaAttN step amplifies that summation-order change
-    // in its attention-parameter gradients past its own parity bars
-    const bool kc1 = am == VST_GEMM_BF16X6 || VST_HALO_KC == 1 || !halo_db_c(hcfg);
-    int S = (kc1 && am != VST_GEMM_F16 && !(mode & VST_GEMM_NOSPLIT)) ? halo_ksplit((long)tiles * (P.Mpad / bm) * N, Cs / 16) : 1;
-    const size_t part_bytes = (size_t)S * N * M * Ho * Wo * sizeof(float);
-    if (S > 1 && part_bytes <= (size_t)VST_SPLITK_MAX_BYTES) {
-      P.part = splitk_scratch(st, part_bytes);
-      if (!P.part) return (int)hipErrorOutOfMemory;
+    // the split's slices go to the caller's workspace (vst_conv_splitk_workspace bytes); a launch
+    // given less runs unsplit -- same result up to fp32 summation order
+    const long need = splitk_bytes(hp, N, M, Ho, Wo);
+    int S = 1;
+    if (need > 0 && workspace && ws_bytes >= need && ((uintptr_t)workspace & 15) == 0) {
+      S = hp.S;
+      P.part = (float*)workspace;
       P.ksplit = S;
-    } else {
-      S = 1;
     }
-    dim3 grid(tiles, P.Mpad / bm, N * S);
+    dim3 grid(hp.tiles, P.Mpad / bm, N * S);
     const bool gm = gmask != nullptr;
     if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, hcfg, grid, st, P);
     else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, hcfg, grid, st, P);
@@ -561,17 +561,26 @@ extern "C" {
 
 int vst_conv_gemm(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                   int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, int mode, void* stream) {
+                  int up, int epi, long a_batch_stride, float* aux, const float* gmask, void* workspace, long ws_bytes,
+                  int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   return vst_conv_gemm_padx(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad,
-                            up, epi, a_batch_stride, aux, gmask, mode, stream);
+                            up, epi, a_batch_stride, aux, gmask, workspace, ws_bytes, mode, stream);
+}
+
+long vst_conv_splitk_workspace(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
+                               int pad_x, int up, int epi, long a_batch_stride, int mode) {
+  if (!vst_mode_ok(mode) || N <= 0 || Cs <= 0 || M <= 0 || Ho <= 0 || Wo <= 0) return 0;
+  const HaloPlan hp = halo_plan(N, Cs, M, Ho, Wo, KH, KW, gmode, stride, pad, pad_x, up, epi, a_batch_stride, mode);
+  return hp.hcfg ? splitk_bytes(hp, N, M, Ho, Wo) : 0;
 }
 
 int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, const float* mask, float* out, int N,
                        int Cs, int Hs, int Ws, int M, int K, int Ho, int Wo, int KH, int KW, int gmode, int stride,
                        int pad, int pad_x, int up, int epi, long a_batch_stride, float* aux, const float* gmask,
-                       int mode, void* stream) {
+                       void* workspace, long ws_bytes, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
+  VST_CHECK_ARG(ws_bytes >= 0 && (workspace || ws_bytes == 0));
   VST_CHECK_ARG(src && wpack && out && N > 0 && Cs > 0 && Hs > 0 && Ws > 0 && M > 0 && Ho > 0 && Wo > 0);
   VST_CHECK_ARG(K == KH * KW * Cs && KH > 0 && KW > 0);
   VST_CHECK_ARG(gmode >= 0 && gmode <= 2 && (stride == 1 || stride == 2) && (up == 1 || up == 2));
@@ -580,7 +589,8 @@ int vst_conv_gemm_padx(const float* src, const float* wpack, const float* bias, 
   VST_CHECK_ARG(pad >= 0 && pad_x >= 0);
   VST_CHECK_ARG(a_batch_stride == 0 || a_batch_stride >= apack_floats(M, K, mode));
   return conv_gemm_launch(src, wpack, bias, mask, out, N, Cs, Hs, Ws, M, K, Ho, Wo, KH, KW, gmode, stride, pad, pad_x,
-                          up, epi, a_batch_stride, aux, gmask, mode, stream);
+                          up, epi, a_batch_stride, aux, gmask, mode, stream, nullptr, nullptr, nullptr, nullptr,
+                          nullptr, 0, 0, 0, workspace, ws_bytes);
 }
 
 // out[n][m][p] = (sum_k A[n][k][m] B[n][k][p] + ra[n][m]) * rb[n][m] * cg[n][p] + rd[n][m]
@@ -711,13 +721,16 @@ int vst_conv_dgrad_padout_kwu(const float* dyu, const float* wpack, const float*
 }
 
 int vst_conv_dgrad_padout(const float* dy, const float* wpack, const float* mask, float* dx, float* border, int N,
-                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, int mode, void* stream) {
+                          int Cout, int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* workspace,
+                          long ws_bytes, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
+  VST_CHECK_ARG(ws_bytes >= 0 && (workspace || ws_bytes == 0));
   VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
                 pad < W && Ho == H + 2 * pad - KS + 1 && Wo == W + 2 * pad - KS + 1);
   return conv_gemm_launch(dy, wpack, nullptr, mask, dx, N, Cout, Ho, Wo, Cin, KS * KS * Cout, H + 2 * pad,
                           W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT | (mask ? EPI_MASK : 0), 0, nullptr,
-                          nullptr, mode, stream, nullptr, nullptr, nullptr, nullptr, border, H, W, pad);
+                          nullptr, mode, stream, nullptr, nullptr, nullptr, nullptr, border, H, W, pad, workspace,
+                          ws_bytes);
 }
 
 int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream) {

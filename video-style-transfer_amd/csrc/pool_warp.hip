@@ -273,98 +273,187 @@ __global__ void warp_bwd_kernel(const float* __restrict__ gout, const float* __r
   }
 }
 
-// Gather form of the warp backward (no float atomics on the gradient): the bilinear taps of
-// every output pixel p are inverted once per image into per-source-pixel lists (up to WG_SLOTS
-// entries each; the flow is shared by all channels), then each source pixel sums its entries
-// for every channel.  Entries beyond WG_SLOTS (strongly converging flow) are added afterwards
-// by an atomic pass over just those taps.
-constexpr int WG_SLOTS = 8;
+// Gather form of the warp backward, deterministic (no float atomics on the gradient, a fixed
+// summation order): the bilinear taps of every output pixel p are inverted once per image into
+// per-source-pixel lists in CSR form (the flow is shared by all channels) -- a counting pass, an
+// exclusive scan of the counts, a fill pass -- then each source pixel q sums its list for every
+// channel in increasing p.  The fill pass takes list positions from integer atomics (their order
+// varies run to run), so the gather sorts each list by p before summing: an 8-input sorting network
+// in registers, a selection scan over memory for the rare longer lists (converging flow).
 struct WgEntry {
   int p;
   float w;
 };
+constexpr int WG_REG = 8;     // lists up to this long are sorted in registers
+constexpr int WS_BLOCK = 1024; // elements per block of the count scan
 
-__global__ void warp_inv_fill_kernel(const float* __restrict__ flo, int* __restrict__ cnt, WgEntry* __restrict__ ent,
-                                     int* __restrict__ rec, int B, int H, int W) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void warp_taps(const float* __restrict__ flo, long idx, int H, int W, long q[4], float w[4]) {
   const long HW = (long)H * W;
-  if (idx >= B * HW) return;
   const int b = (int)(idx / HW);
   const long p = idx - b * HW;
   const int y = (int)(p / W), xx = (int)(p % W);
   const float* f = flo + (long)b * 2 * HW;
-  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
-  // all four counter atomics in flight before any result is used
-  long q[4];
-  int slot[4];
+  const Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int cx = bl.x0 + (k & 1), cy = bl.y0 + (k >> 1);
     q[k] = (cx >= 0 && cx < W && cy >= 0 && cy < H) ? (long)b * HW + (long)cy * W + cx : -1;
+    w[k] = bl.w[k];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) slot[k] = q[k] >= 0 ? atomicAdd(cnt + q[k], 1) : -1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (slot[k] >= 0 && slot[k] < WG_SLOTS) ent[q[k] * WG_SLOTS + slot[k]] = WgEntry{(int)p, bl.w[k]};
-  *reinterpret_cast<int4*>(rec + idx * 4) = make_int4(slot[0], slot[1], slot[2], slot[3]);
 }
 
-// gx[b][c][q] (+)= sum over q's entries of w * gout[b][c][p]; grid.y: channel groups of WB_CPT
-__global__ void warp_inv_gather_kernel(const float* __restrict__ gout, const int* __restrict__ cnt,
+__global__ void warp_inv_count_kernel(const float* __restrict__ flo, int* __restrict__ cnt, int B, int H, int W) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * H * W) return;
+  long q[4];
+  float w[4];
+  warp_taps(flo, idx, H, W, q, w);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (q[k] >= 0) atomicAdd(cnt + q[k], 1);
+}
+
+// exclusive scan of cnt[0..n) into off[0..n], three passes: block-local scan (+ block totals),
+// one-block scan of the totals, block offsets added
+__global__ __launch_bounds__(256) void scan_blocks_kernel(const int* __restrict__ cnt, int* __restrict__ off,
+                                                          int* __restrict__ bsum, long n) {
+  __shared__ int sh[256];
+  const long base = (long)blockIdx.x * WS_BLOCK + threadIdx.x * 4;
+  int v[4], t = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = base + i < n ? cnt[base + i] : 0;
+    t += v[i];
+  }
+  sh[threadIdx.x] = t;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan of the thread totals
+    const int a = threadIdx.x >= d ? sh[threadIdx.x - d] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += a;
+    __syncthreads();
+  }
+  int run = sh[threadIdx.x] - t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (base + i < n) off[base + i] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == 255) bsum[blockIdx.x] = sh[255];
+}
+
+__global__ __launch_bounds__(1024) void scan_totals_kernel(int* __restrict__ bsum, int nb, int* __restrict__ total) {
+  __shared__ int sh[1024];
+  int carry = 0;
+  for (int c0 = 0; c0 < nb; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    const int v = i < nb ? bsum[i] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int a = threadIdx.x >= d ? sh[threadIdx.x - d] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += a;
+      __syncthreads();
+    }
+    if (i < nb) bsum[i] = carry + sh[threadIdx.x] - v;  // exclusive
+    carry += sh[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void scan_add_kernel(int* __restrict__ off, const int* __restrict__ bsum, long n) {
+  const long base = (long)blockIdx.x * WS_BLOCK + threadIdx.x * 4;
+  const int add = bsum[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (base + i < n) off[base + i] += add;
+}
+
+// each tap's entry into its source pixel's list; cnt counts back down to 0 (ready for the next call)
+__global__ void warp_inv_fill_kernel(const float* __restrict__ flo, int* __restrict__ cnt, const int* __restrict__ off,
+                                     WgEntry* __restrict__ ent, int B, int H, int W) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long HW = (long)H * W;
+  if (idx >= B * HW) return;
+  long q[4];
+  float w[4];
+  warp_taps(flo, idx, H, W, q, w);
+  int slot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) slot[k] = q[k] >= 0 ? atomicSub(cnt + q[k], 1) - 1 : -1;  // all in flight
+  const int p = (int)(idx % HW);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (slot[k] >= 0) ent[off[q[k]] + slot[k]] = WgEntry{p, w[k]};
+}
+
+__device__ __forceinline__ void wg_cswap(WgEntry& a, WgEntry& b) {
+  const bool sw = b.p < a.p;
+  const WgEntry t = a;
+  a = sw ? b : a;
+  b = sw ? t : b;
+}
+
+// gx[b][c][q] (+)= sum over q's list, in increasing p, of w * gout[b][c][p]; grid.y: channel groups
+__global__ void warp_inv_gather_kernel(const float* __restrict__ gout, const int* __restrict__ off,
                                        const WgEntry* __restrict__ ent, float* __restrict__ gx, int B, int C, int H,
                                        int W, int accumulate) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long HW = (long)H * W;
   if (idx >= B * HW) return;
   const int b = (int)(idx / HW);
   const long q = idx - b * HW;
-  const int n = min(cnt[idx], WG_SLOTS);
+  const int s0 = off[idx], n = off[idx + 1] - s0;
   const int c0 = blockIdx.y * WB_CPT, c1 = min(C, c0 + WB_CPT);
   const float* gb = gout + ((long)b * C + c0) * HW;
   float s[WB_CPT];
 #pragma unroll
   for (int c = 0; c < WB_CPT; ++c) s[c] = 0.f;
-  for (int j = 0; j < n; ++j) {
-    const WgEntry e = ent[idx * WG_SLOTS + j];
+  if (n <= WG_REG) {
+    WgEntry e[WG_REG];
 #pragma unroll
-    for (int c = 0; c < WB_CPT; ++c)
-      if (c0 + c < c1) s[c] += e.w * gb[c * HW + e.p];
+    for (int j = 0; j < WG_REG; ++j) e[j] = j < n ? ent[s0 + j] : WgEntry{0x7fffffff, 0.f};
+    // Batcher's odd-even merge sort network for 8 inputs (19 comparators; empty slots sort last)
+#define WG_CS(i, j) wg_cswap(e[i], e[j])
+    WG_CS(0, 1); WG_CS(2, 3); WG_CS(4, 5); WG_CS(6, 7);
+    WG_CS(0, 2); WG_CS(1, 3); WG_CS(4, 6); WG_CS(5, 7);
+    WG_CS(1, 2); WG_CS(5, 6);
+    WG_CS(0, 4); WG_CS(1, 5); WG_CS(2, 6); WG_CS(3, 7);
+    WG_CS(2, 4); WG_CS(3, 5);
+    WG_CS(1, 2); WG_CS(3, 4); WG_CS(5, 6);
+#undef WG_CS
+#pragma unroll
+    for (int j = 0; j < WG_REG; ++j) {
+      if (j >= n) break;
+#pragma unroll
+      for (int c = 0; c < WB_CPT; ++c)
+        if (c0 + c < c1) s[c] += e[j].w * gb[c * HW + e[j].p];
+    }
+  } else {
+    // long list: take its entries in increasing p by repeated minimum search (p unique per list)
+    int last = -1;
+    for (int it = 0; it < n; ++it) {
+      int bp = 0x7fffffff;
+      float bw = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const WgEntry e = ent[s0 + j];
+        if (e.p > last && e.p < bp) {
+          bp = e.p;
+          bw = e.w;
+        }
+      }
+      last = bp;
+#pragma unroll
+      for (int c = 0; c < WB_CPT; ++c)
+        if (c0 + c < c1) s[c] += bw * gb[c * HW + bp];
+    }
   }
   float* xb = gx + ((long)b * C + c0) * HW + q;
 #pragma unroll
   for (int c = 0; c < WB_CPT; ++c)
     if (c0 + c < c1) xb[c * HW] = accumulate ? xb[c * HW] + s[c] : s[c];
-}
-
-// the taps that did not fit their source pixel's list (rec >= WG_SLOTS), added with atomics;
-// grid.y: channel groups of WB_CPT (a handful of such pixels must not serialise over all channels)
-__global__ void warp_inv_overflow_kernel(const float* __restrict__ gout, const float* __restrict__ flo,
-                                         const int* __restrict__ rec, float* __restrict__ gx, int B, int C, int H,
-                                         int W) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long HW = (long)H * W;
-  if (idx >= B * HW) return;
-  const int4 r = *reinterpret_cast<const int4*>(rec + idx * 4);
-  if (r.x < WG_SLOTS && r.y < WG_SLOTS && r.z < WG_SLOTS && r.w < WG_SLOTS) return;
-  const int b = (int)(idx / HW);
-  const long p = idx - b * HW;
-  const int y = (int)(p / W), xx = (int)(p % W);
-  const float* f = flo + (long)b * 2 * HW;
-  Bilin bl = warp_coords(xx, y, f[p], f[HW + p], H, W);
-  const int rk[4] = {r.x, r.y, r.z, r.w};
-  const int c0 = blockIdx.y * WB_CPT, c1 = min(C, c0 + WB_CPT);
-  float g[WB_CPT];
-#pragma unroll
-  for (int c = 0; c < WB_CPT; ++c) g[c] = c0 + c < c1 ? gout[((long)b * C + c0 + c) * HW + p] : 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (rk[k] < WG_SLOTS) continue;  // (-1: out of range; 0..WG_SLOTS-1: gathered)
-    const long o = (long)(bl.y0 + (k >> 1)) * W + bl.x0 + (k & 1);
-#pragma unroll
-    for (int c = 0; c < WB_CPT; ++c)
-      if (c0 + c < c1) atomicAdd(gx + ((long)b * C + c0 + c) * HW + o, bl.w[k] * g[c]);
-  }
 }
 
 // mask[y][x] = (|warp(grid+flo01, flo10) - grid|_1 < thr)
@@ -620,29 +709,34 @@ int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, i
   return vst_launch_status();
 }
 
+// workspace: [cnt: n ints][off: n + 1 ints][block totals][entries: up to 4 per pixel], 16-B aligned
+static long align16(long x) { return (x + 15) / 16 * 16; }
 long vst_warp_bwd_workspace(int B, int H, int W) {
-  const long n = (long)B * H * W;
-  return n * 16 + n * WG_SLOTS * (long)sizeof(WgEntry) + n * 4;  // rec, entries, cnt
+  const long n = (long)B * H * W, nb = (n + WS_BLOCK - 1) / WS_BLOCK;
+  return align16(n * 4) + align16((n + 1) * 4) + align16((nb + 1) * 4) + 4 * n * (long)sizeof(WgEntry);
 }
 
 int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* workspace, int B, int C, int H, int W,
                         int accumulate, void* stream) {
   VST_CHECK_ARG(gout && flo && gx && workspace && B > 0 && C > 0 && H > 0 && W > 0);
   VST_CHECK_ARG(((uintptr_t)workspace & 15) == 0);
-  const long n = (long)B * H * W;
-  VST_CHECK_ARG(n * WG_SLOTS < (1L << 31));
+  const long n = (long)B * H * W, nb = (n + WS_BLOCK - 1) / WS_BLOCK;
+  VST_CHECK_ARG(4 * n < (1L << 31));
   hipStream_t st = (hipStream_t)stream;
-  // [rec: 4 ints per pixel (16-B aligned int4 reads)][entries][counts]
   char* base = static_cast<char*>(workspace);
-  int* rec = reinterpret_cast<int*>(base);
-  WgEntry* ent = reinterpret_cast<WgEntry*>(base + n * 16);
-  int* cnt = reinterpret_cast<int*>(base + n * 16 + n * WG_SLOTS * (long)sizeof(WgEntry));
+  int* cnt = reinterpret_cast<int*>(base);
+  int* off = reinterpret_cast<int*>(base + align16(n * 4));
+  int* bsum = reinterpret_cast<int*>(base + align16(n * 4) + align16((n + 1) * 4));
+  WgEntry* ent = reinterpret_cast<WgEntry*>(base + align16(n * 4) + align16((n + 1) * 4) + align16((nb + 1) * 4));
   hipError_t e = hipMemsetAsync(cnt, 0, n * 4, st);
   if (e != hipSuccess) return (int)e;
-  warp_inv_fill_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, ent, rec, B, H, W);
+  warp_inv_count_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, B, H, W);
+  scan_blocks_kernel<<<nb, 256, 0, st>>>(cnt, off, bsum, n);
+  scan_totals_kernel<<<1, 1024, 0, st>>>(bsum, (int)nb, off + n);
+  scan_add_kernel<<<nb, 256, 0, st>>>(off, bsum, n);
+  warp_inv_fill_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, off, ent, B, H, W);
   dim3 g(ceil_div(n, 256), (C + WB_CPT - 1) / WB_CPT);
-  warp_inv_gather_kernel<<<g, 256, 0, st>>>(gout, cnt, ent, gx, B, C, H, W, accumulate);
-  warp_inv_overflow_kernel<<<g, 256, 0, st>>>(gout, flo, rec, gx, B, C, H, W);
+  warp_inv_gather_kernel<<<g, 256, 0, st>>>(gout, off, ent, gx, B, C, H, W, accumulate);
   return vst_launch_status();
 }
 

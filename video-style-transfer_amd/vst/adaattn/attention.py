@@ -98,7 +98,7 @@ def _ones(n, like):
     if v is None:
         v = ops.persistent(torch.ones(n, device=like.device, dtype=torch.float32))
         _ONES[key] = v
-    return v
+    return ops.constant(v)
 
 
 def attn_gemm(x, M, K, b, P, rb, cg, ra=None, rd=None, role="attn", transpose=False):
@@ -462,6 +462,7 @@ def instance_norm_plain(x, eps=1e-5):
     key = (x.device, C)
     wb = _AFFINE_ID.get(key)
     if wb is None:
+        # (one event after both fills: the zeros are enqueued last)
         wb = (torch.ones(C, device=x.device), ops.persistent(torch.zeros(C, device=x.device)))
         _AFFINE_ID[key] = wb
-    return ops.instance_norm(x, wb[0], wb[1], eps=eps)
+    return ops.instance_norm(x, wb[0], ops.constant(wb[1]), eps=eps)

@@ -117,7 +117,7 @@ class ImageSimilarityFn(Function):
         Gc, unc, vnc, Gs, uns, vns, colc, cols, s1, s2 = ctx.saved_tensors
         N, C, P = s1.shape
         dG = _empty((N, C, C), s1)
-        dun = torch.zeros((N, C), device=s1.device, dtype=torch.float32)
+        dun = _empty((N, C), s1)
         dvn = _empty((N, C), s1)
         lib.vst_simloss_bwd(ptr(Gc), ptr(unc), ptr(vnc), ptr(Gs), ptr(uns), ptr(vns), ptr(colc), ptr(cols),
                             ptr(g.contiguous()), ctx.weight, ptr(dG), ptr(dun), ptr(dvn), N, C, P, stream())

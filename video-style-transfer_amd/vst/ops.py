@@ -331,14 +331,33 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     kh = ks if kh is None else kh
     if out is None:
         out = _empty((N, M, Ho, Wo), src)
+    pad_x = pad if pad_x is None else pad_x
+    mode = gemm_mode()
+    ws, nws = splitk_workspace(src, N, Cs, M, Ho, Wo, kh, ks, gmode, stride, pad, pad_x, up, epi, a_batch_stride, mode)
     tok = kprof.begin(algo_flops if algo_flops is not None else 2.0 * N * M * Ho * Wo * Cs * ks * kh,
                       4.0 * (src.numel() + wpack.numel() + out.numel()),
-                      (N, Cs, Hs, Ws, M, Ho, Wo, kh, ks, gmode, stride, pad, up), gemm_mode())
+                      (N, Cs, Hs, Ws, M, Ho, Wo, kh, ks, gmode, stride, pad, up), mode)
     lib.vst_conv_gemm_padx(ptr(src), ptr(wpack), ptr(bias), ptr(mask), ptr(out), N, Cs, Hs, Ws, M, kh * ks * Cs, Ho,
-                           Wo, kh, ks, gmode, stride, pad, pad if pad_x is None else pad_x, up, epi, a_batch_stride,
-                           ptr(aux), ptr(gmask), gemm_mode(), stream())
+                           Wo, kh, ks, gmode, stride, pad, pad_x, up, epi, a_batch_stride, ptr(aux), ptr(gmask), ptr(ws),
+                           nws, mode, stream())
     kprof.end(tok)
     return out
+
+
+_SPLITK_WS = {}  # launch geometry -> split-K workspace bytes (vst_conv_splitk_workspace; host arithmetic)
+EPI_PADOUT = 128
+
+
+def splitk_workspace(like, *geom):
+    """(workspace tensor or None, bytes) for a conv GEMM launch of geometry `geom`
+    (vst_conv_splitk_workspace's arguments): the split-K scratch comes from PyTorch's caching
+    allocator on the current stream, so the library never allocates (include/vst_hip.h)."""
+    nb = _SPLITK_WS.get(geom)
+    if nb is None:
+        nb = _SPLITK_WS[geom] = int(lib.vst_conv_splitk_workspace(*geom))
+    if nb <= 0:
+        return None, 0
+    return _empty(((nb + 3) // 4,), like), nb
 
 
 def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=None):
@@ -392,10 +411,13 @@ def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dmask=None):
     wp = packed_weight(w, transposed=True)
     dx = _empty(x_shape, gz)
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
+    mode = gemm_mode()
+    ws, nws = splitk_workspace(gz, N, Cout, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 0, 1,
+                               EPI_PADOUT | (EPI_MASK if dmask is not None else 0), 0, mode)
     tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
-                      (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), gemm_mode())
+                      (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), mode)
     lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
-                              gemm_mode(), stream())
+                              ptr(ws), nws, mode, stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dmask), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -661,12 +683,31 @@ def side_branch(*inputs):
     return _SideBranch(inputs)
 
 
+_CONST_FILL = {}  # id(constant) -> (event after its fill, streams ordered after that event)
+
+
 def persistent(t):
     """A lazily created constant kept in a module-level cache (read afterwards from either stream):
-    its fill kernels complete before it is handed out, so a first use on the side stream cannot race
-    the current stream's reads (one synchronisation per constant, on first creation only)."""
+    an event is recorded after its fill on the creating stream; `constant(t)` makes any other
+    stream wait for that event the first time it reads t (no host synchronisation)."""
     if t.is_cuda:
-        torch.cuda.current_stream(t.device).synchronize()
+        cur = torch.cuda.current_stream(t.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        _CONST_FILL[id(t)] = (ev, {cur})
+    return t
+
+
+def constant(t):
+    """Hand out a `persistent` constant on the current stream: a stream other than the one that
+    filled it first waits on the fill's event (once per stream).  Cached constants are never freed,
+    so their ids stay unique."""
+    e = _CONST_FILL.get(id(t))
+    if e is not None:
+        cur = torch.cuda.current_stream(t.device)
+        if cur not in e[1]:
+            cur.wait_event(e[0])
+            e[1].add(cur)
     return t
 
 
@@ -1319,7 +1360,6 @@ def tensor_to_frames(y, bgr=True, clamped=None, frames=None):
     return frames
 
 
-_DIFF_WS = {}
 FRAME_MSE_WS_BYTES = 16384  # VST_FRAME_MSE_WS_BYTES (include/vst_hip.h)
 
 
@@ -1329,10 +1369,8 @@ def frame_diff_mse(x0, x1, y0, y1, out):
         _check(t, n)
         if t.shape != x0.shape:
             raise VstError(f"{n}: shape {tuple(t.shape)} != {tuple(x0.shape)}")
-    dev = x0.device
-    ws = _DIFF_WS.get(dev)
-    if ws is None:
-        ws = _DIFF_WS[dev] = torch.empty(FRAME_MSE_WS_BYTES // 4, dtype=torch.float32, device=dev)
+    # per-call workspace from the caching allocator (stream-ordered reuse; no scratch shared by streams)
+    ws = torch.empty(FRAME_MSE_WS_BYTES // 4, dtype=torch.float32, device=x0.device)
     lib.vst_frame_diff_mse(ptr(x0), ptr(x1), ptr(y0), ptr(y1), x0.numel(), ptr(ws), ptr(out), stream())
     return out
 
@@ -1487,8 +1525,10 @@ def _pil_tables(in_size, out_size, device):
     t = _PIL_TABLES.get(key)
     if t is None:
         b, k = pil_bilinear_coeffs(in_size, out_size)
-        t = (torch.from_numpy(b).to(device), torch.from_numpy(k).to(device), k.shape[1])
+        bd = torch.from_numpy(b).to(device)
+        t = (bd, persistent(torch.from_numpy(k).to(device)), k.shape[1])
         _PIL_TABLES[key] = t
+    constant(t[1])  # (the loader's background thread stages on its own stream)
     return t
 
 

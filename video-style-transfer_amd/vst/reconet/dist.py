@@ -38,6 +38,13 @@ def shard_seed(base, rank):
     return base + rank
 
 
+def step_seed(step, rank, base=1234):
+    """numpy seed of the synthetic batch of training step `step` on `rank` (SURVEY.md §8(d):
+    seed = 1234 + step; other ranks draw their own stream [1234 + step, rank], never another
+    rank's or another step's)."""
+    return base + step if rank == 0 else [base + step, rank]
+
+
 def allreduce_grads(flat_g, group=None):
     """Sum the flat gradient over ranks (one collective); return the scale (1/world) that the
     optimizer applies, so the update uses the mean of the per-shard reference gradients."""

@@ -20,14 +20,21 @@ def _smooth(rng, B, H, W, coarse=None, amp=8.0, jitter=None):
     return c, full
 
 
-def frame_pair_batch(seed, B, H, W, mask_fn=None, device="cpu"):
+def frame_pair_parts(seed, B, H, W):
+    """The random draws of one batch (CPU tensors): img1, img2, flow into the future, flow into the
+    past, motion mask -- the occlusion mask is formed from them by frame_pair_batch's mask_fn."""
     rng = np.random.default_rng(seed)
     img1 = torch.from_numpy(rng.uniform(0.0, 255.0, (B, 3, H, W)).astype(np.float32))
     img2 = torch.from_numpy(rng.uniform(0.0, 255.0, (B, 3, H, W)).astype(np.float32))
     fwd_c, flow_future = _smooth(rng, B, H, W)
     _, flow_past = _smooth(rng, B, H, W, coarse=fwd_c, jitter=1.0)
     motion = torch.from_numpy((rng.random((B, H, W)) < 0.9).astype(np.float32))
-    img1, img2, flow_future, flow_past, motion = (t.to(device) for t in (img1, img2, flow_future, flow_past, motion))
+    return img1, img2, flow_future, flow_past, motion
+
+
+def frame_pair_batch(seed, B, H, W, mask_fn=None, device="cpu"):
+    parts = frame_pair_parts(seed, B, H, W)
+    img1, img2, flow_future, flow_past, motion = (t.to(device) for t in parts)
     if mask_fn is None:
         mask = motion
     else:
