@@ -182,8 +182,15 @@ int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS,
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
                      void* stream);
 /* weight gradient, split-K over output pixels with deterministic slab reduction;
- * workspace floats = vst_wgrad_workspace(N, Cout, KS*KS*Cin, Ho*Wo) */
+ * workspace floats = vst_conv_wgrad_workspace(same geometry and mode).  3x3 stride-1 pad-1 convs over
+ * 32-channel multiples with 16-multiple widths (ResidualBlock, the AdaAttN decoder) run on the halo
+ * weight gradient under the split-product modes (bf16x6 / bf16 / fp16): one block owns all nine taps
+ * of 32 input channels and walks a 16-column strip down the rows, the source rows in an LDS ring (each
+ * loaded and split once instead of nine times).  VST_GEMM_PERTAP in `mode` selects the row-tiled
+ * kernel instead (same sums, other fp32 summation order). */
 long vst_wgrad_workspace(int N, int M, int J, int HWo);
+long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
+                              int stride, int pad, int up, int mode);
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
                    int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
                    int mode, void* stream);

@@ -197,9 +197,9 @@ def test_halo_split_k(mode, shape, epi):
     wp = _pack(w, m)
     e = {"bias_relu": EPI_BIAS | EPI_RELU, "mask": EPI_MASK, "accum": EPI_ACCUM}[epi]
     kw = dict(bias=b) if epi == "bias_relu" else dict(mask=mask) if epi == "mask" else {}
-    # the split is planned (the library asks for workspace) except for the full-size residual layer
+    # every shape here under-fills the chip: the split is planned (the library asks for workspace)
     nb = _ws_bytes(N, Cin, Cout, H, W, GM_REFLECT, 1, e, m)
-    assert (nb > 0) == (N * H * W < 4 * 64 * 128), nb
+    assert nb > 0, nb
     assert _ws_bytes(N, Cin, Cout, H, W, GM_REFLECT, 1, e, m | NOSPLIT) == 0
     outs = [_conv(x, wp, Cout, H, W, GM_REFLECT, 1, mm, e, out=base.clone() if epi == "accum" else None, ws=w_, **kw)
             for mm, w_ in ((m, True), (m | NOSPLIT, True), (m, False))]

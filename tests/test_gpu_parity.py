@@ -72,6 +72,8 @@ CONV_CASES = [
     (2, 16, 3, 5, 32, 3, 2, "reflect", 1, None),      # stride 2, 3-row input (border band = all rows)
     (1, 16, 11, 13, 32, 5, 2, "reflect", 1, None),    # stride 2, k5 pad 2 (3x3 phase window)
     (2, 192, 9, 15, 192, 3, 1, "reflect", 1, None),   # residual conv, ragged
+    (2, 192, 10, 32, 192, 3, 1, "reflect", 1, None),  # residual conv, 16-multiple width (halo weight gradient)
+    (1, 64, 7, 48, 128, 3, 1, "zero", 1, "relu"),     # zero-pad conv over 32-channel blocks (halo weight gradient)
     (2, 192, 5, 8, 96, 3, 1, "reflect", 2, None),     # deconv1 (nearest x2 upsample)
     (1, 96, 9, 6, 48, 3, 1, "reflect", 2, None),      # deconv2
     (1, 40, 7, 33, 24, 3, 1, "reflect", 2, None),     # upsample conv, (W+1) over two k-tiles, odd H

@@ -14,7 +14,7 @@ for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
 # the roofline families bench.py prices (vst/kprof.py): every conv fwd / data-gradient launch
 # (halo-tiled + per-tap implicit GEMM) and every weight-gradient launch
 fams = {"conv (conv_halo_kernel + conv_gemm_kernel)": ("conv_halo_kernel", "conv_gemm_kernel"),
-        "wgrad (wgrad2_kernel + wgrad_kernel)": ("wgrad2_kernel", "wgrad_kernel")}
+        "wgrad (wgrad2_kernel + wgrad_kernel + wgrad_halo_kernel)": ("wgrad2_kernel", "wgrad_kernel", "wgrad_halo_kernel")}
 for fname, keys in fams.items():
     sel = [r for r in rows if any(k in r["Name"] for k in keys)]
     calls = sum(int(r["Calls"]) for r in sel)

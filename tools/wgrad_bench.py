@@ -10,8 +10,9 @@ import sys
 
 import torch
 
-# GEMM arithmetic passed to every call (vst_hip.h VST_GEMM_*): 0 f32, 1 bf16x3, 2 bf16, 3 bf16x6
-MODE = int(os.environ.get("BENCH_GEMM_MODE", "3"))
+# GEMM arithmetic passed to every call (vst_hip.h VST_GEMM_*): 0 f32, 1 bf16x3, 2 bf16, 3 bf16x6, 4 f16;
+# BENCH_MODES: several modes as columns (e.g. "3,35": bf16x6 halo / row-tiled via VST_GEMM_PERTAP = 32)
+MODES = [int(m) for m in os.environ.get("BENCH_MODES", os.environ.get("BENCH_GEMM_MODE", "3")).split(",")]
 
 sys.path.insert(0, "video-style-transfer_amd")
 from vst._lib import LIB_PATH, _CTYPES, parse_header  # noqa: E402
@@ -53,7 +54,8 @@ def main():
     paths = sys.argv[1:] or [LIB_PATH]
     libs = [load(p) for p in paths]
     st = torch.cuda.current_stream().cuda_stream
-    res = {(p, s[0]): [] for p in paths for s in SHAPES}
+    cols = [(p, lib, m) for p, lib in zip(paths, libs) for m in MODES]
+    res = {(p, m, s[0]): [] for p, _, m in cols for s in SHAPES}
     bufs = {}
     for s in SHAPES:
         name, N, Cin, H, W, Cout, k, stride, gm, pad, up = s
@@ -65,10 +67,11 @@ def main():
         if name.endswith("_p"):
             ws = torch.empty(libs[0].vst_conv_wgrad_up2_workspace(N, Cin, H, W, Cout), device="cuda")
         else:
-            ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout, k * k * Cin, Ho * Wo), device="cuda")
+            ws = torch.empty(max(libs[0].vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, k, k, gm, stride, pad, up, m)
+                                 for m in MODES), device="cuda")
         bufs[name] = (x, dy, dw, ws, Ho, Wo, 2.0 * N * Cout * Ho * Wo * Cin * k * k)
     for _ in range(5):
-        for p, lib in zip(paths, libs):
+        for p, lib, MODE in cols:
             for s in SHAPES:
                 name, N, Cin, H, W, Cout, k, stride, gm, pad, up = s
                 x, dy, dw, ws, Ho, Wo, fl = bufs[name]
@@ -86,12 +89,12 @@ def main():
                     fn(*args)
                 e1.record()
                 torch.cuda.synchronize()
-                res[(p, name)].append(e0.elapsed_time(e1) / 5)
+                res[(p, MODE, name)].append(e0.elapsed_time(e1) / 5)
     for s in SHAPES:
         fl = bufs[s[0]][-1]
         line = f"{s[0]:10s}"
-        for p in paths:
-            ms = statistics.median(res[(p, s[0])])
+        for p, _, m in cols:
+            ms = statistics.median(res[(p, m, s[0])])
             line += f"  {ms:7.3f} ms {fl / ms / 1e9:6.1f} TF"
         print(line)
 

@@ -14,6 +14,7 @@
 
 #include "vst_common.h"
 #include "vst_hip.h"
+#include "wgrad_halo.h"
 
 namespace {
 
@@ -1095,12 +1096,38 @@ long vst_wgrad_workspace(int N, int M, int J, int HWo) {
   return (long)N * splits_for(N, M, J, HWo) * Mpad * Jpad;
 }
 
+// the halo weight gradient (wgrad_halo.hip) applies: 3x3 stride-1 pad-1 over 32-channel blocks and
+// 16-column strips, a split-product mode, unless the call asks for the row-tiled kernel
+static bool use_wgrad_halo(int Cin, int Hs, int Ws, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
+                           int up, int mode) {
+  return !(mode & VST_GEMM_PERTAP) && Ho == Hs && Wo == Ws &&
+         wgrad_halo_ok(Cin, Hs, Ws, KH, KW, stride, pad, up, gmode, mode);
+}
+
+long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
+                              int stride, int pad, int up, int mode) {
+  if (N <= 0 || Cin <= 0 || Cout <= 0 || Ho <= 0 || Wo <= 0 || KH <= 0 || KW <= 0 || !vst_mode_ok(mode)) return 0;
+  if (use_wgrad_halo(Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
+    return wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws));
+  return vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
+}
+
 int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
                    int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
                    int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
+  if (use_wgrad_halo(Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode)) {
+    const WhPlan p = wgrad_halo_plan(N, Cout, Cin, Hs, Ws);
+    hipStream_t st = (hipStream_t)stream;
+    int rc = wgrad_halo_launch(p, dy, x, workspace, N, Cout, Cin, Hs, Ws, gmode, mode, st);
+    if (rc) return rc;
+    const long total = (long)Cout * 9 * Cin;
+    wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * p.S, Cout, p.Mpad, 9 * Cin, Cin, 3, 3,
+                                                             0, 1.0f, accumulate);
+    return vst_launch_status();
+  }
   long J = (long)KH * KW * Cin;
   int S = splits_for(N, Cout, J, Ho * Wo);
   hipStream_t st = (hipStream_t)stream;

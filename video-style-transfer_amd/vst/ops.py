@@ -496,13 +496,15 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     Ho, Wo = gz.shape[2:]
     if _WGRAD_UP2 and up == 2 and ks == 3 and stride == 1 and pad == 1 and pad_mode == "reflect":
         return conv_wgrad_up2(gz, x, w_shape, out)
-    ws = _empty((lib.vst_wgrad_workspace(N, Cout, ks * ks * Cin, Ho * Wo),), x)
+    gm = GM_REFLECT if pad_mode == "reflect" else GM_ZERO
+    mode = gemm_mode()
+    ws = _empty((lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up, mode),), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
     tok = kprof.begin(2.0 * N * Cout * Ho * Wo * Cin * ks * ks, 4.0 * (gz.numel() + x.numel() + dw.numel()),
-                      ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), gemm_mode())
-    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks,
-                       GM_REFLECT if pad_mode == "reflect" else GM_ZERO, stride, pad, up, int(acc), gemm_mode(), stream())
+                      ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), mode)
+    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up,
+                       int(acc), mode, stream())
     kprof.end(tok, family="wgrad")
     return dw
 
