@@ -15,7 +15,7 @@ import csv
 import json
 import sys
 
-FAMILIES = ("conv_halo_kernel", "conv_gemm_kernel", "wgrad2_kernel", "wgrad_kernel")
+FAMILIES = ("conv_halo_kernel", "conv_gemm_kernel", "wgrad2_kernel", "wgrad_kernel", "wgrad_halo_kernel", "wgrad_reduce_kernel")
 SIMDS = 1024
 
 

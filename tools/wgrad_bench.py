@@ -33,6 +33,10 @@ SHAPES = [
     ("aadec3", 16, 256, 128, 256, 256, 3, 1, 0, 1, 1),
     ("aadec5", 16, 128, 256, 512, 128, 3, 1, 0, 1, 1),
     ("aadec7", 16, 64, 512, 1024, 64, 3, 1, 0, 1, 1),
+    # the same 64-output decoder convs as row-split GEMMs (vst_conv_wgrad_rowsplit, ops.rowsplit_wgrad_ok)
+    ("aadec6_rs", 16, 128, 256, 512, 64, 3, 1, 0, 1, 1),
+    ("aadec6", 16, 128, 256, 512, 64, 3, 1, 0, 1, 1),
+    ("aadec7_rs", 16, 64, 512, 1024, 64, 3, 1, 0, 1, 1),
 ]
 ONLY = os.environ.get("BENCH_ONLY")
 
@@ -66,6 +70,8 @@ def main():
         dw = torch.empty(Cout, Cin, k, k, device="cuda")
         if name.endswith("_p"):
             ws = torch.empty(libs[0].vst_conv_wgrad_up2_workspace(N, Cin, H, W, Cout), device="cuda")
+        elif name.endswith("_rs"):
+            ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout * k, k * Cin, (H + k - 1) * W), device="cuda")
         else:
             ws = torch.empty(max(libs[0].vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, k, k, gm, stride, pad, up, m)
                                  for m in MODES), device="cuda")
@@ -80,6 +86,9 @@ def main():
                 if name.endswith("_p"):
                     args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, 0, MODE, st)
                     fn = lib.vst_conv_wgrad_up2
+                elif name.endswith("_rs"):
+                    args = (dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, k, 0, MODE, st)
+                    fn = lib.vst_conv_wgrad_rowsplit
                 else:
                     fn = lib.vst_conv_wgrad
                 assert fn(*args) == 0

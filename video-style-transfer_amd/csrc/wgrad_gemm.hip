@@ -1124,8 +1124,8 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
     int rc = wgrad_halo_launch(p, dy, x, workspace, N, Cout, Cin, Hs, Ws, gmode, mode, st);
     if (rc) return rc;
     const long total = (long)Cout * 9 * Cin;
-    wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, N * p.S, Cout, p.Mpad, 9 * Cin, Cin, 3, 3,
-                                                             0, 1.0f, accumulate);
+    wgrad_reduce_kernel<<<ceil_div(total, 256), 256, 0, st>>>(workspace, dw, p.NB, Cout, p.Mpad, 9 * Cin, Cin, 3, 3, 0,
+                                                             1.0f, accumulate);
     return vst_launch_status();
   }
   long J = (long)KH * KW * Cin;

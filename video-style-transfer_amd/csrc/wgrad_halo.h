@@ -9,13 +9,13 @@
 struct WhParams {
   const float* a;  // dY [N][M][H][W]
   const float* x;  // X  [N][Cs][H][W]
-  float* slab;     // [N*S][Mpad][9*Cs]
-  int M, Mpad, J, Cs, H, W;
-  int nchunk, rch, G, S;  // row chunks of rch rows; S slabs per image of G (strip, chunk) segments
+  float* slab;     // [NB][Mpad][9*Cs]
+  int M, Mpad, J, Cs, H, W, N;
+  int nchunk, rch, NB;  // row chunks of rch rows; NB blocks (slabs) per (channel block, M tile) pair
 };
 
 struct WhPlan {
-  int Mpad, nchunk, rch, G, S;
+  int Mpad, nchunk, rch, NB;
 };
 
 bool wgrad_halo_ok(int Cs, int H, int W, int KH, int KW, int stride, int pad, int up, int gmode, int mode);

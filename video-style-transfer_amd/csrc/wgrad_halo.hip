@@ -30,17 +30,17 @@ constexpr int WH_BK = 16;  // pixels per k-tile (one output row of a 16-column s
 constexpr int WH_CB = 32;  // input channels per block (one MFMA column tile per tap)
 
 template <int WM, int PREC, int GMODE>
-// (3 waves per SIMD: two 6-wave blocks, four 3-wave blocks or one 12-wave block per CU)
+// (3 waves per SIMD: two 6-wave blocks or one 12-wave block per CU)
 __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) {
   static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo wgrad: bf16x6, bf16 or fp16 products");
   constexpr int NTH = WM * 3 * 64;
   constexpr int BM = WM * 32;
   constexpr int NPC = PREC == 3 ? 3 : 1;   // bf16 pieces per value
   constexpr int LS = NPC * 8 + 4;          // LDS dwords per (row | channel) of a k-tile (+4: conflict-free)
-  constexpr int R = NTH / 64;              // staging: one B task per R threads, A tasks on the rest
-  constexpr int A_TASKS = 4 * BM;          // (row, 4-pixel quarter)
+  constexpr int A_TASKS = 4 * BM;          // (row, 4-pixel quarter): waves 0 .. 2 WM - 1
+  constexpr int B_WAVE = A_TASKS / 64;     // the 128 (channel, 4-pixel quarter) B tasks: the next two waves
   constexpr int OOR = 0x7ffffff0;
-  static_assert(64 * (R - 1) >= A_TASKS, "staging tasks");
+  static_assert(B_WAVE + 2 <= WM * 3, "staging waves");
 
   __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
   __shared__ __attribute__((aligned(16))) float Bs[4][3][WH_CB][LS];  // [ring slot][kw copy][channel]
@@ -57,24 +57,22 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
   const int rest = __builtin_amdgcn_readfirstlane(wk / gx), bz = __builtin_amdgcn_readfirstlane(rest / gy);
   const int c0 = __builtin_amdgcn_readfirstlane((wk - rest * gx) * WH_CB);
   const int m0 = __builtin_amdgcn_readfirstlane((rest - bz * gy) * BM);
-  const int n = __builtin_amdgcn_readfirstlane(bz / P.S);
-  const int sidx = bz - n * P.S;
   const int H = P.H, W = P.W, HW = H * W;
+  // (the image's buffer descriptors, rebuilt per segment: segments of one block may span images)
+  __amdgpu_buffer_rsrc_t asrd, xsrd;
 
-  const float* a_n = P.a + (long)n * P.M * HW;
-  const float* x_n = P.x + (long)n * P.Cs * HW;
-  const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)((long)P.M * HW * 4));
-  const __amdgpu_buffer_rsrc_t xsrd = uniform_rsrc(x_n, (uint32_t)((long)P.Cs * HW * 4));
-
-  // staging task of this thread
-  const bool is_b = (tid % R) == 0;
-  const int bt = tid / R;                                  // B task: channel bt % 32, half bt / 32
-  const int at = (tid / R) * (R - 1) + (tid % R) - 1;      // A task: row at % BM, quarter at / BM
-  const bool a_ok = !is_b && at < A_TASKS;
-  const int a_row = a_ok ? at % BM : 0, a_q = a_ok ? at / BM : 0;
+  // staging task of this thread, wave-uniform kind (no divergent A / B paths inside a wave)
+  const bool is_b = wave == B_WAVE || wave == B_WAVE + 1;
+  const int bt = tid - 64 * B_WAVE;  // B task: (channel, quarter)
+  const int at = tid;   // A task: (row, quarter)
+  const bool a_ok = at < A_TASKS;
+  // (a 16-lane store group = 8 rows x 2 quarters: its ds_write_b64 cover 32 distinct banks with the
+  // 28-dword row stride, where 16 rows of one quarter would hit each bank pair twice)
+  const int a_row = a_ok ? 8 * ((at >> 4) >> 1) + (at & 7) : 0;
+  const int a_q = a_ok ? 2 * ((at >> 4) & 1) + ((at >> 3) & 1) : 0;
   const bool a_live = a_ok && m0 + a_row < P.M;
   const int a_voff = a_live ? ((m0 + a_row) * HW + 4 * a_q) * 4 : OOR;
-  const int b_c = bt & 31, b_h = bt >> 5;
+  const int b_c = 8 * ((bt >> 4) & 3) + (bt & 7), b_q = 2 * ((bt >> 6) & 1) + ((bt >> 3) & 1);  // (same grouping)
   const int b_cbase = (c0 + b_c) * HW;
 
   f32x16 acc[3];
@@ -83,7 +81,7 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-  float rv[10];  // staged values: A (4) or B (10)
+  float rv0[10], rv1[10];  // staged values of one tile (A uses 4, B 6); bf16x6 keeps two tiles in flight
 
   // source row / column maps (reflect or zero border); -1 = zero
   auto src_row = [&](int yy) -> int {
@@ -101,41 +99,37 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
     return (xx >= 0 && xx < W) ? xx : -1;
   };
 
-  // global loads of one k-tile's staging: the dY quarter row (A task) of output row y, or the 10
-  // source values x[c][row(yb)][ox0 + 8h - 1 .. ox0 + 8h + 8] (B task) of logical source row yb
-  auto load_a = [&](int y, int ox0) {
+  // global loads of one k-tile's staging: the dY quarter row (A task) of output row y, or the 6
+  // source values x[c][row(yb)][ox0 + 4q - 1 .. ox0 + 4q + 4] (B task) of logical source row yb
+  auto load_a = [&](float (&rv)[10], int y, int ox0) {
     const int soff = __builtin_amdgcn_readfirstlane((y * W + ox0) * 4);
     const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff, soff, 0));
 #pragma unroll
     for (int e = 0; e < 4; ++e) rv[e] = v[e];
   };
-  auto load_b = [&](int yb, int ox0) {
+  auto load_b = [&](float (&rv)[10], int yb, int ox0) {
     const int sy = src_row(yb);
-    const int x0 = ox0 + 8 * b_h - 1;
-    if (sy >= 0 && x0 >= 0 && x0 + 9 < W) {
+    const int x0 = ox0 + 4 * b_q - 1;
+    if (sy >= 0 && x0 >= 0 && x0 + 5 < W) {
       const int vo = (b_cbase + sy * W + x0) * 4;
       const f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, vo, 0, 0));
-      const f32x4 v1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, vo + 16, 0, 0));
-      const f32x2 v2 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xsrd, vo + 32, 0, 0));
+      const f32x2 v1 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xsrd, vo + 16, 0, 0));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        rv[e] = v0[e];
-        rv[4 + e] = v1[e];
-      }
-      rv[8] = v2[0];
-      rv[9] = v2[1];
+      for (int e = 0; e < 4; ++e) rv[e] = v0[e];
+      rv[4] = v1[0];
+      rv[5] = v1[1];
     } else {
 #pragma unroll
-      for (int e = 0; e < 10; ++e) {
+      for (int e = 0; e < 6; ++e) {
         const int sx = src_col(x0 + e);
         const int vo = (sy >= 0 && sx >= 0) ? (b_cbase + sy * W + sx) * 4 : OOR;
         rv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xsrd, vo, 0, 0));
       }
     }
   };
-  auto load_stage = [&](int y, int yb, int ox0) {
-    if (is_b) load_b(yb, ox0);
-    else if (a_ok) load_a(y, ox0);
+  auto load_stage = [&](float (&rv)[10], int y, int yb, int ox0) {
+    if (is_b) load_b(rv, yb, ox0);
+    else if (a_ok) load_a(rv, y, ox0);
   };
 
   // split a pair into the mode's pieces (packed dwords, element 0 low)
@@ -147,7 +141,7 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
       split2<PREC>(u, v, d[0], l);
     }
   };
-  auto store_a = [&](int buf) {
+  auto store_a = [&](const float (&rv)[10], int buf) {
     if (!a_ok) return;
     uint32_t p0[3], p1[3];
     split_pair(rv[0], rv[1], p0);
@@ -156,26 +150,24 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) *reinterpret_cast<u32x2*>(d + 8 * pc) = u32x2{p0[pc], p1[pc]};
   };
-  auto store_b = [&](int slot) {
-    uint32_t p[5][3];
+  // copy kw holds x[ox0 + i + kw - 1], i = 4q .. 4q + 3: from the quarter's 6 values v = x[ox0 + 4q - 1 ..]
+  // copies 0 and 2 are the pairs (v0 v1)(v2 v3) and (v2 v3)(v4 v5); copy 1 re-pairs them
+  auto store_b = [&](const float (&rv)[10], int slot) {
+    uint32_t p[3][3];
 #pragma unroll
-    for (int q = 0; q < 5; ++q) split_pair(rv[2 * q], rv[2 * q + 1], p[q]);
+    for (int q = 0; q < 3; ++q) split_pair(rv[2 * q], rv[2 * q + 1], p[q]);
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) {
-      uint32_t* d0 = reinterpret_cast<uint32_t*>(&Bs[slot][0][b_c][0]) + 8 * pc + 4 * b_h;
-      uint32_t* d1 = reinterpret_cast<uint32_t*>(&Bs[slot][1][b_c][0]) + 8 * pc + 4 * b_h;
-      uint32_t* d2 = reinterpret_cast<uint32_t*>(&Bs[slot][2][b_c][0]) + 8 * pc + 4 * b_h;
-      *reinterpret_cast<u32x4*>(d0) = u32x4{p[0][pc], p[1][pc], p[2][pc], p[3][pc]};
-      *reinterpret_cast<u32x4*>(d2) = u32x4{p[1][pc], p[2][pc], p[3][pc], p[4][pc]};
-      // kw = 1: values 1..8 = the odd shift, re-paired from neighbouring dwords
-      *reinterpret_cast<u32x4*>(d1) =
-          u32x4{__builtin_amdgcn_alignbit(p[1][pc], p[0][pc], 16), __builtin_amdgcn_alignbit(p[2][pc], p[1][pc], 16),
-                __builtin_amdgcn_alignbit(p[3][pc], p[2][pc], 16), __builtin_amdgcn_alignbit(p[4][pc], p[3][pc], 16)};
+      const int o = 8 * pc + 2 * b_q;
+      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][0][b_c][0]) + o) = u32x2{p[0][pc], p[1][pc]};
+      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][2][b_c][0]) + o) = u32x2{p[1][pc], p[2][pc]};
+      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][1][b_c][0]) + o) =
+          u32x2{__builtin_amdgcn_alignbit(p[1][pc], p[0][pc], 16), __builtin_amdgcn_alignbit(p[2][pc], p[1][pc], 16)};
     }
   };
-  auto store_stage = [&](int buf, int slot) {
-    if (is_b) store_b(slot);
-    else store_a(buf);
+  auto store_stage = [&](const float (&rv)[10], int buf, int slot) {
+    if (is_b) store_b(rv, slot);
+    else store_a(rv, buf);
   };
 
   // the three taps (kh, kw = 0..2) of this wave for k-tile y (A buffer buf)
@@ -213,35 +205,65 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
     }
   };
 
-  // this block's segments: seg = sidx * G + i over (strip, row chunk), strip-major
+  // this block's segments: its share [T bz / NB, T (bz + 1) / NB) of the T = N x strips x row chunks
+  // segments of the tile pair, image-major, then strip, then chunk (consecutive segments of a block
+  // are neighbouring strips of one image)
   const int nstrip = W / WH_BK;
   const int nseg = nstrip * P.nchunk;
-  const int g0 = sidx * P.G, g1 = min(nseg, g0 + P.G);
+  const int T = P.N * nseg;
+  const int g0 = __builtin_amdgcn_readfirstlane((int)((long)T * bz / P.NB));
+  const int g1 = __builtin_amdgcn_readfirstlane((int)((long)T * (bz + 1) / P.NB));
   for (int g = g0; g < g1; ++g) {
-    const int strip = g / P.nchunk, chunk = g - strip * P.nchunk;
+    const int n = g / nseg, gi = g - n * nseg;
+    const int strip = gi / P.nchunk, chunk = gi - strip * P.nchunk;
+    asrd = uniform_rsrc(P.a + (long)n * P.M * HW, (uint32_t)((long)P.M * HW * 4));
+    xsrd = uniform_rsrc(P.x + (long)n * P.Cs * HW, (uint32_t)((long)P.Cs * HW * 4));
     const int ox0 = __builtin_amdgcn_readfirstlane(strip * WH_BK);
     const int y0 = __builtin_amdgcn_readfirstlane(chunk * P.rch);
     const int y1 = __builtin_amdgcn_readfirstlane(min(H, y0 + P.rch));
-    // prologue: source rows y0 - 1 and y0 into their ring slots, then A(y0) and row y0 + 1
+    // prologue: source rows y0 - 1 and y0 into their ring slots, A(y0) and row y0 + 1; the registers
+    // then hold tile y0 + 1's staging
     if (is_b) {
-      load_b(y0 - 1, ox0);
-      store_b((y0 + 3) & 3);
-      load_b(y0, ox0);
-      store_b(y0 & 3);
+      load_b(rv0, y0 - 1, ox0);
+      store_b(rv0, (y0 + 3) & 3);
+      load_b(rv0, y0, ox0);
+      store_b(rv0, y0 & 3);
     }
-    load_stage(y0, y0 + 1, ox0);
-    store_stage(y0 & 1, (y0 + 1) & 3);
+    load_stage(rv0, y0, y0 + 1, ox0);
+    store_stage(rv0, y0 & 1, (y0 + 1) & 3);
+    if (y0 + 1 < y1) load_stage(rv0, y0 + 1, y0 + 2, ox0);
     __syncthreads();
-    for (int y = y0; y < y1; ++y) {
-      const bool more = y + 1 < y1;
-      if (more) load_stage(y + 1, y + 2, ox0);
-      compute(y, y & 1);
-      if (more) store_stage((y + 1) & 1, (y + 2) & 3);
-      __syncthreads();
+    // step y: LDS holds A(y) and source rows y - 1 .. y + 1; the registers hold tile y + 1 (loaded
+    // during step y - 1), stored into the A buffer and ring slot tile y does not read.
+    // Single products: store first, then issue tile y + 2's loads into the same registers and run tile
+    // y's MFMAs over them (the store's wait is exact: no younger load pending).  bf16x6: tile y + 2's
+    // loads go into a second register set before the MFMAs and the store (the VALU-heavy three-way
+    // split) follows them, beside the other waves' MFMAs.  Measured on the residual / decoder shapes
+    // (tools/wgrad_bench.py, one box each): bf16x6 store-first 1.08 / 0.74 of the row-tiled kernel's
+    // time, this order 1.01 / 0.69; fp16 store-first 0.63 / 0.59, the bf16x6 order 0.70 / 0.72.
+    if constexpr (PREC != 3) {
+      for (int y = y0; y < y1; ++y) {
+        if (y + 1 < y1) store_stage(rv0, (y + 1) & 1, (y + 2) & 3);
+        if (y + 2 < y1) load_stage(rv0, y + 2, y + 3, ox0);
+        compute(y, y & 1);
+        __syncthreads();
+      }
+    } else {
+      auto step = [&](int y, float (&cur)[10], float (&nxt)[10]) {
+        if (y + 2 < y1) load_stage(nxt, y + 2, y + 3, ox0);
+        compute(y, y & 1);
+        if (y + 1 < y1) store_stage(cur, (y + 1) & 1, (y + 2) & 3);
+        __syncthreads();
+      };
+      for (int y = y0; y < y1; y += 2) {
+        step(y, rv0, rv1);
+        if (y + 1 < y1) step(y + 1, rv1, rv0);
+      }
     }
   }
 
-  // raw sums of this block's segments: slab[bz][m][(kh*3 + kw)*Cs + c0 + lo]
+  // raw sums of this block's segments: slab[bz][m][(kh*3 + kw)*Cs + c0 + lo] (each tile pair's block
+  // bz writes its own region of slab bz, so the NB slabs together cover every (m, j))
   float* slab = P.slab + (long)bz * P.Mpad * P.J;
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw) {
@@ -256,8 +278,7 @@ __global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) 
 
 template <int PREC, int GMODE>
 void launch_wm(int wm, dim3 g, hipStream_t st, const WhParams& P) {
-  if (wm == 1) wgrad_halo_kernel<1, PREC, GMODE><<<g, 192, 0, st>>>(P);
-  else if (wm == 4) wgrad_halo_kernel<4, PREC, GMODE><<<g, 768, 0, st>>>(P);
+  if (wm == 4) wgrad_halo_kernel<4, PREC, GMODE><<<g, 768, 0, st>>>(P);
   else wgrad_halo_kernel<2, PREC, GMODE><<<g, 384, 0, st>>>(P);
 }
 
@@ -279,40 +300,32 @@ bool wgrad_halo_ok(int Cs, int H, int W, int KH, int KW, int stride, int pad, in
          (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
 }
 
-// Split plan: row chunks of >= 32 rows, S slabs per image each summing G consecutive (strip, chunk)
-// segments.  Chosen like the row-tiled kernel's split count: minimise (waves of blocks at two per
-// CU) x (k-tiles + ring prologue per block) plus the slab write / reduce traffic.
+// Split plan: one resident round of blocks (two per CU; one for the 12-wave 128-row tiles), NB
+// blocks per (channel block, M tile) pair, each summing a contiguous share of the pair's
+// (image, strip, row chunk) segments into its own slab -- NB slabs of Mpad x 9 Cs whatever the batch
+// and image size.  Row chunks halve (down to 16 rows; each costs a two-row ring prologue) until
+// every block has >= 4 segments, so the shares differ by at most a quarter.
 WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W) {
   WhPlan p;
   const int bm = wgrad_halo_bm(M);
   p.Mpad = (M + bm - 1) / bm * bm;
   const int nstrip = W / WH_BK;
-  const long tiles = (long)(Cs / WH_CB) * (p.Mpad / bm);
-  const double slab_b = (double)p.Mpad * 9.0 * Cs * 4.0;
-  const double t_kt = 0.8e-6;  // s per k-tile step of a resident block (18 bf16x6 MFMAs per wave, 3 waves / SIMD)
-  double best = 1e30;
-  p.nchunk = 1, p.G = nstrip, p.S = 1;
-  for (int nchunk = 1; nchunk * 32 <= H || nchunk == 1; nchunk *= 2) {
-    const int rch = (H + nchunk - 1) / nchunk, nseg = nstrip * nchunk;
-    for (int G = 1; G <= nseg; ++G) {
-      const int S = (nseg + G - 1) / G;
-      if ((nseg + S - 1) / S != G) continue;  // (each distinct group size once)
-      const long blocks = tiles * N * S;
-      const long waves = (blocks + 511) / 512;
-      const double t = waves * (double)G * (rch + 2) * t_kt + 2.0 * N * S * slab_b / 5e12;
-      if (t < best * 0.995) {
-        best = t;
-        p.nchunk = nchunk;
-        p.G = G;
-        p.S = S;
-      }
-    }
-  }
+  const int pairs = (Cs / WH_CB) * (p.Mpad / bm);
+  const int slots = 256 * (bm == 128 ? 1 : 2);
+  p.NB = slots / pairs > 1 ? slots / pairs : 1;
+  p.nchunk = 1;
+  while ((long)N * nstrip * p.nchunk < 4L * p.NB && (H + 2 * p.nchunk - 1) / (2 * p.nchunk) >= 16) p.nchunk *= 2;
   p.rch = (H + p.nchunk - 1) / p.nchunk;
+  p.nchunk = (H + p.rch - 1) / p.rch;
+  const long T = (long)N * nstrip * p.nchunk;
+  if (p.NB > T) p.NB = (int)T;
   return p;
 }
 
-long wgrad_halo_slab_floats(int N, int Cs, const WhPlan& p) { return (long)N * p.S * p.Mpad * 9L * Cs; }
+long wgrad_halo_slab_floats(int N, int Cs, const WhPlan& p) {
+  (void)N;
+  return (long)p.NB * p.Mpad * 9L * Cs;
+}
 
 int wgrad_halo_launch(const WhPlan& p, const float* dy, const float* x, float* slab, int N, int M, int Cs, int H,
                       int W, int gmode, int mode, hipStream_t st) {
@@ -328,10 +341,10 @@ int wgrad_halo_launch(const WhPlan& p, const float* dy, const float* x, float* s
   P.W = W;
   P.nchunk = p.nchunk;
   P.rch = p.rch;
-  P.G = p.G;
-  P.S = p.S;
+  P.NB = p.NB;
+  P.N = N;
   const int bm = wgrad_halo_bm(M);
-  dim3 g(Cs / WH_CB, P.Mpad / bm, N * P.S);
+  dim3 g(Cs / WH_CB, P.Mpad / bm, P.NB);
   const int wm = bm / 32;
   switch (vst_mode_arith(mode)) {
     case VST_GEMM_BF16X6: launch_prec<3>(wm, gmode, g, st, P); break;
