@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--replay-input", action="store_true",
+                    help="A/B only: replay the first synthetic batch every step instead of one batch per step")
     ap.add_argument("--no-vgg19", action="store_true", help="skip the VGG19 fwd+dgrad north-star sub-benchmark")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="oracle threads (default: os.cpu_count(), capped by OMP_NUM_THREADS = the box's CPU share)")
@@ -470,7 +472,7 @@ def per_step_batches(args, rank, draw, stage):
 
     from vst.reconet.dist import step_seed
 
-    n = args.warmup + args.steps + args.prof_steps
+    n = 1 if args.replay_input else args.warmup + args.steps + args.prof_steps
     ranks_here = max(int(os.environ.get("LOCAL_WORLD_SIZE", "1")), 1)
     workers = max(1, min(8, (os.cpu_count() or 1) // ranks_here))
     t0 = time.perf_counter()

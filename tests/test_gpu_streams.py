@@ -65,6 +65,7 @@ def _batch(kind):
 def test_side_streams_bitwise(kind, policy):
     from vst import ops
 
+    ops.gemm_role("fwd")  # (applies the environment's policy first, so it is the one restored)
     saved = (ops.WGRAD_SIDE, ops.CONTENT_SIDE, ops.POLICY_NAME[0])
     runs = []
     try:
@@ -78,8 +79,7 @@ def test_side_streams_bitwise(kind, policy):
             runs.append(({k: float(v) for k, v in out.items()}, tr.flat.g.clone(), tr.flat.p.clone()))
     finally:
         ops.WGRAD_SIDE, ops.CONTENT_SIDE = saved[:2]
-        if saved[2] not in (None, "custom"):
-            ops.use_policy(saved[2])
+        ops.use_policy(saved[2])
     (l0, g0, p0) = runs[0]
     assert torch.isfinite(g0).all()
     assert float(g0.abs().max()) > 0
@@ -92,7 +92,7 @@ def test_side_streams_bitwise(kind, policy):
 def test_warp_backward_deterministic_under_converging_flow():
     """The warp adjoint's per-source-pixel lists (CSR, sorted by output pixel before the sum) give
     bitwise identical gradients run after run, also where many taps converge on one source pixel (a
-    flow that folds a whole row band onto a few pixels: long lists take the selection path), and
+    flow that folds a whole row band onto a few pixels: long lists take the queued block sort), and
     match the scatter form in float64 (RC/utilities.py:39-57 backward)."""
     from vst import ops
 

@@ -8,7 +8,7 @@ steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"total kernel time {tot/1e6:.2f} ms  ({tot/1e6/steps:.2f} ms per step over {steps} steps)")
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:45]:
     nm = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
     print(f"{float(r['TotalDurationNs'])/1e6/steps:8.2f} ms/step {float(r['Percentage']):5.1f}% calls={int(r['Calls'])/steps:6.1f} avg={float(r['AverageNs'])/1e3:8.1f}us {nm[:90]}")
 # the roofline families bench.py prices (vst/kprof.py): every conv fwd / data-gradient launch

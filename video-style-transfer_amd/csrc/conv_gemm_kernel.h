@@ -12,19 +12,7 @@ __device__ __forceinline__ f32x4 mk4(float a, float b, float c, float d) {
   return v;
 }
 
-#ifndef VST_CONV_BK
-#define VST_CONV_BK 16
-#endif
-constexpr int BK = VST_CONV_BK;  // k-tile depth (multiple of 16)
-// timing ablations for variant builds only (results are wrong when set): 1 no B split, 2 no B
-// loads, 4 no A loads, 8 no LDS stores in the k loop, 16 no k-loop barrier, 32 no MFMA phase
-#ifndef VST_ABL
-#define VST_ABL 0
-#endif
-#ifndef VST_B4_SWZ
-#define VST_B4_SWZ 1
-#endif
-constexpr int ABL = VST_ABL;
+constexpr int BK = 16;  // k-tile depth
 constexpr int NT = 256;
 
 struct ConvParams {
@@ -307,8 +295,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   // 8 consecutive columns with row group j, so each 16-lane store group hits 16 distinct 2-bank
   // pairs (the plain tid % BN order put columns r and r+8 on the same banks: 2-way conflicts).
   // The gather then reads 8 consecutive pixels per 8 lanes instead of 64 per wave.
-  const int bcol = (ROWSTEP == 4 && VST_B4_SWZ) ? ((tid & 7) | ((tid >> 5) << 3)) % BN : tid % BN;
-  const int brow0 = (ROWSTEP == 4 && VST_B4_SWZ) ? (tid >> 3) & 3 : tid / BN;
+  const int bcol = ROWSTEP == 4 ? ((tid & 7) | ((tid >> 5) << 3)) % BN : tid % BN;
+  const int brow0 = ROWSTEP == 4 ? (tid >> 3) & 3 : tid / BN;
   const int krow0 = PREC ? brow0 * B_PER : brow0;
   const int p = p0 + bcol;
   const bool pvalid = p < HWo;
@@ -382,8 +370,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     } else
 #pragma unroll
     for (int i = 0; i < A_PER; ++i)
-      ra[i] = (ABL & 4) ? f32x4{(float)t, 1.f, 2.f, (float)i}
-                        : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
+      ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff[i], a_soff, 0));
     if (!bthread) {
     } else if (CFAST) {
       // every 16-row group of the tile shares one tap (Cs % 16 == 0): scalar tap decode, one
@@ -405,8 +392,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       const int sstep = __builtin_amdgcn_readfirstlane(KSTEP * plane_i * 4);
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        rb[i] = (ABL & 2) ? __int_as_float(vo + i)
-                          : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
+        rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, i * sstep, 0));
         if (GM) rg[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, i * sstep, 0));
       }
       // advance in select form: a branchy in-place update (`++st_tap` under one flag, `st_c0 += 16`
@@ -461,13 +447,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       uint32_t h[B_PER / 2], m[B_PER / 2], l[B_PER / 2];
 #pragma unroll
       for (int q = 0; q < B_PER / 2; ++q) {
-        if (ABL & 1) {
-          h[q] = __float_as_uint(bv[2 * q]);
-          m[q] = __float_as_uint(bv[2 * q + 1]);
-          l[q] = h[q] ^ m[q];
-        } else {
-          split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
-        }
+        split3_bf16x2(bv[2 * q], bv[2 * q + 1], h[q], m[q], l[q]);
       }
       uint32_t* d = reinterpret_cast<uint32_t*>(&Bsb[bcol][0]);
       if constexpr (ROWSTEP == 4) {  // k = 4*brow0 .. 4*brow0+3: one b64 per piece
@@ -586,11 +566,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
       if (d == 0 || s * KD + d < ntiles) store_tile(As[buf][d], Bs[buf][d], ra0[d], rb0[d], rg0[d]);
   };
   auto compute_stage = [&](int s) {
-    if (!(ABL & 32)) {
 #pragma unroll
-      for (int d = 0; d < KD; ++d)
-        if (d == 0 || s * KD + d < ntiles) compute_tile(s & 1, d);
-    }
+    for (int d = 0; d < KD; ++d)
+      if (d == 0 || s * KD + d < ntiles) compute_tile(s & 1, d);
   };
   load_stage(0);
   store_stage(0, 0);
@@ -599,9 +577,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
   for (int s = 0; s < nst; ++s) {
     if (s + 1 < nst) load_stage(s + 1);
     compute_stage(s);
-    if (s + 1 < nst && !(ABL & 8)) store_stage((s & 1) ^ 1, s + 1);
+    if (s + 1 < nst) store_stage((s & 1) ^ 1, s + 1);
     if (s + 1 < nst) rotate_a();
-    if (!(ABL & 16)) __syncthreads();
+    __syncthreads();
   }
 
   int pix[TN];

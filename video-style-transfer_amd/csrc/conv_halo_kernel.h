@@ -341,9 +341,6 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
 #ifndef VST_HALO_SMINW_SP
 #define VST_HALO_SMINW_SP 4  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
 #endif
-#ifndef VST_HALO_PD_X6
-#define VST_HALO_PD_X6 0  // 1: two patches in flight for the bf16x6 8-wave tiles too
-#endif
 #ifndef VST_HALO_PD
 #define VST_HALO_PD 2  // patches in flight for the single-product double-buffered tiles
 #endif
@@ -369,7 +366,7 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // 144, conv5 123 -> 89; config 5 145.07 -> 141.5 ms, profiles/r04_halo_pd.txt).  Not on the 4-wave
   // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
   // bf16x6 (MFMA-bound, registers spoken for)
-  constexpr int PD = ((PR != 3 || VST_HALO_PD_X6) && halo_db_c(C) && KC == 1 && WM * WN >= 8) ? VST_HALO_PD : 1;
+  constexpr int PD = (PR != 3 && halo_db_c(C) && KC == 1 && WM * WN >= 8) ? VST_HALO_PD : 1;
   conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC, PD><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 

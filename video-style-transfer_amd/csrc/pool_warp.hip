@@ -278,8 +278,9 @@ __global__ void warp_bwd_kernel(const float* __restrict__ gout, const float* __r
 // per-source-pixel lists in CSR form (the flow is shared by all channels) -- a counting pass, an
 // exclusive scan of the counts, a fill pass -- then each source pixel q sums its list for every
 // channel in increasing p.  The fill pass takes list positions from integer atomics (their order
-// varies run to run), so the gather sorts each list by p before summing: an 8-input sorting network
-// in registers, a selection scan over memory for the rare longer lists (converging flow).
+// varies run to run), so a sort pass orders each list by p first (once per call, not per channel
+// group of the gather): an 8-input sorting network in registers, insertion sort in place for the
+// rare longer lists (converging flow).
 struct WgEntry {
   int p;
   float w;
@@ -396,7 +397,87 @@ __device__ __forceinline__ void wg_cswap(WgEntry& a, WgEntry& b) {
   b = sw ? t : b;
 }
 
-// gx[b][c][q] (+)= sum over q's list, in increasing p, of w * gout[b][c][p]; grid.y: channel groups
+// Batcher's odd-even merge sort network over N (a power of two) register entries, ascending p
+template <int N>
+__device__ __forceinline__ void wg_sort_net(WgEntry (&e)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j <= N - 1 - k; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i <= (k - 1 < N - j - k - 1 ? k - 1 : N - j - k - 1); ++i)
+          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) wg_cswap(e[i + j], e[i + j + k]);
+}
+
+template <int N>
+__device__ __forceinline__ void wg_sort_list(WgEntry* __restrict__ L, int n) {
+  WgEntry e[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) e[j] = j < n ? L[j] : WgEntry{0x7fffffff, 0.f};  // (empty slots sort last)
+  wg_sort_net<N>(e);
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (j < n) L[j] = e[j];
+}
+
+// sort each source pixel's list by output pixel p, once per call (the channel groups of the gather
+// then read it in order): sorting networks in registers for lists of up to 8 / 16 entries; a longer
+// list (strongly converging flow) is queued for warp_inv_sort_long_kernel, so no wave waits on one
+// thread's long sort.  p is unique within a list, so the order is fully determined.
+__global__ void warp_inv_sort_kernel(const int* __restrict__ off, WgEntry* __restrict__ ent, long n_src,
+                                     int* __restrict__ long_count, int* __restrict__ long_queue) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_src) return;
+  const int s0 = off[idx], n = off[idx + 1] - s0;
+  if (n <= 1) return;
+  if (n <= 8) wg_sort_list<8>(ent + s0, n);
+  else if (n <= 16) wg_sort_list<16>(ent + s0, n);
+  else long_queue[atomicAdd(long_count, 1)] = (int)idx;  // (queue order is irrelevant)
+}
+
+// the queued long lists, one wave per list (grid-stride over the device-side count): the list is
+// staged in the wave's LDS slice and every entry is written to its rank (the number of entries with
+// a smaller p); a list beyond the slice (not seen on smooth flows) is insertion-sorted by one lane
+constexpr int WG_LONG = 512;
+__global__ __launch_bounds__(256) void warp_inv_sort_long_kernel(const int* __restrict__ off, WgEntry* __restrict__ ent,
+                                                                 const int* __restrict__ long_count,
+                                                                 const int* __restrict__ long_queue) {
+  __shared__ WgEntry sh[4][WG_LONG];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int cnt = *long_count;
+  for (int i = blockIdx.x * 4 + wv; i < cnt; i += gridDim.x * 4) {
+    const int q = long_queue[i];
+    const int s0 = off[q], n = off[q + 1] - s0;
+    WgEntry* L = ent + s0;
+    if (n > WG_LONG) {
+      if (lane == 0)
+        for (int a = 1; a < n; ++a) {
+          const WgEntry v = L[a];
+          int j = a - 1;
+          while (j >= 0 && L[j].p > v.p) {
+            L[j + 1] = L[j];
+            --j;
+          }
+          L[j + 1] = v;
+        }
+      continue;
+    }
+    for (int j = lane; j < n; j += 64) sh[wv][j] = L[j];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int j = lane; j < n; j += 64) {
+      const int pj = sh[wv][j].p;
+      int rank = 0;
+      for (int k = 0; k < n; ++k) rank += sh[wv][k].p < pj;
+      L[rank] = sh[wv][j];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// gx[b][c][q] (+)= sum over q's (sorted) list of w * gout[b][c][p]; grid.y: channel groups of WB_CPT
 __global__ void warp_inv_gather_kernel(const float* __restrict__ gout, const int* __restrict__ off,
                                        const WgEntry* __restrict__ ent, float* __restrict__ gx, int B, int C, int H,
                                        int W, int accumulate) {
@@ -411,44 +492,11 @@ __global__ void warp_inv_gather_kernel(const float* __restrict__ gout, const int
   float s[WB_CPT];
 #pragma unroll
   for (int c = 0; c < WB_CPT; ++c) s[c] = 0.f;
-  if (n <= WG_REG) {
-    WgEntry e[WG_REG];
+  for (int j = 0; j < n; ++j) {
+    const WgEntry e = ent[s0 + j];
 #pragma unroll
-    for (int j = 0; j < WG_REG; ++j) e[j] = j < n ? ent[s0 + j] : WgEntry{0x7fffffff, 0.f};
-    // Batcher's odd-even merge sort network for 8 inputs (19 comparators; empty slots sort last)
-#define WG_CS(i, j) wg_cswap(e[i], e[j])
-    WG_CS(0, 1); WG_CS(2, 3); WG_CS(4, 5); WG_CS(6, 7);
-    WG_CS(0, 2); WG_CS(1, 3); WG_CS(4, 6); WG_CS(5, 7);
-    WG_CS(1, 2); WG_CS(5, 6);
-    WG_CS(0, 4); WG_CS(1, 5); WG_CS(2, 6); WG_CS(3, 7);
-    WG_CS(2, 4); WG_CS(3, 5);
-    WG_CS(1, 2); WG_CS(3, 4); WG_CS(5, 6);
-#undef WG_CS
-#pragma unroll
-    for (int j = 0; j < WG_REG; ++j) {
-      if (j >= n) break;
-#pragma unroll
-      for (int c = 0; c < WB_CPT; ++c)
-        if (c0 + c < c1) s[c] += e[j].w * gb[c * HW + e[j].p];
-    }
-  } else {
-    // long list: take its entries in increasing p by repeated minimum search (p unique per list)
-    int last = -1;
-    for (int it = 0; it < n; ++it) {
-      int bp = 0x7fffffff;
-      float bw = 0.f;
-      for (int j = 0; j < n; ++j) {
-        const WgEntry e = ent[s0 + j];
-        if (e.p > last && e.p < bp) {
-          bp = e.p;
-          bw = e.w;
-        }
-      }
-      last = bp;
-#pragma unroll
-      for (int c = 0; c < WB_CPT; ++c)
-        if (c0 + c < c1) s[c] += bw * gb[c * HW + bp];
-    }
+    for (int c = 0; c < WB_CPT; ++c)
+      if (c0 + c < c1) s[c] += e.w * gb[c * HW + e.p];
   }
   float* xb = gx + ((long)b * C + c0) * HW + q;
 #pragma unroll
@@ -709,11 +757,13 @@ int vst_warp_bwd(const float* gout, const float* flo, float* gx, int B, int C, i
   return vst_launch_status();
 }
 
-// workspace: [cnt: n ints][off: n + 1 ints][block totals][entries: up to 4 per pixel], 16-B aligned
+// workspace: [cnt: n ints + the long-list count][off: n + 1 ints][block totals][long-list queue: n ints]
+// [entries: up to 4 per pixel], 16-B aligned
 static long align16(long x) { return (x + 15) / 16 * 16; }
 long vst_warp_bwd_workspace(int B, int H, int W) {
   const long n = (long)B * H * W, nb = (n + WS_BLOCK - 1) / WS_BLOCK;
-  return align16(n * 4) + align16((n + 1) * 4) + align16((nb + 1) * 4) + 4 * n * (long)sizeof(WgEntry);
+  return align16((n + 1) * 4) + align16((n + 1) * 4) + align16((nb + 1) * 4) + align16(n * 4) +
+         4 * n * (long)sizeof(WgEntry);
 }
 
 int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* workspace, int B, int C, int H, int W,
@@ -724,17 +774,20 @@ int vst_warp_bwd_gather(const float* gout, const float* flo, float* gx, void* wo
   VST_CHECK_ARG(4 * n < (1L << 31));
   hipStream_t st = (hipStream_t)stream;
   char* base = static_cast<char*>(workspace);
-  int* cnt = reinterpret_cast<int*>(base);
-  int* off = reinterpret_cast<int*>(base + align16(n * 4));
-  int* bsum = reinterpret_cast<int*>(base + align16(n * 4) + align16((n + 1) * 4));
-  WgEntry* ent = reinterpret_cast<WgEntry*>(base + align16(n * 4) + align16((n + 1) * 4) + align16((nb + 1) * 4));
-  hipError_t e = hipMemsetAsync(cnt, 0, n * 4, st);
+  int* cnt = reinterpret_cast<int*>(base);  // (cnt[n]: the long-list count)
+  int* off = reinterpret_cast<int*>(base + align16((n + 1) * 4));
+  int* bsum = reinterpret_cast<int*>(base + 2 * align16((n + 1) * 4));
+  int* lq = reinterpret_cast<int*>(base + 2 * align16((n + 1) * 4) + align16((nb + 1) * 4));
+  WgEntry* ent = reinterpret_cast<WgEntry*>(base + 2 * align16((n + 1) * 4) + align16((nb + 1) * 4) + align16(n * 4));
+  hipError_t e = hipMemsetAsync(cnt, 0, (n + 1) * 4, st);
   if (e != hipSuccess) return (int)e;
   warp_inv_count_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, B, H, W);
   scan_blocks_kernel<<<nb, 256, 0, st>>>(cnt, off, bsum, n);
   scan_totals_kernel<<<1, 1024, 0, st>>>(bsum, (int)nb, off + n);
   scan_add_kernel<<<nb, 256, 0, st>>>(off, bsum, n);
   warp_inv_fill_kernel<<<ceil_div(n, 256), 256, 0, st>>>(flo, cnt, off, ent, B, H, W);
+  warp_inv_sort_kernel<<<ceil_div(n, 256), 256, 0, st>>>(off, ent, n, cnt + n, lq);
+  warp_inv_sort_long_kernel<<<256, 256, 0, st>>>(off, ent, cnt + n, lq);
   dim3 g(ceil_div(n, 256), (C + WB_CPT - 1) / WB_CPT);
   warp_inv_gather_kernel<<<g, 256, 0, st>>>(gout, off, ent, gx, B, C, H, W, accumulate);
   return vst_launch_status();

@@ -364,12 +364,6 @@ __global__ __launch_bounds__(NT, MINW) void wgrad_kernel(WgParams P) {
 //   * both operands are split (per PREC) in registers and stored with one ds_write_b128 per
 //     section; 8 consecutive lanes take 8 consecutive LDS rows, so the 28- / 20-dword row stride
 //     puts them on 8 distinct 4-bank groups (conflict-free).
-#ifndef VST_WG_VEC
-#define VST_WG_VEC 1
-#endif
-#ifndef VST_WABL
-#define VST_WABL 0  // timing-ablation builds: 1 no A split, 2 no B split, 3 neither (results wrong)
-#endif
 struct Wg2Params {
   const float* a;    // [N][M][HWo]
   const float* src;  // [N][Cs][Hs][Ws]
@@ -525,17 +519,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
           // stride 1: the 8 source elements are contiguous -> two 16-byte loads (dword-aligned;
           // gfx950 buffer loads take unaligned addresses)
           const int vo = ok ? (rowoff + xv0) * 4 : OOR;
-          if (VST_WG_VEC) {
-            const f32x4 a0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo, 0, 0));
-            const f32x4 a1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo + 16, 0, 0));
+          const f32x4 a0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo, 0, 0));
+          const f32x4 a1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, vo + 16, 0, 0));
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              rb[i][e] = a0[e];
-              rb[i][4 + e] = a1[e];
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 4 * e, 0, 0));
+          for (int e = 0; e < 4; ++e) {
+            rb[i][e] = a0[e];
+            rb[i][4 + e] = a1[e];
           }
         }
       } else {  // border window: per element
@@ -559,16 +548,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   };
 
   // 8 consecutive k (pixels 8*half .. 8*half+7) of one LDS row, in the layout of PREC
-  auto store8 = [&](float* row, int half, const float* v, bool isA) {
-    if (VST_WABL && (VST_WABL == 3 || (VST_WABL == 1) == isA)) {  // timing ablation: no split (wrong results)
-      uint32_t* d = reinterpret_cast<uint32_t*>(row) + 4 * half;
-      const u32x4 x0 = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-      const u32x4 x1 = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
-      *reinterpret_cast<u32x4*>(d) = x0;
-      *reinterpret_cast<u32x4*>(d + 8) = x1;
-      if (PREC == 3) *reinterpret_cast<u32x4*>(d + 16) = x0;
-      return;
-    }
+  auto store8 = [&](float* row, int half, const float* v) {
     if constexpr (PREC == 0) {  // fp32 [hi][s]: k = 2s + hi -> even k at dwords 4*half.., odd at 8 + 4*half..
       *reinterpret_cast<f32x4*>(row + 4 * half) = f32x4{v[0], v[2], v[4], v[6]};
       *reinterpret_cast<f32x4*>(row + 8 + 4 * half) = f32x4{v[1], v[3], v[5], v[7]};
@@ -619,12 +599,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       } else if (A_TASKS % NTH == 0 || tid + i * NTH < A_TASKS) {
         const float v[8] = {ra[i][0][0], ra[i][0][1], ra[i][0][2], ra[i][0][3],
                             ra[i][1][0], ra[i][1][1], ra[i][1][2], ra[i][1][3]};
-        store8(&As[buf][s][a_row[i]][0], a_half[i], v, true);
+        store8(&As[buf][s][a_row[i]][0], a_half[i], v);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i)
-      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][s][b_col[i]][0], b_half[i], rb[i], false);
+      if (B_TASKS % NTH == 0 || tid + i * NTH < B_TASKS) store8(&Bs[buf][s][b_col[i]][0], b_half[i], rb[i]);
   };
   auto advance = [&]() {
     t_ox += BK;
@@ -713,7 +693,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   }
 }
 
-enum { W32 = 0, W64, W96, W128, W192, W64N, W96N, W128N };  // *N: 256-column variants (row-tiled kernel only)
+enum { W32 = 0, W64, W96, W128, W192, W64N, W96N };  // *N: 256-column variants (row-tiled kernel only)
 static int wsel(int M) {
   if (M <= 32) return W32;
   if (M <= 64) return W64;
@@ -841,9 +821,6 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
     case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W128N:
-      if constexpr (PR == 2 || PR == 4) wgrad2_kernel<2, 2, 2, 4, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P);
-      break;
     default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
   }
 }
@@ -851,10 +828,6 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
 // k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
 #ifndef VST_WKD_SP
 #define VST_WKD_SP 2
-#endif
-// 128 x 256 blocks (each wave 64 x 128) for the single-product modes' 128-row tiles
-#ifndef VST_WG128N
-#define VST_WG128N 0
 #endif
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
@@ -912,9 +885,6 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     // the slab layout and the workspace size do not change.
     int cw = c;
     if ((c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
-    const int am = vst_mode_arith(mode);
-    if (VST_WG128N && c == W128 && (am == VST_GEMM_BF16 || am == VST_GEMM_F16) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0)
-      cw = W128N;
     dim3 g(Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
     if (gmode == 0) launch_wg2<0>(cw, g, mode, st, Q);
     else if (gmode == 2) launch_wg2<2>(cw, g, mode, st, Q);

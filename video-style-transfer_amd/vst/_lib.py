@@ -13,8 +13,9 @@ import re
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# VST_LIB_PATH: a library built from the same sources with other compile-time choices (csrc/Makefile
-# VARIANT_FLAGS), for A/B step measurements only (tools/gpu_r04_*.sh)
+# VST_LIB_PATH: a library built from THIS tree's sources with other compile-time choices (csrc/Makefile
+# VARIANT_FLAGS), for A/B step measurements only (tools/gpu_r04_*.sh); its build id must still match
+# the sources here, so it can never be a stale or foreign build
 LIB_PATH = os.environ.get("VST_LIB_PATH") or os.path.join(_HERE, "libvst_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "vst_hip.h")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
@@ -89,7 +90,7 @@ class _Lib:
         # provenance: the library must have been built from the sources of this tree
         built = lib.vst_build_id().decode()
         want = source_build_id() if os.path.isdir(CSRC) else built
-        if built != want and os.environ.get("VST_ALLOW_STALE_BUILD") != "1":
+        if built != want:
             raise VstError(f"libvst_hip.so build id {built} does not match the sources in {CSRC} ({want}): "
                            "stale build, rebuild with `make -C video-style-transfer_amd/csrc`")
         self.build_id = built

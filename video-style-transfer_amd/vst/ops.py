@@ -540,8 +540,14 @@ def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
     is re-read for 3x fewer column tiles (64 x 576 -> 192 x 192 for 64 -> 64)."""
     if rowsplit_ok(Cout, ks, stride, pad_mode, up):
         return True
-    return (RS_WGRAD and Cout <= 64 and Cin >= 64 and ks == 3 and stride == 1 and pad_mode == "reflect" and up == 1
-            and W % 16 == 0)
+    if not (RS_WGRAD and Cout <= 64 and Cin >= 64 and ks == 3 and stride == 1 and pad_mode == "reflect" and up == 1
+            and W % 16 == 0):
+        return False
+    # the halo weight gradient (vst_conv_wgrad: 32-channel multiples, split-product modes) beats the
+    # row-split GEMM on these shapes (fp16 decoder conv6 1.12 vs 1.41 ms, conv7 3.6 vs 4.5 ms at config 5,
+    # tools/wgrad_bench.py); the row-split form stays for the f32 / bf16x3 modes and other widths
+    return not (Cin % 32 == 0 and (gemm_role("wgrad") & 7) in (GEMM_MODES["bf16x6"], GEMM_MODES["bf16"],
+                                                               GEMM_MODES["f16"]))
 
 
 def conv_fwd_rowsplit(x, w, b, epi, aux):
