@@ -38,7 +38,7 @@ def _ref(dy, x, gmode):
 
 
 # (N, Cin, H, W, Cout): residual 192 (ragged rows, several strips), decoder widths, tall (row chunks)
-SHAPES = [(2, 192, 20, 48, 192), (1, 64, 9, 32, 64), (2, 128, 16, 64, 128), (1, 256, 8, 16, 256),
+SHAPES = [(2, 192, 20, 48, 192), (2, 192, 20, 48, 64), (1, 64, 9, 32, 64), (2, 128, 16, 64, 128), (1, 256, 8, 16, 256),
           (1, 32, 70, 16, 64), (3, 96, 13, 32, 192)]
 
 
@@ -79,8 +79,11 @@ def test_halo_wgrad_workspace_query():
     """The workspace query plans exactly what the launch uses; shapes outside the halo kernel's
     domain (odd width, stride 2, fp32 mode) keep the row-tiled kernel's size."""
     q = lib.vst_conv_wgrad_workspace
-    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, BF16X6) > 0
-    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, BF16X6) != q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
+    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, F16) > 0
+    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, F16) != q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
+                                                                        1, 1, F16 | PERTAP)
+    # (bf16x6 192-row layers keep the row-tiled kernel: DESIGN.md §4.6)
+    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, BF16X6) == q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
                                                                            1, 1, BF16X6 | PERTAP)
     assert q(2, 192, 9, 15, 192, 9, 15, 3, 3, 0, 1, 1, 1, BF16X6) == lib.vst_wgrad_workspace(2, 192, 1728, 135)
     assert q(2, 192, 8, 16, 192, 8, 16, 3, 3, 0, 1, 1, 1, 0) == lib.vst_wgrad_workspace(2, 192, 1728, 128)

@@ -1,6 +1,7 @@
 """vst.reconet.loop: sync-free step logging and the reference's epoch loop (host logic, CPU)."""
 import json
 
+import pytest
 import torch
 
 from vst.reconet.loop import StepLog, fit
@@ -77,3 +78,53 @@ def test_fit_adaattn_triples_and_reference_checkpoint_name(tmp_path):
     assert [r["steps"] for r in log.records] == [2, 1]
     assert [r["loss_is"] for r in log.records] == [0.75, 1.5]
     assert (tmp_path / "AdaAttN-video_epoch_1_batchSize_4.pth").exists()
+
+
+def test_fit_fills_the_batch_field_of_the_reference_pattern(tmp_path):
+    """AA_VIDEO_CHECKPOINT (AA/train_video.py:138) passed as is: {batch} comes from checkpoint_fields
+    or the loader's batch_size; a pattern the loop cannot fill raises before training."""
+    from vst.reconet.loop import AA_VIDEO_CHECKPOINT
+
+    B = 4
+    triple = tuple(torch.zeros(B, 3, 8, 16) for _ in range(3))
+    pat = str(tmp_path / AA_VIDEO_CHECKPOINT.replace("./models/", ""))
+    fit(_StubAdaAttN(), [triple], epochs=1, checkpoint=pat, checkpoint_fields={"batch": B})
+    assert (tmp_path / "AdaAttN-video_epoch_1_batchSize_4.pth").exists()
+
+    class Loader(list):
+        batch_size = 2
+
+    fit(_StubAdaAttN(), Loader([triple]), epochs=1, checkpoint=pat)
+    assert (tmp_path / "AdaAttN-video_epoch_1_batchSize_2.pth").exists()
+    with pytest.raises(ValueError):
+        fit(_StubAdaAttN(), [triple], epochs=1, checkpoint=pat)
+
+
+def test_train_state_roundtrip_restores_adam_and_scaler():
+    """train_state / load_train_state (vst/reconet/_flat.py): Adam moments, step count and the loss
+    scaler's state survive a save / load (CPU tensors; the scaler's device state is a plain tensor)."""
+    import io
+
+    from vst.reconet import _flat
+
+    class _Tr:
+        pass
+
+    class _Flat:
+        def __init__(self):
+            self.numel = 5
+            self.m, self.v, self.p = torch.arange(5.0), torch.arange(5.0) * 2, torch.zeros(5)
+
+    src = _Tr()
+    src.flat, src.step_count = _Flat(), 7
+    src.scaler = _flat.LossScaler("cpu", init_scale=2.0 ** 10)
+    src.scaler.state[1] = 3.0
+    buf = io.BytesIO()
+    torch.save(_flat.train_state(src), buf)
+    buf.seek(0)
+    dst = _Tr()
+    dst.flat, dst.step_count, dst.scaler = _Flat(), 0, None
+    dst.flat.m.zero_(), dst.flat.v.zero_()
+    _flat.load_train_state(dst, torch.load(buf, weights_only=True))
+    assert dst.step_count == 7 and torch.equal(dst.flat.m, src.flat.m) and torch.equal(dst.flat.v, src.flat.v)
+    assert dst.scaler.state_dict() == src.scaler.state_dict()

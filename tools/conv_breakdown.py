@@ -20,6 +20,7 @@ def main():
     sys.argv = [sys.argv[0], "--model", model]
     args = bench.parse()
     args.batch = args.batch or (8 if model == "reconet" else 4)
+    args.replay_input = True  # (one synthetic batch: the launch shapes are what is measured)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     step = (bench.build_reconet if model == "reconet" else bench.build_adaattn)(args, dev, 0)

@@ -1068,16 +1068,16 @@ long vst_wgrad_workspace(int N, int M, int J, int HWo) {
 
 // the halo weight gradient (wgrad_halo.hip) applies: 3x3 stride-1 pad-1 over 32-channel blocks and
 // 16-column strips, a split-product mode, unless the call asks for the row-tiled kernel
-static bool use_wgrad_halo(int Cin, int Hs, int Ws, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                           int up, int mode) {
+static bool use_wgrad_halo(int Cout, int Cin, int Hs, int Ws, int Ho, int Wo, int KH, int KW, int gmode, int stride,
+                           int pad, int up, int mode) {
   return !(mode & VST_GEMM_PERTAP) && Ho == Hs && Wo == Ws &&
-         wgrad_halo_ok(Cin, Hs, Ws, KH, KW, stride, pad, up, gmode, mode);
+         wgrad_halo_ok(Cout, Cin, Hs, Ws, KH, KW, stride, pad, up, gmode, mode);
 }
 
 long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
                               int stride, int pad, int up, int mode) {
   if (N <= 0 || Cin <= 0 || Cout <= 0 || Ho <= 0 || Wo <= 0 || KH <= 0 || KW <= 0 || !vst_mode_ok(mode)) return 0;
-  if (use_wgrad_halo(Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
+  if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
     return wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws));
   return vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
 }
@@ -1088,7 +1088,7 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
-  if (use_wgrad_halo(Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode)) {
+  if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode)) {
     const WhPlan p = wgrad_halo_plan(N, Cout, Cin, Hs, Ws);
     hipStream_t st = (hipStream_t)stream;
     int rc = wgrad_halo_launch(p, dy, x, workspace, N, Cout, Cin, Hs, Ws, gmode, mode, st);

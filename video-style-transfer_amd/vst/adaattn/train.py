@@ -23,7 +23,7 @@ import os
 import torch
 
 from .. import ops
-from ..reconet._flat import FlatParams, backward_and_adam
+from ..reconet._flat import FlatParams, backward_and_adam, load_train_state, train_state
 from ..reconet.dist import GradBuckets, broadcast_params, world_info
 from .lossfn import global_stylized_loss, image_similarity_loss, local_feature_loss
 from .network import AdaAttnNoConv
@@ -190,6 +190,14 @@ class AdaAttNTrainer:
     def image_step(self, c, s):
         """backward + Adam of `image_losses` (AA/train_image.py:109-110)."""
         return self._update(self.image_losses, c, s)
+
+    def train_state(self):
+        """Adam moments / step count and the fp16 loss scaler's state, for a resume next to the
+        model's state_dict checkpoint (reconet._flat.train_state)."""
+        return train_state(self)
+
+    def load_train_state(self, sd):
+        load_train_state(self, sd)
 
     def step(self, c1, c2=None, s=None):
         return self._update(self.losses, c1, c2, s)

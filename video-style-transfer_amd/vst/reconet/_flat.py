@@ -116,6 +116,29 @@ class LossScaler:
         self.state.copy_(vals)
 
 
+def train_state(trainer):
+    """What a resumed run needs beyond the model's state_dict (which the reference's checkpoint holds,
+    train_candy.py:170 / train_video.py:138): Adam's moments and step count and, under a loss-scaled
+    policy, the dynamic scaler's state -- without it a resumed fp16 run re-learns its scale over the
+    first skipped steps and restarts Adam's bias correction."""
+    return {"step_count": trainer.step_count, "adam_m": trainer.flat.m.detach().cpu(),
+            "adam_v": trainer.flat.v.detach().cpu(),
+            "scaler": None if trainer.scaler is None else trainer.scaler.state_dict()}
+
+
+def load_train_state(trainer, sd):
+    """Inverse of train_state (after the model's own load_state_dict)."""
+    if sd["adam_m"].numel() != trainer.flat.numel:
+        raise ValueError(f"train state holds {sd['adam_m'].numel()} Adam moments, the model {trainer.flat.numel}")
+    trainer.step_count = int(sd["step_count"])
+    trainer.flat.m.copy_(sd["adam_m"])
+    trainer.flat.v.copy_(sd["adam_v"])
+    if sd.get("scaler") is not None:
+        if trainer.scaler is None:
+            trainer.scaler = LossScaler(trainer.flat.p.device)
+        trainer.scaler.load_state_dict(sd["scaler"])
+
+
 def backward_and_adam(trainer, loss):
     """loss.backward(), the data-parallel gradient exchange and one Adam step for a trainer holding
     `flat`, `dp`, `lr`, `betas`, `eps`, `step_count` and `scaler` (the reference's

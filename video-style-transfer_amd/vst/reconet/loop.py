@@ -61,14 +61,24 @@ class StepLog:
         return rec
 
 
-def fit(trainer, loader, epochs, epoch_start=1, log=None, checkpoint=None):
+def fit(trainer, loader, epochs, epoch_start=1, log=None, checkpoint=None, checkpoint_fields=None,
+        train_state=False):
     """train_candy.py:62-170 / train_video.py:64-138: for each epoch, one trainer step per batch of
     the loader (ReCoNet: FramePairLoader (img1, img2, flow, mask) or ImageLoader images; AdaAttN:
     (content1, content2, style) triples), the terms to `log` (StepLog) without a per-step sync, and
-    `torch.save(model.state_dict(), checkpoint.format(epoch=e))` at the end of each epoch when
-    `checkpoint` is given (the reference's patterns, e.g.
-    "./models/Flow_input_1_epoch_{epoch}_batchSize_2.pth", AA_VIDEO_CHECKPOINT with its batch
-    filled in)."""
+    `torch.save(model.state_dict(), checkpoint.format(epoch=e, **checkpoint_fields))` at the end of
+    each epoch when `checkpoint` is given (the reference's patterns, e.g.
+    "./models/Flow_input_1_epoch_{epoch}_batchSize_2.pth", or AA_VIDEO_CHECKPOINT with
+    checkpoint_fields={"batch": B}; a {batch} field left unfilled is the loader's batch size when
+    it has one).  train_state: also save the trainer's resume state (Adam moments, step count, the
+    fp16 loss scaler; trainer.train_state()) next to it as <checkpoint>.train_state -- the
+    reference's checkpoint holds the model alone."""
+    fields = dict(checkpoint_fields or {})
+    if checkpoint and "{batch}" in checkpoint and "batch" not in fields:
+        bs = getattr(loader, "batch_size", None)
+        if bs is None:
+            raise ValueError(f"checkpoint pattern {checkpoint!r} has a {{batch}} field: pass checkpoint_fields")
+        fields["batch"] = bs
     for epoch in range(epoch_start, epochs + 1):
         trainer.model.train()
         for batch in loader:
@@ -84,5 +94,8 @@ def fit(trainer, loader, epochs, epoch_start=1, log=None, checkpoint=None):
         if log is not None:
             log.flush()
         if checkpoint:
-            torch.save(trainer.model.state_dict(), checkpoint.format(epoch=epoch))
+            path = checkpoint.format(epoch=epoch, **fields)
+            torch.save(trainer.model.state_dict(), path)
+            if train_state:
+                torch.save(trainer.train_state(), path + ".train_state")
     return log

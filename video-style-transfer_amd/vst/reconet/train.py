@@ -29,7 +29,7 @@ on its (per-rank) batch.
 import torch
 
 from .. import ops
-from ._flat import FlatParams, backward_and_adam
+from ._flat import FlatParams, backward_and_adam, load_train_state, train_state
 from .dist import GradBuckets, broadcast_params, world_info
 
 LOSS_WEIGHTS = dict(ALPHA=1e5, BETA=2e10, GAMMA=1e-2, LAMBDA_F=1e12, LAMBDA_O=1e7)
@@ -176,6 +176,14 @@ class ReCoNetTrainer:
             return 1.0
         loss.backward(torch.full((), s, device=loss.device))
         return 1.0 / s
+
+    def train_state(self):
+        """Adam moments / step count and the fp16 loss scaler's state, for a resume next to the
+        model's state_dict checkpoint (_flat.train_state)."""
+        return train_state(self)
+
+    def load_train_state(self, sd):
+        load_train_state(self, sd)
 
     def step_batch(self, batch):
         """One step on a loader batch: FramePairLoader's (img1, img2, flow, mask) or, for the
