@@ -235,7 +235,7 @@ def adaattn_level_parity(model, vgg, c, s, ref_form=True):
         fc, fs = list(vgg(c).values()), list(vgg(s).values())
         for i in range(3):
             idx, mod = i + 2, model.adaattn[i]
-            with ops.gemm_scope("stylizer"):
+            with ops.gemm_scope("stylizer"), ops.gemm_scope("attn"):  # (the policy scope AdaAttN's own convs run in)
                 Q = ops.conv2d(instance_norm_plain(feature_down_sample(fc, idx)), mod.f.weight, mod.f.bias)
                 K = ops.conv2d(instance_norm_plain(feature_down_sample(fs, idx)), mod.g.weight, mod.g.bias)
                 V = ops.conv2d(fs[idx], mod.h.weight, mod.h.bias)

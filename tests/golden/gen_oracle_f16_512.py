@@ -1,0 +1,47 @@
+"""Fixture for tests/test_gpu_adaattn.py::test_train_video_f16_512x1024: the ORACLE's fp32 loss terms
+of one train_video forward (AA/train_video.py:84-114) at config 5's frame size, 512x1024 (B = 1), on
+the seeded weights (stylizer 61, VGG19 62) and the seeded triple (vst.synthetic.content_style_batch
+63).  The oracle itself is pinned against the reference's own train_video step at 64x128
+(tests/golden/aa_step.npz, tests/test_oracle_golden.py); this fixture only moves its CPU forward at
+the full frame size (about a minute on 8 cores) out of the GPU test.
+
+    python tests/golden/gen_oracle_f16_512.py      (CPU; writes tests/golden/aa_f16_512.npz)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [REPO, os.path.join(REPO, "video-style-transfer_amd")]
+
+import oracle  # noqa: E402
+from oracle import adaattn_ref as A  # noqa: E402
+from oracle import shapes  # noqa: E402
+from vst.synthetic import content_style_batch  # noqa: E402
+
+SEEDS = (61, 62, 63)
+B, H, W = 1, 512, 1024
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 1)
+    c1, c2, s = content_style_batch(SEEDS[2], B, H, W)
+    P = oracle.seeded_params(shapes.stylizing_network(), SEEDS[0])
+    VP = oracle.seeded_params(shapes.vgg19(), SEEDS[1])
+    t0 = time.time()
+    with torch.no_grad():
+        L = A.adaattn_losses(P, VP, c1, c2, s)
+    out = {k: np.float64(L[k].item()) for k in ("loss", "loss_gs", "loss_lf", "loss_is")}
+    out["seeds"] = np.array(SEEDS)
+    out["shape"] = np.array([B, H, W])
+    out["input_sums"] = np.array([float(t.double().sum()) for t in (c1, c2, s)])
+    np.savez(os.path.join(HERE, "aa_f16_512.npz"), **out)
+    print({k: float(v) for k, v in out.items() if v.ndim == 0}, f"{time.time() - t0:.1f} s")
+
+
+if __name__ == "__main__":
+    main()

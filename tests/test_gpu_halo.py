@@ -9,7 +9,12 @@ The shapes are the training paths' 3x3 layers at reduced size (VGG16 / VGG19 64.
 ReCoNet residual 192, AdaAttN decoder 256 / 128 / 64) plus ragged grids.  These small grids would be
 split over the channel blocks (split-K: fewer than 512 blocks); the bitwise comparisons keep the
 halo launch unsplit (VST_GEMM_NOSPLIT), and the split results are held to the unsplit ones within
-fp32 summation-order rounding and to fp64."""
+fp32 summation-order rounding and to fp64.
+
+The 2x2 form of the same kernel (KS = 2) runs the phase-stacked GEMMs: the stride-2 data gradient
+(four parity phases of the padded grid, EPI_PHASE2, ReCoNet conv2 / conv3, RC/network.py:161-162) and
+the nearest-x2 upsample forward (edge-clamped source grid, UpsampleConvLayer RC/network.py:114-120);
+those are held bitwise to the per-tap kernel and to fp64 the same way."""
 import ctypes
 
 import numpy as np
@@ -21,10 +26,14 @@ from vst._lib import lib
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-BF16, BF16X6, F16 = 2, 3, 4
+BF16X3, BF16, BF16X6, F16 = 1, 2, 3, 4
 KBLOCK, PERTAP, NOSPLIT = 16, 32, 64
 GM_REFLECT, GM_ZERO, GM_TRANSPOSED = 0, 1, 2
 EPI_BIAS, EPI_RELU, EPI_MASK, EPI_ACCUM, EPI_PADOUT = 1, 2, 8, 16, 128
+
+
+# output error vs fp64 (max-norm relative) by product precision
+TOL = {BF16X6: 5e-6, BF16X3: 1e-4, F16: 2e-3, BF16: 2e-2}
 
 
 def _dims(M, K):
@@ -71,7 +80,7 @@ def _rand(*shape, seed=0, scale=1.0):
     return (torch.randn(*shape, generator=g) * scale).to(DEV)
 
 
-MODES = [BF16X6, F16, BF16]
+MODES = [BF16X6, F16, BF16, BF16X3]
 # (N, Cin, H, W, Cout): VGG layers, ReCoNet residual, AdaAttN decoder, ragged tiles
 SHAPES = [(2, 64, 37, 70, 64), (1, 128, 16, 64, 128), (2, 192, 20, 36, 192), (1, 256, 9, 40, 256),
           (1, 64, 12, 33, 512), (1, 32, 7, 31, 256), (2, 16, 5, 3, 64), (1, 256, 8, 16, 128)]
@@ -101,7 +110,7 @@ def test_halo_forward_bitwise(mode, shape, pad_mode):
     if pad_mode == "zero":
         y = y.clamp_min(0)
     err = float((halo.double() - y).abs().max() / y.abs().max())
-    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+    assert err < TOL[mode], err
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -127,7 +136,7 @@ def test_halo_dgrad_bitwise(mode, shape, masked):
     if masked:
         dx = dx * (dmask > 0).double()
     err = float((halo.double() - dx).abs().max() / dx.abs().max())
-    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+    assert err < TOL[mode], err
 
 
 @pytest.mark.parametrize("mode", [BF16X6, F16])
@@ -179,7 +188,7 @@ def test_halo_accumulate_and_fallbacks():
         assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-6
 
 
-@pytest.mark.parametrize("mode", [BF16X6, BF16])  # (fp16 launches are never split)
+@pytest.mark.parametrize("mode", [BF16X6, BF16, F16])
 @pytest.mark.parametrize("shape", [(4, 192, 64, 128, 192), (2, 192, 20, 36, 192), (1, 128, 16, 64, 128),
                                    (1, 256, 8, 16, 128)])
 @pytest.mark.parametrize("epi", ["bias_relu", "mask", "accum"])
@@ -218,7 +227,7 @@ def test_halo_split_k(mode, shape, epi):
     scale = float(y.abs().max())
     assert float((split - whole).abs().max()) / scale < 1e-5  # fp32 summation order over K = 9 Cin
     err = float((split.double() - y).abs().max()) / scale
-    assert err < (5e-6 if mode == BF16X6 else (2e-3 if mode == F16 else 2e-2)), err
+    assert err < TOL[mode], err
 
 
 @pytest.mark.parametrize("threads", [False, True])
@@ -263,3 +272,60 @@ def test_split_k_two_streams(threads):
         assert float((outs[i][0] - ref[i]).abs().max()) / scale < 1e-5
         for r in range(1, reps):
             assert torch.equal(outs[i][r], outs[i][0])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 48, 30, 62, 96), (1, 96, 16, 34, 192), (1, 32, 9, 13, 64), (2, 64, 7, 40, 32)])
+def test_halo2_stride2_dgrad_bitwise(mode, shape):
+    """Stride-2 reflect-pad 3x3 conv input gradient (vst_conv_dgrad_s2): rows ci*4 + phase over the
+    phase grid, 2x2 transposed taps, interior into dx and border into the side buffer, then folded."""
+    N, Cin, H, W, Cout = shape
+    KS, pad = 3, 1
+    Ho, Wo = (H + 2 * pad - KS) // 2 + 1, (W + 2 * pad - KS) // 2 + 1
+    dy = _rand(N, Cout, Ho, Wo, seed=60)
+    w = _rand(Cout, Cin, KS, KS, seed=61, scale=0.05)
+    st = torch.cuda.current_stream().cuda_stream
+    res = []
+    for mm in (mode | KBLOCK, mode | KBLOCK | PERTAP):
+        Mpad, Kpad = _dims(4 * Cin, 4 * Cout)
+        wp = torch.empty(Mpad * Kpad * 3 // 2 if mode == BF16X6 else Mpad * Kpad, device=DEV)
+        assert lib.vst_pack_weight_phase2(w.data_ptr(), wp.data_ptr(), Cout, Cin, KS, Mpad, Kpad, mm, st) == 0
+        dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
+        border = torch.zeros(N, Cin, H + 2 * pad, W + 2 * pad, device=DEV)
+        assert lib.vst_conv_dgrad_s2(dy.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N, Cout, Ho,
+                                     Wo, Cin, H, W, KS, pad, mm, st) == 0
+        lib.vst_fold_border(border.data_ptr(), None, dx.data_ptr(), N * Cin, H, W, pad, st)
+        res.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    x = torch.zeros(N, Cin, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
+    F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w.double(), stride=2).backward(dy.double())
+    err = float((res[0].double() - x.grad).abs().max() / x.grad.abs().max())
+    assert err < TOL[mode], err
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 192, 12, 20, 96), (1, 96, 15, 33, 48), (1, 64, 5, 9, 64), (2, 32, 8, 31, 32)])
+def test_halo2_up2_forward_bitwise(mode, shape):
+    """Nearest-x2 upsample -> reflect pad 1 -> 3x3 conv + bias (vst_conv_up2_fwd): the phase-stacked
+    2x2 GEMM over the (H+1) x (W+1) edge-clamped source grid, four phase rows per channel scattered."""
+    N, Cin, H, W, Cout = shape
+    x = _rand(N, Cin, H, W, seed=62, scale=3.0)
+    w = _rand(Cout, Cin, 3, 3, seed=63, scale=0.05)
+    b = _rand(Cout, seed=64)
+    st = torch.cuda.current_stream().cuda_stream
+    w2 = torch.empty(4 * Cout, Cin, 2, 2, device=DEV)
+    assert lib.vst_up2_phase_weights(w.data_ptr(), w2.data_ptr(), Cout, Cin, st) == 0
+    res = []
+    for mm in (mode | KBLOCK, mode | KBLOCK | PERTAP):
+        wp = _pack(w2, mm)
+        out = torch.full((N, Cout, 2 * H, 2 * W), float("nan"), device=DEV)
+        assert lib.vst_conv_up2_fwd(x.data_ptr(), wp.data_ptr(), b.data_ptr(), out.data_ptr(), N, Cin, H, W, Cout, mm,
+                                    st) == 0
+        res.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    xu = F.interpolate(x.double(), scale_factor=2, mode="nearest")
+    y = F.conv2d(F.pad(xu, (1, 1, 1, 1), mode="reflect"), w.double(), b.double())
+    err = float((res[0].double() - y).abs().max() / y.abs().max())
+    assert err < TOL[mode], err

@@ -82,8 +82,9 @@ def test_halo_wgrad_workspace_query():
     assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, F16) > 0
     assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, F16) != q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
                                                                         1, 1, F16 | PERTAP)
-    # (bf16x6 192-row layers keep the row-tiled kernel: DESIGN.md §4.6)
-    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, BF16X6) == q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
+    # (the kernel choice is the caller's: vst.ops keeps ReCoNet's bf16x6 192-row layers on the
+    # row-tiled kernel by passing VST_GEMM_PERTAP)
+    assert q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1, BF16X6) != q(16, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1,
                                                                            1, 1, BF16X6 | PERTAP)
     assert q(2, 192, 9, 15, 192, 9, 15, 3, 3, 0, 1, 1, 1, BF16X6) == lib.vst_wgrad_workspace(2, 192, 1728, 135)
     assert q(2, 192, 8, 16, 192, 8, 16, 3, 3, 0, 1, 1, 1, 0) == lib.vst_wgrad_workspace(2, 192, 1728, 128)

@@ -1,0 +1,171 @@
+"""Where does the fp16 policy's (config 5) gradient noise come from, and which tensors does it hit?
+
+For each policy variant, two HIP train_video steps on the same seeded weights: one on the triple,
+one on the triple with the content frames nudged by a relative 2^-20 (far below fp16's 2^-11
+resolution, about what a different fp32 summation order does to a conv output).  Reported per
+gradient tensor: the own-norm error of both realisations against the oracle's fp32 step, the cosine
+between the two realisations, and the tensor's cancellation condition
+
+    kappa = || |dZ|^T |x| || / || dZ^T x ||     (weights;  sum |dZ| / |sum dZ| for biases)
+
+from the oracle's own backward (dZ the conv's output gradient, x its input).  A product error u on
+every term of a gradient sum leaves a relative error of about u * kappa on the sum, so a tensor whose
+gradient is a near-cancelling sum inherits the upstream fp16 noise amplified by kappa.
+
+    python tools/f16_sensitivity.py [64x128|128x256 ...]    (GPU; one JSON object per size)
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "video-style-transfer_amd"), os.path.join(REPO, "tests")]
+
+import oracle  # noqa: E402
+from oracle import adaattn_ref as A  # noqa: E402
+from oracle import shapes  # noqa: E402
+
+DEV = "cuda"
+# the fp16 policy as it stood before the loss network's forward left fp16 (round 5), and variants:
+# which further roles leave fp16 (bf16x3: fp32 exponent range, ~2^-16 products).  "f16" is the
+# shipped policy (ops.POLICIES["f16"]).
+F16_BASE = {"stylizer.attn.fwd": "bf16x3", "stylizer.attn.dgrad": "bf16x3", "stylizer.attn.wgrad": "bf16x3",
+            "attn_cosine": "bf16x3", "attn_softmax": "f32", "loss_fwd": "bf16x3", "loss_dgrad": "bf16x3"}
+VARIANTS = {
+    "f16": None,
+    "f16_attn_only": {},
+    "f16+dgrad": {"dgrad": "bf16x3"},
+    "f16+encode_fwd": {"encode.fwd": "bf16x3", "encode.fwd_img": "bf16x3"},
+    "f16+lossnet_fwd": {"lossnet.fwd": "bf16x3", "lossnet.fwd_img": "bf16x3"},
+    "f16+vgg_fwd": {"encode.fwd": "bf16x3", "encode.fwd_img": "bf16x3", "lossnet.fwd": "bf16x3",
+                    "lossnet.fwd_img": "bf16x3"},
+    "f16+dec_fwd": {"stylizer.dec.fwd": "bf16x3"},
+}
+
+
+def oracle_step(B, H, W, seeds):
+    """fp32 oracle step; returns (loss terms, {param: grad}, {param: kappa})."""
+    from vst.synthetic import content_style_batch
+
+    c1, c2, s = content_style_batch(seeds[2], B, H, W)
+    P = oracle.seeded_params(shapes.stylizing_network(), seeds[0], requires_grad=True)
+    VP = oracle.seeded_params(shapes.vgg19(), seeds[1])
+    byid = {id(p): n for n, p in P.items()}
+    rec = []
+    orig = F.conv2d
+
+    def conv2d(x, w, b=None, *a, **k):
+        y = orig(x, w, b, *a, **k)
+        if id(w) in byid:
+            assert not a and not k  # the stylizer's convs: stride 1, no padding (pre-padded input)
+            xd = x.detach()
+            y.register_hook(lambda g, xd=xd, w=w, b=b: rec.append((xd, g.detach(), w, b)))
+        return y
+
+    F.conv2d = conv2d
+    try:
+        L = A.adaattn_losses(P, VP, c1, c2, s)
+        L["loss"].backward()
+    finally:
+        F.conv2d = orig
+    num, den = {}, {}
+    for xd, g, w, b in rec:
+        wn = byid[id(w)]
+        ga = torch.nn.grad.conv2d_weight(xd.abs(), w.shape, g.abs())
+        num[wn] = num.get(wn, 0) + ga
+        if b is not None:
+            bn = byid[id(b)]
+            num[bn] = num.get(bn, 0) + g.abs().sum(dim=(0, 2, 3))
+    kappa = {n: float(num[n].double().norm() / (P[n].grad.double().norm() + 1e-30)) for n in num}
+    return (c1, c2, s), {k: L[k].item() for k in ("loss", "loss_gs", "loss_lf", "loss_is")}, \
+        {n: p.grad.detach().double() for n, p in P.items()}, kappa
+
+
+def hip_step(variant, frames, seeds):
+    from vst import ops
+    from vst.adaattn.network import StylizingNetwork
+    from vst.adaattn.train import AdaAttNTrainer
+    from vst.adaattn.vgg19 import VGG19
+
+    if VARIANTS[variant] is None:
+        ops.use_policy("f16")
+    else:
+        name = "sens_" + variant
+        ops.POLICIES[name] = ("f16", {**F16_BASE, **VARIANTS[variant]})
+        ops.LOSS_SCALE[name] = ops.LOSS_SCALE["f16"]
+        ops.use_policy(name)
+
+    def seeded(m, spec, seed):
+        P = oracle.seeded_params(spec, seed)
+        with torch.no_grad():
+            for n, p in m.named_parameters():
+                p.copy_(P[n])
+        return m.to(DEV)
+
+    model = seeded(StylizingNetwork("cosine"), shapes.stylizing_network(), seeds[0])
+    vgg = seeded(VGG19(), shapes.vgg19(), seeds[1])
+    tr = AdaAttNTrainer(model, vgg, activation="cosine")
+    tr.flat.zero_grad()
+    out = tr.losses(torch.stack(frames).to(DEV))
+    unscale = tr.backward(out["loss"])
+    torch.cuda.synchronize()
+    return {k: out[k].item() for k in ("loss", "loss_gs", "loss_lf", "loss_is")}, \
+        {n: (p.grad * unscale).detach().cpu().double() for n, p in model.named_parameters()}
+
+
+def cos(a, b):
+    a, b = a.reshape(-1), b.reshape(-1)
+    return float(a @ b / (a.norm() * b.norm() + 1e-300))
+
+
+def whole_cos(ga, gb, ref):
+    a = torch.cat([ga[n].reshape(-1) / (ref[n].double().norm() + 1e-30) for n in ref])
+    b = torch.cat([gb[n].reshape(-1) / (ref[n].double().norm() + 1e-30) for n in ref])
+    return cos(a, b)
+
+
+def run(size, seeds=(61, 62, 63), variants=None):
+    H, W = map(int, size.split("x"))
+    frames, lref, gref, kappa = oracle_step(1, H, W, seeds)
+    g = torch.Generator().manual_seed(5)
+    nudge = 1 + 2.0 ** -20 * (2 * torch.randint(0, 2, frames[0].shape, generator=g).float() - 1)
+    frames2 = (frames[0] * nudge, frames[1] * nudge, frames[2])
+    rn = {n: float(v.double().norm()) for n, v in gref.items()}
+    gmax = max(rn.values())
+    live = [n for n in gref if rn[n] >= 1e-6 * gmax]
+    res = {"size": size, "kappa_top": sorted(((round(kappa[n], 1), n) for n in live), reverse=True)[:8], "variants": {}}
+    for v in variants or VARIANTS:
+        l1, g1 = hip_step(v, frames, seeds)
+        l2, g2 = hip_step(v, frames2, seeds)
+        own1 = {n: abs(float(g1[n].norm()) - rn[n]) / rn[n] for n in live}
+        own2 = {n: abs(float(g2[n].norm()) - rn[n]) / rn[n] for n in live}
+        pair = {n: 1 - cos(g1[n], g2[n]) for n in live}
+        ref_c = {n: 1 - cos(g1[n], gref[n]) for n in live}
+        worst = sorted(live, key=lambda n: -max(own1[n], own2[n]))[:6]
+        res["variants"][v] = {
+            "loss_rel": max(abs(l1[k] - lref[k]) / abs(lref[k]) for k in l1),
+            "whole_cos_vs_ref": [whole_cos(g1, gref, gref), whole_cos(g2, gref, gref)],
+            "whole_cos_pair": whole_cos(g1, g2, gref),
+            "worst_own": [(n, round(own1[n], 5), round(own2[n], 5), round(kappa.get(n, 0), 1)) for n in worst],
+            "worst_pair_1mcos": sorted(((round(pair[n], 6), n, round(kappa.get(n, 0), 1)) for n in live), reverse=True)[:5],
+            "worst_ref_1mcos": sorted(((round(ref_c[n], 6), n) for n in live), reverse=True)[:5],
+            # own error / kappa: ~ the upstream per-term noise if the condition explains the spread
+            "own_over_kappa_max": max(max(own1[n], own2[n]) / max(kappa.get(n, 1.0), 1.0) for n in live),
+        }
+        print(json.dumps({size: {v: res["variants"][v]}}), flush=True)
+    return res
+
+
+def main():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    sizes = [a for a in sys.argv[1:] if "x" in a] or ["64x128", "128x256"]
+    variants = [a for a in sys.argv[1:] if a in VARIANTS] or None
+    out = [run(s, variants=variants) for s in sizes]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -352,28 +352,32 @@ struct HaloPlan {
   int hcfg, S, tiles, mpad;
 };
 static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad,
-                          int pad_x, int up, int epi, long a_batch_stride, int mode) {
+                          int pad_x, int up, int epi, long a_batch_stride, int mode, bool gmask_free = true) {
   HaloPlan hp{0, 1, 0, 0};
   const int am = vst_mode_arith(mode);
   // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
   const int pack_bm = cfg_bm(select_cfg(M));
   hp.mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
   const int hcfg = halo_cfg(M, hp.mpad, am == VST_GEMM_BF16X6, (epi & EPI_PADOUT) != 0);
-  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && KH == 3 &&
-                    KW == 3 && stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
-                    (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED) &&
-                    !(epi & (EPI_AFFINE | EPI_PHASE2)) &&
-                    (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
+  // 3x3 taps (stride 1, reflect / zero / transposed gathers), or the 2x2 phase-stacked GEMMs
+  // (EPI_PHASE2: the stride-2 data gradient's transposed gather, the up2 forward's edge clamp)
+  const bool ph2 = (epi & EPI_PHASE2) != 0;
+  const bool taps_ok = ph2 ? (KH == 2 && KW == 2 && (gmode == GM_TRANSPOSED || gmode == GM_CLAMP) && gmask_free)
+                           : (KH == 3 && KW == 3 && (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED));
+  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
+                    stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
+                    !(epi & EPI_AFFINE) &&
+                    (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
   if (!halo) return hp;
   hp.hcfg = hcfg;
   const int bm = 32 * halo_wm(hcfg), th = 4 * halo_wn(hcfg);
   hp.tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
   // split-K when the grid is too small for the chip (AdaAttN config 4's decoder and VGG19 conv4 /
-  // conv5 layers: 128-384 blocks).  Not under fp16: every split launch matches its unsplit launch
-  // to <= 3e-6 (tools/split_diag.py), but the fp16 AdaAttN step amplifies that summation-order change
-  // in its attention-parameter gradients past its own parity bars
+  // conv5 layers: 128-384 blocks); every split launch matches its unsplit launch to <= 3e-6
+  // (tools/split_diag.py).  Not for the phase-stacked epilogue (the reduce writes plain / padded-grid
+  // outputs only).
   const bool kc1 = am == VST_GEMM_BF16X6 || VST_HALO_KC == 1 || !halo_db_c(hcfg);
-  if (kc1 && am != VST_GEMM_F16 && !(mode & VST_GEMM_NOSPLIT))
+  if (kc1 && !ph2 && !(mode & VST_GEMM_NOSPLIT))
     hp.S = halo_ksplit((long)hp.tiles * (hp.mpad / bm) * N, Cs / 16);
   return hp;
 }
@@ -435,7 +439,8 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   // 3x3 stride-1 convs in the channel-blocked K order: the halo-tiled kernel (conv_halo_kernel.h),
   // one A-direct wave per 32 weight rows -- 2 / 4 / 6 / 8 waves as the per-tap kernel's blocks
   const int am = vst_mode_arith(mode);
-  const HaloPlan hp = halo_plan(N, Cs, M, Ho, Wo, KH, KW, gmode, stride, pad, pad_x, up, epi, a_batch_stride, mode);
+  const HaloPlan hp =
+      halo_plan(N, Cs, M, Ho, Wo, KH, KW, gmode, stride, pad, pad_x, up, epi, a_batch_stride, mode, gmask == nullptr);
   if (hp.hcfg) {
     const int hcfg = hp.hcfg, bm = 32 * halo_wm(hcfg);
     P.Mpad = hp.mpad;
@@ -468,9 +473,10 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     }
     dim3 grid(hp.tiles, P.Mpad / bm, N * S);
     const bool gm = gmask != nullptr;
-    if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, hcfg, grid, st, P);
-    else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, hcfg, grid, st, P);
-    else launch_halo_prec<2>(gm, hcfg, grid, st, P);
+    if (am == VST_GEMM_BF16X6) launch_halo_prec<3>(gm, hcfg, KH, grid, st, P);
+    else if (am == VST_GEMM_F16) launch_halo_prec<4>(gm, hcfg, KH, grid, st, P);
+    else if (am == VST_GEMM_BF16X3) launch_halo_prec<1>(gm, hcfg, KH, grid, st, P);
+    else launch_halo_prec<2>(gm, hcfg, KH, grid, st, P);
     if (S > 1) {
       const int HWo = Ho * Wo;
       dim3 rgrid((HWo + 1023) / 1024, N * M);

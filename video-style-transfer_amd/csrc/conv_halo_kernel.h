@@ -35,7 +35,7 @@ constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave
 template <int TN, int PREC, int LS>
 __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&ar)[1][3], const float (*B)[LS],
                                          int lane, int jstride) {
-  constexpr int NPC = PREC == 3 ? 3 : 1;
+  constexpr int NPC = PREC == 3 ? 3 : PREC == 1 ? 2 : 1;
   const int r = lane & 31, h = lane >> 5;
   bf16x8_t b[2][3];
   auto load = [&](int j, bf16x8_t (&d)[3]) {
@@ -56,6 +56,10 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
       a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][1], c[0], a, 0, 0, 0);
       a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[1], a, 0, 0, 0);
       a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[0], a, 0, 0, 0);
+    } else if constexpr (PREC == 1) {  // bf16x3: lo*hi + hi*lo + hi*hi (mfma_bf16_ktile's order)
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][1], c[0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[0][0], c[0], a, 0, 0, 0);
     } else if constexpr (PREC == 4) {
       a = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, ar[0][0]), __builtin_bit_cast(f16x8_t, c[0]),
                                                  a, 0, 0, 0);
@@ -70,22 +74,26 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // oy0 + 4 wn .. +3 (TN = 4 fragments of 32 pixels), so the tile is TH = 4 WN rows x 32 columns and
 // the patch (TH + 2) x 34 pixels.  DB: double-buffered patch (the next channel block's stores need
 // no second barrier) or one buffer (half the LDS: more blocks per CU, two barriers per block).
-// PREC 3: bf16x6 (three bf16 pieces per value); 2 / 4: single bf16 / fp16 product (one piece).
+// PREC 3: bf16x6 (three bf16 pieces per value); 1: bf16x3 (hi / lo pieces, three products); 2 / 4:
+// single bf16 / fp16 product (one piece).
 // KC: 16-channel blocks per stage (one barrier per KC blocks; their patch loads in flight across KC x 9
 // taps).  The single-product modes do one MFMA per fragment pair, so a one-block stage (36 MFMAs per
 // wave) does not cover a first-touch gather of the next patch from HBM (config 5: 67 % of wave time
 // waiting on memory at KC = 1, profiles/r04_mfma_busy_adaattn_c5.json).  Measured, it does not pay:
 // fp16 VGG + residual shapes 2.38 ms at KC = 1, 2.58 ms at 2, 2.61 ms at 4 (the larger stage halves the
 // blocks per CU; profiles/r04_halo_kc.txt), so VST_HALO_KC stays 1 (KC > 1 kept for the record).
-template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1, int PD = 1>
+// KS: taps per side (3: the 3x3 stride-1 convs; 2: the phase-stacked 2x2 GEMMs of the stride-2 data
+// gradient and the nearest-x2 upsample forward, EPI_PHASE2 -- patch (TH + 1) x 33, four taps).
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1, int PD = 1, int KS = 3>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
-  static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo kernel: bf16x6, bf16 or fp16 products");
-  constexpr int TM = 1, TN = 4;
-  constexpr int TH = 4 * WN, HPH = TH + 2, HPW = HTW + 2, HPP = HPH * HPW;
+  static_assert(PREC >= 1 && PREC <= 4, "halo kernel: bf16x3, bf16x6, bf16 or fp16 products");
+  static_assert(KS == 2 || KS == 3, "halo kernel: 2x2 or 3x3 taps");
+  constexpr int TM = 1, TN = 4, NTAP = KS * KS;
+  constexpr int TH = 4 * WN, HPH = TH + KS - 1, HPW = HTW + KS - 1, HPP = HPH * HPW;
   constexpr int NTT = WM * WN * 64;
   constexpr int BM = WM * 32;
   constexpr int AW = PREC == 3 ? 24 : 16;  // packed A dwords per (k-tile, row) (vst_common.h apack_store)
-  constexpr int NPC = PREC == 3 ? 3 : 1;   // bf16 pieces per value in the patch
+  constexpr int NPC = PREC == 3 ? 3 : PREC == 1 ? 2 : 1;  // bf16 pieces per value in the patch
   constexpr int LS = NPC * 8 + 4;          // LDS dwords per patch pixel (+4 pad: conflict-free b128 reads)
   constexpr int NTASK = 2 * HPP;           // (patch pixel, channel octet)
   constexpr int TIT = (NTASK + NTT - 1) / NTT;
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   const int oy0 = ty * TH, ox0 = (tile - ty * tiles_x) * HTW;
   // forward: source row oy - pad + kh; data gradient (transposed, stride 1): dY row oy + pad - kh
   const bool tr = P.gmode == GM_TRANSPOSED;
-  const int y0 = oy0 + (tr ? P.pad - 2 : -P.pad), x0 = ox0 + (tr ? P.pad - 2 : -P.pad);
+  const int y0 = oy0 + (tr ? P.pad - (KS - 1) : -P.pad), x0 = ox0 + (tr ? P.pad - (KS - 1) : -P.pad);
 
   const int plane = P.Hs * P.Ws;
   const long plane_l = (long)plane;
@@ -138,6 +146,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       y = y >= P.Hs ? 2 * P.Hs - 2 - y : y;
       x = abs(x);
       x = x >= P.Ws ? 2 * P.Ws - 2 - x : x;
+    } else if (P.gmode == GM_CLAMP) {  // (the up2 phase forward: the reflect border of the virtual grid)
+      y = min(max(y, 0), P.Hs - 1);
+      x = min(max(x, 0), P.Ws - 1);
     }
     const bool ok = t < NTASK && (unsigned)y < (unsigned)P.Hs && (unsigned)x < (unsigned)P.Ws;
     t_voff[it] = ok ? ((8 * o) * plane + y * P.Ws + x) * 4 : OOR;
@@ -191,10 +202,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #pragma unroll
         for (int q = 0; q < 4; ++q) split2<PREC>(v[2 * q], v[2 * q + 1], h[q], l[q]);
         *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+        if constexpr (PREC == 1) *reinterpret_cast<u32x4*>(d + 8) = u32x4{l[0], l[1], l[2], l[3]};
       }
     }
   };
-  // A fragments of k-tile kt (channel block cb, tap t: kt = 9 cb + t under the blocked K order)
+  // A fragments of k-tile kt (channel block cb, tap t: kt = NTAP cb + t under the blocked K order)
   bf16x8_t arN[TM][3], arC[TM][3];
   auto load_a = [&](int kt, bf16x8_t (&ar)[TM][3]) {
     const int a_soff = __builtin_amdgcn_readfirstlane(((kt * P.Mpad + m0) * AW) * 4);
@@ -206,17 +218,17 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   const int nst_all = P.Cs / (16 * KC);
   const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
   const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
-  // the nine taps of every channel block of stage st, B fragments from patch buffer buf
+  // the taps of every channel block of stage st, B fragments from patch buffer buf
   auto taps = [&](int st, int buf) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int cb = st * KC + kc;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int kh = t / 3, kw = t % 3;
-        const int ph = tr ? 2 - kh : kh, pw = tr ? 2 - kw : kw;  // (tr is block-uniform)
-        const int kt_next = t < 8 ? 9 * cb + t + 1 : 9 * (cb + 1);
-        if (t < 8 || cb + 1 < nst * KC) load_a(kt_next, arN);
+      for (int t = 0; t < NTAP; ++t) {
+        const int kh = t / KS, kw = t % KS;
+        const int ph = tr ? KS - 1 - kh : kh, pw = tr ? KS - 1 - kw : kw;  // (tr is block-uniform)
+        const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : NTAP * (cb + 1);
+        if (t < NTAP - 1 || cb + 1 < nst * KC) load_a(kt_next, arN);
         // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
         // columns lo + pw
         const float(*Bt)[LS] = &Ps[buf][kc][(4 * wn + ph) * HPW + pw];
@@ -227,7 +239,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
     }
   };
   load_into(st0, rv, rgv);
-  load_a(9 * KC * st0, arC);
+  load_a(NTAP * KC * st0, arC);
   store_from(0, rv, rgv);
   if constexpr (PD == 1) {
     __syncthreads();
@@ -344,7 +356,7 @@ inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
 #ifndef VST_HALO_PD
 #define VST_HALO_PD 2  // patches in flight for the single-product double-buffered tiles
 #endif
-template <int C, int PR, bool GM>
+template <int C, int PR, bool GM, int KS = 3>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
   // (the one-buffer tiles already sit at their 128-VGPR budget with one block's staging registers)
@@ -354,10 +366,10 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // budget (measured: the spilling 2x2 tile 1088 us vs 758 us at 3 waves per SIMD on the 64-row VGG
   // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
   // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
-  constexpr int MINW = !halo_db_c(C) ? (PR == 3 ? 3 : VST_HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
+  constexpr int MINW = !halo_db_c(C) ? (PR == 3 || PR == 1 ? 3 : VST_HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
   if constexpr (KC > 1) {
     if ((P.Cs / 16) % KC != 0) {  // (a channel count that does not fill whole stages)
-      conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), 1><<<grid, WM * WN * 64, 0, st>>>(P);
+      conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), 1, 1, KS><<<grid, WM * WN * 64, 0, st>>>(P);
       return;
     }
   }
@@ -367,7 +379,7 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
   // bf16x6 (MFMA-bound, registers spoken for)
   constexpr int PD = (PR != 3 && halo_db_c(C) && KC == 1 && WM * WN >= 8) ? VST_HALO_PD : 1;
-  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC, PD><<<grid, WM * WN * 64, 0, st>>>(P);
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC, PD, KS><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 // only the block shapes the build's selection can reach are instantiated
@@ -379,13 +391,25 @@ void launch_halo(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
   else launch_halo_c<VST_HALO_M256, PR, GM>(grid, st, P);
 }
 
+// the 2x2 phase-stacked GEMMs (no gather mask on their paths): M = 4 x channels, the 128- and 192-row
+// selections (ReCoNet deconv1 / conv3: 384 rows; deconv2 / conv2: 192)
 template <int PR>
-void launch_halo_prec(bool gm, int c, dim3 grid, hipStream_t st, const ConvParams& P) {
-  gm ? launch_halo<PR, true>(c, grid, st, P) : launch_halo<PR, false>(c, grid, st, P);
+void launch_halo2(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (c == VST_HALO_M192) launch_halo_c<VST_HALO_M192, PR, false, 2>(grid, st, P);
+  else if (c == VST_HALO_M128) launch_halo_c<VST_HALO_M128, PR, false, 2>(grid, st, P);
+  else if (c == VST_HALO_M64) launch_halo_c<VST_HALO_M64, PR, false, 2>(grid, st, P);
+  else launch_halo_c<VST_HALO_M256, PR, false, 2>(grid, st, P);
 }
 
-extern template void launch_halo_prec<2>(bool, int, dim3, hipStream_t, const ConvParams&);
-extern template void launch_halo_prec<3>(bool, int, dim3, hipStream_t, const ConvParams&);
-extern template void launch_halo_prec<4>(bool, int, dim3, hipStream_t, const ConvParams&);
+template <int PR>
+void launch_halo_prec(bool gm, int c, int ks, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (ks == 2) launch_halo2<PR>(c, grid, st, P);
+  else gm ? launch_halo<PR, true>(c, grid, st, P) : launch_halo<PR, false>(c, grid, st, P);
+}
+
+extern template void launch_halo_prec<1>(bool, int, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_halo_prec<2>(bool, int, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_halo_prec<3>(bool, int, int, dim3, hipStream_t, const ConvParams&);
+extern template void launch_halo_prec<4>(bool, int, int, dim3, hipStream_t, const ConvParams&);
 
 }  // namespace vstk

@@ -2,5 +2,5 @@
 #include "conv_halo_kernel.h"
 
 namespace vstk {
-template void launch_halo_prec<4>(bool, int, dim3, hipStream_t, const ConvParams&);
+template void launch_halo_prec<4>(bool, int, int, dim3, hipStream_t, const ConvParams&);
 }  // namespace vstk

@@ -293,15 +293,12 @@ void launch_prec(int wm, int gmode, dim3 g, hipStream_t st, const WhParams& P) {
 // block rows (32 x WM) for M weight rows: 64 (the 192- and 64-row layers), 128 for 128-multiples
 static int wgrad_halo_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 
-// Not for the bf16x6 192-row layers (ReCoNet's residual convs): there the halo kernel only ties the
-// row-tiled one in isolation (0.629 vs 0.624 ms, tools/wgrad_bench.py) and, run on the side stream
-// beside the data-gradient GEMMs, overlaps them worse (two 57-KB-LDS blocks per CU): config 3 45.97
-// vs 44.80 ms per step with it, 46.39 vs 46.28 with the side streams off (one box,
-// tools/gpu_r05_l.sh).  Everywhere else it wins: AdaAttN decoder shapes 0.69-0.75 of the row-tiled
-// time under bf16x6, 0.46-0.65 under fp16.
+// Feasibility only (3x3 stride-1 pad-1, 32-channel blocks, 16-column strips); which layers use it is
+// the caller's choice (VST_GEMM_PERTAP in the mode selects the row-tiled kernel: vst/ops.py keeps
+// ReCoNet's bf16x6 residual layers there, where the halo form only ties it and overlaps the
+// data-gradient GEMMs worse on the side stream).
 bool wgrad_halo_ok(int M, int Cs, int H, int W, int KH, int KW, int stride, int pad, int up, int gmode, int mode) {
   const int am = vst_mode_arith(mode);
-  if (am == VST_GEMM_BF16X6 && M % 192 == 0 && M % 128 != 0) return false;
   return VST_WGRAD_HALO && KH == 3 && KW == 3 && stride == 1 && pad == 1 && up == 1 && (gmode == 0 || gmode == 1) &&
          Cs % WH_CB == 0 && W % WH_BK == 0 && H >= 2 && W >= 2 &&
          (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);

@@ -118,7 +118,7 @@ class AdaAttNTrainer:
 
     def encode(self, c1, c2=None, s=None):
         """VGG19 features of the data images (no gradient).  c1 may be a [3, B, 3, H, W] buffer."""
-        with torch.no_grad():
+        with torch.no_grad(), ops.gemm_scope("encode"):
             if c2 is None:
                 T, B = c1.shape[:2]
                 f = self.vgg(c1.reshape(T * B, *c1.shape[2:]))
@@ -145,7 +145,9 @@ class AdaAttNTrainer:
             with torch.no_grad():
                 targets = [self.noconv[i](*args[i]) for i in range(3)]
             side.produced(*targets)
-        fcs = self.vgg(self.model(fc12, fs2, down=down))  # cs1 ++ cs2
+        cs = self.model(fc12, fs2, down=down)  # cs1 ++ cs2
+        with ops.gemm_scope("lossnet"):
+            fcs = self.vgg(cs)
         halves = {k: _halves(v, B) for k, v in fcs.items()}
         fcs1 = {k: h[0] for k, h in halves.items()}
         fcs2 = {k: h[1] for k, h in halves.items()}

@@ -41,7 +41,7 @@ class KernelTimer:
         # modes' peaks, flops / sum(flops_i / peak_i)
         by_mode = {}
         for r in recs:
-            a = by_mode.setdefault(r[6] & ~16 if r[6] is not None else r[6], [0, 0.0, 0.0])  # K-order flag off
+            a = by_mode.setdefault(r[6] & 7 if r[6] is not None else r[6], [0, 0.0, 0.0])  # arithmetic bits only
             a[0] += 1
             a[1] += r[0].elapsed_time(r[1])
             a[2] += r[2]

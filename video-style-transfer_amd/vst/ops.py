@@ -37,6 +37,7 @@ def _check(t, name, ndim=None):
 
 GEMM_MODES = {"f32": 0, "bf16x3": 1, "bf16": 2, "bf16x6": 3, "f16": 4}
 KBLOCK = 16  # VST_GEMM_KBLOCK: channel-blocked K order flag of a conv pack + GEMM call pair
+PERTAP = 32  # VST_GEMM_PERTAP: the per-tap conv / row-tiled weight-gradient kernel for this call
 # where the channel-blocked K order applies (VST_KBLOCK): "res" (default) the loss networks, the
 # ReCoNet stylizer's residual blocks and the AdaAttN decoder (scope "stylizer.dec": no InstanceNorm
 # there, and its 3x3 convs then run on the halo-tiled kernel); "1" nowhere inside a stylizer; "2"
@@ -45,6 +46,7 @@ _KB = os.environ.get("VST_KBLOCK", "res")
 KBLOCK_ON = _KB != "0"
 KBLOCK_STYLIZER = _KB == "2"
 KBLOCK_RES = _KB in ("2", "res")
+KBLOCK_UP2 = KBLOCK_ON and os.environ.get("VST_KBLOCK_UP2", "1") != "0"  # A/B: the up2 phase forward blocked
 # The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
@@ -94,8 +96,8 @@ def _mode_id(mode):
 #     ragged golden step; none -> 0.002); the softmax attention stays exact fp32.
 #   "bf16x3": every GEMM split in two (fails the ragged golden step's gradient tolerance, 1.07).
 #   "bf16": single bf16 products (~2^-8): a reduced-precision option for BASELINE config 5.
-#   "f16": single fp16 products (~2^-11 per operand) with a static loss scale (LOSS_SCALE): the
-#     fp16 MFMA path BASELINE config 5 names.
+#   "f16": single fp16 products (~2^-11 per operand) with a dynamic loss scale starting at
+#     LOSS_SCALE: the fp16 MFMA path BASELINE config 5 names.
 POLICIES = {
     "f32": ("f32", {}),
     "bf16x6": ("bf16x6", {"attn_softmax": "f32"}),
@@ -106,11 +108,17 @@ POLICIES = {
     # attention, whose intermediates G = K^ [V; V^2]^T sum over every style position) and in the
     # image-similarity loss (the C x C cosine-distance matrix gradient) the 2^12-scaled gradients
     # leave fp16's range (tools/nan_diag.py): those products stay on bf16x3 (fp32 exponent range,
-    # ~2^-16; a small share of the step's FLOPs)
+    # ~2^-16; a small share of the step's FLOPs).  So does the loss network's forward over the
+    # stylised frames (scope "lossnet"): its ReLU / max-pool decisions and the feature differences the
+    # losses take route the whole backward, and in fp16 they made the attention-parameter gradients
+    # noise-dominated -- a 2^-20 nudge of the input moved them by up to 9 % (tools/f16_sensitivity.py,
+    # DESIGN.md section 4.4)
     "f16": ("f16", {"stylizer.attn.fwd": "bf16x3", "stylizer.attn.dgrad": "bf16x3", "stylizer.attn.wgrad": "bf16x3",
-                    "attn_cosine": "bf16x3", "attn_softmax": "f32", "loss_fwd": "bf16x3", "loss_dgrad": "bf16x3"}),
+                    "attn_cosine": "bf16x3", "attn_softmax": "f32", "loss_fwd": "bf16x3", "loss_dgrad": "bf16x3",
+                    "lossnet.fwd": "bf16x3", "lossnet.fwd_img": "bf16x3"}),
 }
-# Static loss scale of a policy: the trainers run backward from loss * scale and Adam unscales.
+# Initial loss scale of a policy: the trainers run backward from loss * scale and Adam unscales
+# (fp16: the dynamic scaler starts here, vst/reconet/_flat.py LossScaler).
 # fp16 operands must lie in [6.1e-5, 65504] to keep their 11-bit significand: the step's
 # backward GEMM operands (gradients) reach at most ~0.85 and go down to ~1e-11
 # (profiles/r02_fp16_range.json), so 2^12 lifts all but the smallest into the normal range while
@@ -119,7 +127,7 @@ LOSS_SCALE = {"f16": 2.0 ** 12}
 
 
 def loss_scale():
-    """The static loss scale of the selected policy (1.0 unless the policy computes in fp16)."""
+    """The initial loss scale of the selected policy (1.0 unless the policy computes in fp16)."""
     _ensure_policy()
     return LOSS_SCALE.get(POLICY_NAME[0], 1.0)
 
@@ -184,7 +192,10 @@ def gemm_scope(name):
     "stylizer.res") and policy keys "<scope>.<role>" match the innermost scope first, then each
     enclosing one, then "<role>"."""
     old = _SCOPE[0]
-    _SCOPE[0] = name if old is None else f"{old}.{name}"
+    # re-entering the innermost scope (a module that names itself, called from a parent of the same
+    # name: AdaAttN / Decoder inside StylizingNetwork) leaves it as is, so "stylizer.attn" stays the
+    # key its policy entries name
+    _SCOPE[0] = name if old is None else old if old.rpartition(".")[2] == name else f"{old}.{name}"
     try:
         yield
     finally:
@@ -344,6 +355,7 @@ def conv_gemm(src, wpack, M, ks, Ho, Wo, gmode, stride, pad, up, epi=0, bias=Non
     return out
 
 
+SPLITK = os.environ.get("VST_SPLITK", "1") != "0"  # A/B: no workspace -> every launch runs unsplit
 _SPLITK_WS = {}  # launch geometry -> split-K workspace bytes (vst_conv_splitk_workspace; host arithmetic)
 EPI_PADOUT = 128
 
@@ -352,6 +364,8 @@ def splitk_workspace(like, *geom):
     """(workspace tensor or None, bytes) for a conv GEMM launch of geometry `geom`
     (vst_conv_splitk_workspace's arguments): the split-K scratch comes from PyTorch's caching
     allocator on the current stream, so the library never allocates (include/vst_hip.h)."""
+    if not SPLITK:
+        return None, 0
     nb = _SPLITK_WS.get(geom)
     if nb is None:
         nb = _SPLITK_WS[geom] = int(lib.vst_conv_splitk_workspace(*geom))
@@ -489,6 +503,15 @@ def conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask=None, flops=None):
 _WGRAD_UP2 = os.environ.get("VST_WGRAD_UP2", "1") != "0"  # A/B switch for the phase-stacked up2 path
 
 
+# ReCoNet's bf16x6 residual weight gradients (192 rows) stay on the row-tiled kernel: the halo weight
+# gradient only ties it in isolation (0.629 vs 0.624 ms, tools/wgrad_bench.py) and, on the side stream
+# beside the data-gradient GEMMs, overlaps them worse (two 57-KB-LDS blocks per CU): config 3 45.97 vs
+# 44.80 ms per step with it, 46.39 vs 46.28 with the side streams off (one box, tools/gpu_r05_l.sh).
+# Everywhere else the halo form wins (AdaAttN decoder shapes 0.69-0.75 of the row-tiled time under
+# bf16x6, 0.46-0.65 under fp16).
+WGRAD_HALO_RES = os.environ.get("VST_WGRAD_HALO_RES", "0") != "0"  # A/B
+
+
 def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     gemm_role("wgrad")
     N, Cin, H, W = x.shape
@@ -498,6 +521,8 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
         return conv_wgrad_up2(gz, x, w_shape, out)
     gm = GM_REFLECT if pad_mode == "reflect" else GM_ZERO
     mode = gemm_mode()
+    if not WGRAD_HALO_RES and (mode & 7) == GEMM_MODES["bf16x6"] and Cout % 192 == 0 and Cout % 128 != 0:
+        mode |= PERTAP
     ws = _empty((lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up, mode),), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
@@ -755,7 +780,10 @@ class Conv2dFn(Function):
             lib.vst_conv_cin3_k3(ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, Cout, int(pad_mode == "reflect"),
                                  int(act == "relu"), stream())
         elif UP2_FWD and up == 2 and ks == 3 and stride == 1 and pad == 1 and pad_mode == "reflect" and act is None:
-            # UpsampleConvLayer: phase-stacked 2x2 GEMM on the source grid (tap-summed weights)
+            # UpsampleConvLayer: phase-stacked 2x2 GEMM on the source grid (tap-summed weights), in
+            # the channel-blocked K order (the halo-tiled kernel's 2x2 form)
+            if KBLOCK_UP2:
+                _CUR[0] |= KBLOCK
             w2 = _empty((4 * Cout, Cin, 2, 2), w)
             lib.vst_up2_phase_weights(ptr(w), ptr(w2), Cout, Cin, stream())
             out = _empty((N, Cout, Ho, Wo), x)
