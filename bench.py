@@ -75,9 +75,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed oracle steps (median)")
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--gemm", default=os.environ.get("VST_GEMM_POLICY"),
-                    choices=("bf16x6", "f32", "parity", "bf16x3", "bf16", "f16"),
-                    help="GEMM arithmetic policy (vst.ops.POLICIES); default bf16x6 (fp32-class split products), "
-                         "bf16 for the config-5 AdaAttN shape (BASELINE's half-precision path)")
+                    help="GEMM arithmetic policy, a name in vst.ops.POLICIES (bf16x6, f32, parity, bf16x3, bf16, "
+                         "f16); default bf16x6 (fp32-class split products), f16 for the config-5 AdaAttN shape "
+                         "(BASELINE's half-precision path)")
     return ap.parse_args()
 
 
@@ -494,6 +494,7 @@ def cycle_steps(step_fn, batches):
         it["i"] += 1
         return step_fn(*b)
 
+    step.trainer = getattr(step_fn, "__self__", None)
     return step
 
 
@@ -652,8 +653,9 @@ def default_policy(args):
     if args.gemm:
         return args.gemm
     if args.model == "adaattn" and (args.height, args.width) == (512, 1024):
-        # config 5: BASELINE's fp16 MFMA path (convolutions on fp16 products under a static loss
-        # scale; the attention modules and the image-similarity products on bf16x3).  Single-bf16
+        # config 5: BASELINE's fp16 MFMA path (convolutions on fp16 products under a dynamic loss
+        # scale; the attention modules, the image-similarity products and the loss network's forward
+        # over the stylised frames on bf16x3).  Single-bf16
         # products fail the policy's own bar at this size
         return "f16"
     return "bf16x6"
@@ -872,6 +874,10 @@ def main():
                                           f"({1e3 * prof_elapsed / max(args.prof_steps, 1):.2f} ms/step instrumented)",
                          "share_of_step": ks["total_ms"] / max(1e3 * prof_elapsed, 1e-9)},
         }
+        trainer = getattr(step, "trainer", None)
+        if getattr(trainer, "scaler", None) is not None:
+            # the fp16 dynamic loss scale after the run: skipped (overflowed) steps did no update
+            result["loss_scaler"] = trainer.scaler.state_dict()
         wg = timer.summary("wgrad")
         if wg["launches"]:
             result["roofline"]["wgrad_kernel"] = {"achieved": wg["tflops"], "peak": wg["peak_tflops"],

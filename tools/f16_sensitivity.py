@@ -44,6 +44,28 @@ VARIANTS = {
                     "lossnet.fwd_img": "bf16x3"},
     "f16+dec_fwd": {"stylizer.dec.fwd": "bf16x3"},
 }
+# variants of the SHIPPED policy (ops.POLICIES["f16"]): which of its bf16x3 roles could return to fp16
+SHIPPED_VARIANTS = {
+    "ship-attn_fwd16": {"stylizer.attn.fwd": "f16"},
+    "ship-attn_fwd16_wgrad16": {"stylizer.attn.fwd": "f16", "stylizer.attn.wgrad": "f16"},
+    "ship-attn_all16": {"stylizer.attn.fwd": "f16", "stylizer.attn.dgrad": "f16", "stylizer.attn.wgrad": "f16"},
+}
+
+
+def register(variant):
+    """Add `variant` to ops.POLICIES (with the fp16 initial loss scale); returns its policy name."""
+    from vst import ops
+
+    if variant in SHIPPED_VARIANTS:
+        pol = {**ops.POLICIES["f16"][1], **SHIPPED_VARIANTS[variant]}
+    elif VARIANTS[variant] is None:
+        return "f16"
+    else:
+        pol = {**F16_BASE, **VARIANTS[variant]}
+    name = "sens_" + variant
+    ops.POLICIES[name] = ("f16", pol)
+    ops.LOSS_SCALE[name] = ops.LOSS_SCALE["f16"]
+    return name
 
 
 def oracle_step(B, H, W, seeds):
@@ -90,13 +112,7 @@ def hip_step(variant, frames, seeds):
     from vst.adaattn.train import AdaAttNTrainer
     from vst.adaattn.vgg19 import VGG19
 
-    if VARIANTS[variant] is None:
-        ops.use_policy("f16")
-    else:
-        name = "sens_" + variant
-        ops.POLICIES[name] = ("f16", {**F16_BASE, **VARIANTS[variant]})
-        ops.LOSS_SCALE[name] = ops.LOSS_SCALE["f16"]
-        ops.use_policy(name)
+    ops.use_policy(register(variant))
 
     def seeded(m, spec, seed):
         P = oracle.seeded_params(spec, seed)
@@ -162,7 +178,7 @@ def run(size, seeds=(61, 62, 63), variants=None):
 def main():
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     sizes = [a for a in sys.argv[1:] if "x" in a] or ["64x128", "128x256"]
-    variants = [a for a in sys.argv[1:] if a in VARIANTS] or None
+    variants = [a for a in sys.argv[1:] if a in VARIANTS or a in SHIPPED_VARIANTS] or None
     out = [run(s, variants=variants) for s in sizes]
     print(json.dumps(out))
 
