@@ -45,7 +45,20 @@ VARIANTS = {
     "f16+dec_fwd": {"stylizer.dec.fwd": "bf16x3"},
 }
 # variants of the SHIPPED policy (ops.POLICIES["f16"]): which of its bf16x3 roles could return to fp16
+def _lossnet_slices(*ks):
+    """the shipped policy with the loss network's forward back on fp16 except slices ks"""
+    d = {"lossnet.fwd": "f16", "lossnet.fwd_img": "f16"}
+    for k in ks:
+        d.update({f"lossnet.s{k}.fwd": "bf16x3", f"lossnet.s{k}.fwd_img": "bf16x3"})
+    return d
+
+
 SHIPPED_VARIANTS = {
+    "ship-lossnet1": _lossnet_slices(1),
+    "ship-lossnet12": _lossnet_slices(1, 2),
+    "ship-lossnet123": _lossnet_slices(1, 2, 3),
+    "ship-lossnet345": _lossnet_slices(3, 4, 5),
+    "ship-lossnet1234": _lossnet_slices(1, 2, 3, 4),
     "ship-attn_fwd16": {"stylizer.attn.fwd": "f16"},
     "ship-attn_fwd16_wgrad16": {"stylizer.attn.fwd": "f16", "stylizer.attn.wgrad": "f16"},
     "ship-attn_all16": {"stylizer.attn.fwd": "f16", "stylizer.attn.dgrad": "f16", "stylizer.attn.wgrad": "f16"},

@@ -3,6 +3,8 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r05r_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r05r_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05r_tests.log | head -30; exit 2; }
 VST_WGRAD_SIDE=0 VST_CONTENT_SIDE=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05_prof3 -o run -- \
   python3 bench.py --steps 10 --warmup 2 --prof-steps 0 --no-cpu-baseline --no-vgg19 > gpurun_out/r05_prof3.log 2>&1 || exit 10
 python tools/prof_summary.py gpurun_out/r05_prof3 12 -shapes > gpurun_out/r05_kernel_summary.txt 2>&1

@@ -67,7 +67,7 @@ def main():
             continue
         cyc = a["GRBM_GUI_ACTIVE"] / 8
         wc = a["SQ_WAVE_CYCLES"]
-        mf = a["SQ_INSTS_MFMA"]
+        mf = max(a["SQ_INSTS_MFMA"], 1.0)  # (the reduce kernels issue no MFMA: their ratios are per instruction)
         out["families"][f] = {
             "launches": n,
             "mfma_busy": a["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc),

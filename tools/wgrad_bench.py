@@ -73,8 +73,9 @@ def main():
         elif name.endswith("_rs"):
             ws = torch.empty(libs[0].vst_wgrad_workspace(N, Cout * k, k * Cin, (H + k - 1) * W), device="cuda")
         else:
-            ws = torch.empty(max(libs[0].vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, k, k, gm, stride, pad, up, m)
-                                 for m in MODES), device="cuda")
+            # (each build plans its own split: the largest workspace any of them asks for)
+            ws = torch.empty(max(lb.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, k, k, gm, stride, pad, up, m)
+                                 for lb in libs for m in MODES), device="cuda")
         bufs[name] = (x, dy, dw, ws, Ho, Wo, 2.0 * N * Cout * Ho * Wo * Cin * k * k)
     for _ in range(5):
         for p, lib, MODE in cols:

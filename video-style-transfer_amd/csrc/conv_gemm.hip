@@ -61,11 +61,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvParams P, int N)
 // slices for a halo launch of `wgs` blocks over `nblk` 16-channel blocks: none when the grid
 // already fills the chip; otherwise the fewest equal slices (>= 3 blocks each) that reach two
 // blocks per CU, at most four per CU
-#ifndef VST_HALO_SPLIT
-#define VST_HALO_SPLIT 1
-#endif
 int halo_ksplit(long wgs, int nblk) {
-  if (!VST_HALO_SPLIT || wgs >= 512) return 1;
+  if (wgs >= 512) return 1;
   int best = 1;
   for (int s : {2, 3, 4, 6, 8}) {
     if (nblk % s || nblk / s < 3 || wgs * s > 1024) continue;
@@ -358,13 +355,13 @@ static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, 
   // (the packed A carries vst_conv_pack_dims' Mpad; the halo block's M tile must divide it)
   const int pack_bm = cfg_bm(select_cfg(M));
   hp.mpad = (M + pack_bm - 1) / pack_bm * pack_bm;
-  const int hcfg = halo_cfg(M, hp.mpad, am == VST_GEMM_BF16X6, (epi & EPI_PADOUT) != 0);
+  const int hcfg = halo_cfg(M, hp.mpad);
   // 3x3 taps (stride 1, reflect / zero / transposed gathers), or the 2x2 phase-stacked GEMMs
   // (EPI_PHASE2: the stride-2 data gradient's transposed gather, the up2 forward's edge clamp)
   const bool ph2 = (epi & EPI_PHASE2) != 0;
   const bool taps_ok = ph2 ? (KH == 2 && KW == 2 && (gmode == GM_TRANSPOSED || gmode == GM_CLAMP) && gmask_free)
                            : (KH == 3 && KW == 3 && (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED));
-  const bool halo = VST_HALO && hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
+  const bool halo = hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
                     stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
                     !(epi & EPI_AFFINE) &&
                     (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
@@ -376,8 +373,7 @@ static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, 
   // conv5 layers: 128-384 blocks); every split launch matches its unsplit launch to <= 3e-6
   // (tools/split_diag.py).  Not for the phase-stacked epilogue (the reduce writes plain / padded-grid
   // outputs only).
-  const bool kc1 = am == VST_GEMM_BF16X6 || VST_HALO_KC == 1 || !halo_db_c(hcfg);
-  if (kc1 && !ph2 && !(mode & VST_GEMM_NOSPLIT))
+  if (!ph2 && !(mode & VST_GEMM_NOSPLIT))
     hp.S = halo_ksplit((long)hp.tiles * (hp.mpad / bm) * N, Cs / 16);
   return hp;
 }
@@ -420,7 +416,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     // bf16x6 A-direct blocks: 64-, 128- and 256-row tiles always, the 192-row tile for data
     // gradients only (its forward keeps the LDS-A tile: DESIGN.md §4.2 item 3)
     const bool dg = gmode == GM_TRANSPOSED;
-    if (VST_ADIR && am == VST_GEMM_BF16X6) {
+    if (am == VST_GEMM_BF16X6) {
       if (cfg == T128 && M % 256 == 0) cfg = T256A;
       if (cfg == T128) cfg = T128A;
       if (cfg == T64W || cfg == T64) cfg = T64A;
@@ -429,7 +425,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     // single-product modes (bf16, fp16): A-direct blocks with two k-tiles per stage -- the LDS-A
     // tiles stage 256 weight rows x 32 B per k-tile through LDS for 8 MFMAs per wave, which puts
     // their LDS store traffic past the array's write rate
-    if (VST_ADIR && VST_ADIR_SP && (am == VST_GEMM_BF16 || am == VST_GEMM_F16)) {
+    if (am == VST_GEMM_BF16 || am == VST_GEMM_F16) {
       if (cfg == T256) cfg = T256A;
       if (cfg == T128) cfg = M % 256 == 0 ? T256A : T128A;
       if (cfg == T64W || cfg == T64) cfg = T64A;

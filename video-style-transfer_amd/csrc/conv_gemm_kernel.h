@@ -608,84 +608,52 @@ inline int cfg_bm(int c) {
   return bm[c];
 }
 inline int cfg_bn(int c) { return (c == T32 || c == T64W || c == T96W) ? 256 : 128; }
-#ifndef VST_WIDE
-#define VST_WIDE 1
-#endif
 // 64/96-row tiles on large pixel grids: 256-column tiles (twice the MFMAs per A fragment)
 inline int widen_cfg(int c, long HWo) {
-  if (!VST_WIDE || HWo < 8192) return c;
+  if (HWo < 8192) return c;
   return c == T64 ? T64W : (c == T96 ? T96W : c);
 }
 
-#ifndef VST_MINW_T128
-#define VST_MINW_T128 4
-#endif
-#ifndef VST_MINW_T256
-#define VST_MINW_T256 2
-#endif
-#ifndef VST_MINW_T192
-#define VST_MINW_T192 2
-#endif
-#ifndef VST_MINW_SMALL
-#define VST_MINW_SMALL 4
-#endif
-// bf16 paths: the hi/lo conversion temporaries push the 2x2-accumulator tile past 128 VGPRs
-#ifndef VST_MINW_T128_BF
-#define VST_MINW_T128_BF 3
-#endif
-// bf16x6 A-direct tiles (one wave per 32 weight rows, 128 pixels per block)
-#ifndef VST_ADIR
-#define VST_ADIR 1
-#endif
-// bf16 / fp16 A-direct tiles (VST_ADIR_SP=0: the LDS-A tiles for those modes)
-#ifndef VST_ADIR_SP
-#define VST_ADIR_SP 1
-#endif
-#ifndef VST_MINW_ADIR
-#define VST_MINW_ADIR 3
-#endif
-#ifndef VST_MINW_A256
-#define VST_MINW_A256 4
-#endif
+// waves per SIMD the tiles' registers must allow (occupancy targets, measured per tile)
+constexpr int MINW_T128 = 4, MINW_T256 = 2, MINW_T192 = 2, MINW_SMALL = 4;
+constexpr int MINW_T128_BF = 3;  // bf16 paths: the hi/lo conversion temporaries push the 2x2-accumulator tile past 128 VGPRs
+constexpr int MINW_ADIR = 3, MINW_A256 = 4;  // A-direct tiles (one wave per 32 weight rows, 128 pixels per block)
 
-#ifndef VST_KD2
-#define VST_KD2 1
-#endif
 // two k-tiles per stage for the single-product modes on the 128- and 256-row tiles; the smaller
 // tiles keep one (their two-tile stages exceed the register budget of their occupancy target).
 // Compile-time only: the library has one tested kernel per (shape, mode) -- no run-time switches.
 template <int WM, int TM, int WN, int TN, bool CF, bool GMK, int MINW, int PR, bool ADIR = false, bool KD2OK = false>
 static void launch_k(dim3 grid, hipStream_t st, const ConvParams& P) {
-  constexpr int KD = (VST_KD2 && KD2OK && (PR == 2 || PR == 4)) ? 2 : 1;
+  constexpr int KD = (KD2OK && (PR == 2 || PR == 4)) ? 2 : 1;
   conv_gemm_kernel<WM, TM, WN, TN, CF, GMK, MINW, PR, ADIR, KD><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 template <bool CF, bool GMK, int PR>
 static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) {
-  constexpr bool AD = (PR == 3 || ((PR == 2 || PR == 4) && VST_ADIR_SP)) && VST_ADIR;
+  constexpr bool AD = PR == 3 || PR == 2 || PR == 4;  // A-direct tiles: bf16x6, bf16, fp16
   switch (cfg) {
     case T32: launch_k<1, 1, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
-    case T64: launch_k<1, 2, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
+    case T64: launch_k<1, 2, 4, 1, CF, GMK, MINW_SMALL, PR>(grid, st, P); break;
     case T64A:
-      if constexpr (AD) launch_k<2, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true, true>(grid, st, P);
+      if constexpr (AD) launch_k<2, 1, 1, 4, CF, GMK, MINW_ADIR, PR, true, true>(grid, st, P);
       break;
     case T192A:
       if constexpr (AD) launch_k<6, 1, 1, 4, CF, GMK, 3, PR, true, true>(grid, st, P);
       break;
     case T256A:  // all eight waves gather the B tile (4 elements each)
-      if constexpr (AD) launch_k<8, 1, 1, 4, CF, GMK, VST_MINW_A256, PR, true, true>(grid, st, P);
+      if constexpr (AD) launch_k<8, 1, 1, 4, CF, GMK, MINW_A256, PR, true, true>(grid, st, P);
       break;
-    case T96: launch_k<1, 3, 4, 1, CF, GMK, VST_MINW_SMALL, PR>(grid, st, P); break;
+    case T96: launch_k<1, 3, 4, 1, CF, GMK, MINW_SMALL, PR>(grid, st, P); break;
     case T64W: launch_k<1, 2, 4, 2, CF, GMK, 3, PR>(grid, st, P); break;
     case T96W: launch_k<1, 3, 4, 2, CF, GMK, 2, PR>(grid, st, P); break;
-    case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? VST_MINW_T128_BF : VST_MINW_T128, PR, false, true>(grid, st, P); break;
+    case T128: launch_k<2, 2, 2, 2, CF, GMK, PR ? MINW_T128_BF : MINW_T128, PR, false, true>(grid, st, P); break;
     case T128A:  // four A-direct waves of 32 rows x 128 pixels
-      if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, VST_MINW_ADIR, PR, true, true>(grid, st, P);
+      if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, MINW_ADIR, PR, true, true>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 / fp16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
-      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, VST_MINW_T256, PR, false, true>(grid, st, P);
+      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, MINW_T256, PR, false, true>(grid, st, P);
       break;
-    default: launch_k<2, 3, 2, 2, CF, GMK, VST_MINW_T192, PR>(grid, st, P); break;
+    default: launch_k<2, 3, 2, 2, CF, GMK, MINW_T192, PR>(grid, st, P); break;
   }
 }
 

@@ -21,10 +21,6 @@
 #pragma once
 #include "conv_gemm_kernel.h"
 
-#ifndef VST_HALO
-#define VST_HALO 1
-#endif
-
 namespace vstk {
 
 constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave covers 4 rows of it
@@ -76,15 +72,11 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // no second barrier) or one buffer (half the LDS: more blocks per CU, two barriers per block).
 // PREC 3: bf16x6 (three bf16 pieces per value); 1: bf16x3 (hi / lo pieces, three products); 2 / 4:
 // single bf16 / fp16 product (one piece).
-// KC: 16-channel blocks per stage (one barrier per KC blocks; their patch loads in flight across KC x 9
-// taps).  The single-product modes do one MFMA per fragment pair, so a one-block stage (36 MFMAs per
-// wave) does not cover a first-touch gather of the next patch from HBM (config 5: 67 % of wave time
-// waiting on memory at KC = 1, profiles/r04_mfma_busy_adaattn_c5.json).  Measured, it does not pay:
-// fp16 VGG + residual shapes 2.38 ms at KC = 1, 2.58 ms at 2, 2.61 ms at 4 (the larger stage halves the
-// blocks per CU; profiles/r04_halo_kc.txt), so VST_HALO_KC stays 1 (KC > 1 kept for the record).
-// KS: taps per side (3: the 3x3 stride-1 convs; 2: the phase-stacked 2x2 GEMMs of the stride-2 data
-// gradient and the nearest-x2 upsample forward, EPI_PHASE2 -- patch (TH + 1) x 33, four taps).
-template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int KC = 1, int PD = 1, int KS = 3>
+// One 16-channel block per stage (one barrier per block).  (Several blocks per stage, meant to cover
+// the single-product modes' first-touch gathers, measured slower -- fp16 VGG + residual shapes 2.38 ms
+// at one block, 2.58 at 2, 2.61 at 4: the larger stage halves the resident blocks per CU,
+// profiles/r04_halo_kc.txt -- and was removed in round 5.)
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int PD = 1, int KS = 3>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC >= 1 && PREC <= 4, "halo kernel: bf16x3, bf16x6, bf16 or fp16 products");
   static_assert(KS == 2 || KS == 3, "halo kernel: 2x2 or 3x3 taps");
@@ -99,7 +91,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   constexpr int TIT = (NTASK + NTT - 1) / NTT;
   constexpr int NBUF = DB ? 2 : 1;
   constexpr int OOR = 0x7ffffff0;
-  __shared__ __attribute__((aligned(16))) float Ps[NBUF][KC][HPP][LS];
+  __shared__ __attribute__((aligned(16))) float Ps[NBUF][HPP][LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -162,34 +154,28 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
 
-  float rv[KC][TIT][8];
-  float rgv[KC][TIT][GM ? 8 : 1];
-  // stage s = channel blocks KC s .. KC s + KC - 1 (Cs / 16 is a multiple of KC: the launcher checks)
+  float rv[TIT][8];
+  float rgv[TIT][GM ? 8 : 1];
+  // stage s = channel block s
   auto load_into = [&](int st, auto& R, auto& G) {
+    const int cb_off = __builtin_amdgcn_readfirstlane(st * 16 * plane * 4);
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const int cb_off = __builtin_amdgcn_readfirstlane((st * KC + kc) * 16 * plane * 4);
+    for (int it = 0; it < TIT; ++it)
 #pragma unroll
-      for (int it = 0; it < TIT; ++it)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          R[kc][it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
-          if constexpr (GM)
-            G[kc][it][i] =
-                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
-        }
-    }
+      for (int i = 0; i < 8; ++i) {
+        R[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
+        if constexpr (GM)
+          G[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
+      }
   };
   auto store_from = [&](int buf, auto& R, auto& G) {
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
     for (int it = 0; it < TIT; ++it) {
       if (NTASK % NTT != 0 && t_lds[it] < 0) continue;
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = GM ? (G[kc][it][i] > 0.f ? R[kc][it][i] : 0.f) : R[kc][it][i];
-      uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][kc][0][0]) + t_lds[it];
+      for (int i = 0; i < 8; ++i) v[i] = GM ? (G[it][i] > 0.f ? R[it][i] : 0.f) : R[it][i];
+      uint32_t* d = reinterpret_cast<uint32_t*>(&Ps[buf][0][0]) + t_lds[it];
       if constexpr (PREC == 3) {
         uint32_t h[4], md[4], l[4];
 #pragma unroll
@@ -215,31 +201,27 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  const int nst_all = P.Cs / (16 * KC);
+  const int nst_all = P.Cs / 16;
   const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
   const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
   // the taps of every channel block of stage st, B fragments from patch buffer buf
-  auto taps = [&](int st, int buf) {
+  auto taps = [&](int cb, int buf) {
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const int cb = st * KC + kc;
+    for (int t = 0; t < NTAP; ++t) {
+      const int kh = t / KS, kw = t % KS;
+      const int ph = tr ? KS - 1 - kh : kh, pw = tr ? KS - 1 - kw : kw;  // (tr is block-uniform)
+      const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : NTAP * (cb + 1);
+      if (t < NTAP - 1 || cb + 1 < nst) load_a(kt_next, arN);
+      // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
+      // columns lo + pw
+      const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
+      halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
 #pragma unroll
-      for (int t = 0; t < NTAP; ++t) {
-        const int kh = t / KS, kw = t % KS;
-        const int ph = tr ? KS - 1 - kh : kh, pw = tr ? KS - 1 - kw : kw;  // (tr is block-uniform)
-        const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : NTAP * (cb + 1);
-        if (t < NTAP - 1 || cb + 1 < nst * KC) load_a(kt_next, arN);
-        // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
-        // columns lo + pw
-        const float(*Bt)[LS] = &Ps[buf][kc][(4 * wn + ph) * HPW + pw];
-        halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
-#pragma unroll
-        for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
-      }
+      for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
     }
   };
   load_into(st0, rv, rgv);
-  load_a(NTAP * KC * st0, arC);
+  load_a(NTAP * st0, arC);
   store_from(0, rv, rgv);
   if constexpr (PD == 1) {
     __syncthreads();
@@ -257,8 +239,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
     // two patches in flight: stage st + 2's loads are issued before stage st's taps, into the
     // register set stage st + 1 is not stored from (the two sets alternate, loop unrolled by two)
     static_assert(PD == 2 && DB, "depth-2 patch prefetch: double-buffered tiles");
-    float rvN[KC][TIT][8];
-    float rgvN[KC][TIT][GM ? 8 : 1];
+    float rvN[TIT][8];
+    float rgvN[TIT][GM ? 8 : 1];
     if (st0 + 1 < nst) load_into(st0 + 1, rv, rgv);
     __syncthreads();
     auto stage = [&](int st, auto& Rs, auto& Gs, auto& Rl, auto& Gl) {
@@ -310,18 +292,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 //   2x4 one-buffer everywhere: 128-row layers 839 us, 256-row 695-770; 4x2 one-buffer: 932-1172 --
 //   both slower than 4x1 / 8x1 (profiles/r04_halo_shapes.txt)
 //   M = 256-multiples (VGG conv3_x / conv4_x): 8x1, 268-274 TF/s vs per-tap 233-245
-#ifndef VST_HALO_M64
-#define VST_HALO_M64 3  // block shape of 64-row layers (HaloCfg below)
-#endif
-#ifndef VST_HALO_M128
-#define VST_HALO_M128 4
-#endif
-#ifndef VST_HALO_M192
-#define VST_HALO_M192 3
-#endif
-#ifndef VST_HALO_M256
-#define VST_HALO_M256 8  // 256-row multiples
-#endif
+// block shape of 64-, 128-, 192-row and 256-multiple layers (HaloCfg below)
+constexpr int HALO_M64 = 3, HALO_M128 = 4, HALO_M192 = 3, HALO_M256 = 8;
 // WM x WN waves (S: one patch buffer)
 enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S, H4x2S };
 constexpr int halo_wm_c(int c) { return c == H2x1 || c == H2x2 || c == H2x2S || c == H2x4S ? 2
@@ -330,75 +302,55 @@ constexpr int halo_wn_c(int c) { return c == H2x4S ? 4 : (c == H2x2 || c == H2x2
 constexpr bool halo_db_c(int c) { return !(c == H2x2S || c == H2x4S || c == H3x1S || c == H3x2S || c == H4x2S); }
 inline int halo_wm(int c) { return halo_wm_c(c); }
 inline int halo_wn(int c) { return halo_wn_c(c); }
-// 0: the per-tap kernel (the M tile would not divide the pack's Mpad; or, with VST_HALO_X6_PADOUT 0,
-// the bf16x6 residual data gradient over the padded grid, whose 66 x 130 grid wastes a fifth of a
-// 32-column tile grid -- slower than per-tap on the 2x4 block, faster on the 2x2 one)
-#ifndef VST_HALO_X6_PADOUT
-#define VST_HALO_X6_PADOUT 1  // the bf16x6 residual padded-grid dgrad on the halo kernel (measured above)
-#endif
-inline int halo_cfg(int M, int pack_mpad, bool bf16x6, bool padout) {
+// 0: the per-tap kernel (the M tile would not divide the pack's Mpad).  (The bf16x6 residual data
+// gradient over the padded grid -- 66 x 130, a fifth of a 32-column tile grid wasted -- is slower than
+// per-tap on the 2x4 block and faster on the 2x2 one, measured above: it runs here.)
+inline int halo_cfg(int M, int pack_mpad) {
   int c;
-  if (M <= 64) c = VST_HALO_M64;
-  else if (M % 256 == 0) c = VST_HALO_M256;
-  else if (M % 192 == 0 && M % 128 != 0) {
-    if (bf16x6 && padout && !VST_HALO_X6_PADOUT) return 0;
-    c = VST_HALO_M192;
-  } else c = VST_HALO_M128;
+  if (M <= 64) c = HALO_M64;
+  else if (M % 256 == 0) c = HALO_M256;
+  else if (M % 192 == 0 && M % 128 != 0) c = HALO_M192;
+  else c = HALO_M128;
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
 }
 
-#ifndef VST_HALO_KC
-#define VST_HALO_KC 1  // channel blocks per stage for the single-product modes (measured above)
-#endif
-#ifndef VST_HALO_SMINW_SP
-#define VST_HALO_SMINW_SP 4  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
-#endif
-#ifndef VST_HALO_PD
-#define VST_HALO_PD 2  // patches in flight for the single-product double-buffered tiles
-#endif
+constexpr int HALO_SMINW_SP = 4;  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
+constexpr int HALO_PD = 2;        // patches in flight for the single-product double-buffered tiles
 template <int C, int PR, bool GM, int KS = 3>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
-  // (the one-buffer tiles already sit at their 128-VGPR budget with one block's staging registers)
-  constexpr int KC = (PR == 3 || !halo_db_c(C)) ? 1 : VST_HALO_KC;
   // waves per SIMD the registers must allow: one-buffer tiles 4 for the single-product modes (their
   // LDS admits 16 waves per CU) but 3 for bf16x6, whose three-piece fragments spill at the 128-VGPR
   // budget (measured: the spilling 2x2 tile 1088 us vs 758 us at 3 waves per SIMD on the 64-row VGG
   // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
   // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
-  constexpr int MINW = !halo_db_c(C) ? (PR == 3 || PR == 1 ? 3 : VST_HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
-  if constexpr (KC > 1) {
-    if ((P.Cs / 16) % KC != 0) {  // (a channel count that does not fill whole stages)
-      conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), 1, 1, KS><<<grid, WM * WN * 64, 0, st>>>(P);
-      return;
-    }
-  }
+  constexpr int MINW = !halo_db_c(C) ? (PR == 3 || PR == 1 ? 3 : HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
   // depth-2 patch prefetch for the 8-wave single-product tiles (config 5: the fp16 tiles wait on the
   // next patch's gather; fp16 shapes, one box: AdaAttN decoder 256-row 69 -> 53 us, VGG conv4 150 ->
   // 144, conv5 123 -> 89; config 5 145.07 -> 141.5 ms, profiles/r04_halo_pd.txt).  Not on the 4-wave
   // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
   // bf16x6 (MFMA-bound, registers spoken for)
-  constexpr int PD = (PR != 3 && halo_db_c(C) && KC == 1 && WM * WN >= 8) ? VST_HALO_PD : 1;
-  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), KC, PD, KS><<<grid, WM * WN * 64, 0, st>>>(P);
+  constexpr int PD = (PR != 3 && halo_db_c(C) && WM * WN >= 8) ? HALO_PD : 1;
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), PD, KS><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 // only the block shapes the build's selection can reach are instantiated
 template <int PR, bool GM>
 void launch_halo(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
-  if (c == VST_HALO_M64) launch_halo_c<VST_HALO_M64, PR, GM>(grid, st, P);
-  else if (c == VST_HALO_M128) launch_halo_c<VST_HALO_M128, PR, GM>(grid, st, P);
-  else if (c == VST_HALO_M192) launch_halo_c<VST_HALO_M192, PR, GM>(grid, st, P);
-  else launch_halo_c<VST_HALO_M256, PR, GM>(grid, st, P);
+  if (c == HALO_M64) launch_halo_c<HALO_M64, PR, GM>(grid, st, P);
+  else if (c == HALO_M128) launch_halo_c<HALO_M128, PR, GM>(grid, st, P);
+  else if (c == HALO_M192) launch_halo_c<HALO_M192, PR, GM>(grid, st, P);
+  else launch_halo_c<HALO_M256, PR, GM>(grid, st, P);
 }
 
 // the 2x2 phase-stacked GEMMs (no gather mask on their paths): M = 4 x channels, the 128- and 192-row
 // selections (ReCoNet deconv1 / conv3: 384 rows; deconv2 / conv2: 192)
 template <int PR>
 void launch_halo2(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
-  if (c == VST_HALO_M192) launch_halo_c<VST_HALO_M192, PR, false, 2>(grid, st, P);
-  else if (c == VST_HALO_M128) launch_halo_c<VST_HALO_M128, PR, false, 2>(grid, st, P);
-  else if (c == VST_HALO_M64) launch_halo_c<VST_HALO_M64, PR, false, 2>(grid, st, P);
-  else launch_halo_c<VST_HALO_M256, PR, false, 2>(grid, st, P);
+  if (c == HALO_M192) launch_halo_c<HALO_M192, PR, false, 2>(grid, st, P);
+  else if (c == HALO_M128) launch_halo_c<HALO_M128, PR, false, 2>(grid, st, P);
+  else if (c == HALO_M64) launch_halo_c<HALO_M64, PR, false, 2>(grid, st, P);
+  else launch_halo_c<HALO_M256, PR, false, 2>(grid, st, P);
 }
 
 template <int PR>

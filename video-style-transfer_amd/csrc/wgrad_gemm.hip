@@ -826,12 +826,10 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
 }
 
 // k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
-#ifndef VST_WKD_SP
-#define VST_WKD_SP 2
-#endif
+constexpr int WKD_SP = 2;
 template <int PR, int GMD>
 static void launch_wg2_p(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
-  launch_wg2_pk<PR, GMD, (PR == 2 || PR == 4) ? VST_WKD_SP : 1>(c, g, st, P);
+  launch_wg2_pk<PR, GMD, (PR == 2 || PR == 4) ? WKD_SP : 1>(c, g, st, P);
 }
 
 template <int GMD>

@@ -2,9 +2,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#ifndef VST_WGRAD_HALO
-#define VST_WGRAD_HALO 1
-#endif
 
 struct WhParams {
   const float* a;  // dY [N][M][H][W]

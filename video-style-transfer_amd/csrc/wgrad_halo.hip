@@ -29,9 +29,16 @@ namespace {
 constexpr int WH_BK = 16;  // pixels per k-tile (one output row of a 16-column strip)
 constexpr int WH_CB = 32;  // input channels per block (one MFMA column tile per tap)
 
+// waves per SIMD the registers must allow: 3 (two 6-wave blocks or one 12-wave block per CU).  The
+// single-product modes wait on their staging loads most of the time (config 5: 80 % of wave time), but
+// twice the resident blocks does not help: fp16 decoder shapes (tools/wgrad_bench.py, one box) at 3 /
+// 5 / 6 waves per SIMD: 512 ch 1.46 / 1.46 / 1.30 ms, 256 ch 1.43 / 1.43 / 1.65, 128 ch 1.69 / 1.68 /
+// 2.00, 64 ch 3.62 / 5.09 / 5.26 (twice the slabs to write and reduce, and the blocks' rows no longer
+// share one XCD's L2); config 5 139.0 -> 142.8 ms at 6.
+constexpr int WH_WAVES = 3;
+
 template <int WM, int PREC, int GMODE>
-// (3 waves per SIMD: two 6-wave blocks or one 12-wave block per CU)
-__global__ __launch_bounds__(WM * 3 * 64, 3) void wgrad_halo_kernel(WhParams P) {
+__global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhParams P) {
   static_assert(PREC == 2 || PREC == 3 || PREC == 4, "halo wgrad: bf16x6, bf16 or fp16 products");
   constexpr int NTH = WM * 3 * 64;
   constexpr int BM = WM * 32;
@@ -299,12 +306,12 @@ static int wgrad_halo_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 // data-gradient GEMMs worse on the side stream).
 bool wgrad_halo_ok(int M, int Cs, int H, int W, int KH, int KW, int stride, int pad, int up, int gmode, int mode) {
   const int am = vst_mode_arith(mode);
-  return VST_WGRAD_HALO && KH == 3 && KW == 3 && stride == 1 && pad == 1 && up == 1 && (gmode == 0 || gmode == 1) &&
+  return KH == 3 && KW == 3 && stride == 1 && pad == 1 && up == 1 && (gmode == 0 || gmode == 1) &&
          Cs % WH_CB == 0 && W % WH_BK == 0 && H >= 2 && W >= 2 &&
          (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
 }
 
-// Split plan: one resident round of blocks (two per CU; one for the 12-wave 128-row tiles), NB
+// Split plan: one resident round of blocks (two 6-wave blocks or one 12-wave block per CU), NB
 // blocks per (channel block, M tile) pair, each summing a contiguous share of the pair's
 // (image, strip, row chunk) segments into its own slab -- NB slabs of Mpad x 9 Cs whatever the batch
 // and image size.  Row chunks halve (down to 16 rows; each costs a two-row ring prologue) until
@@ -315,7 +322,7 @@ WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W) {
   p.Mpad = (M + bm - 1) / bm * bm;
   const int nstrip = W / WH_BK;
   const int pairs = (Cs / WH_CB) * (p.Mpad / bm);
-  const int slots = 256 * (bm == 128 ? 1 : 2);
+  const int slots = 256 * (4 * WH_WAVES / (3 * (bm / 32)));
   p.NB = slots / pairs > 1 ? slots / pairs : 1;
   p.nchunk = 1;
   while ((long)N * nstrip * p.nchunk < 4L * p.NB && (H + 2 * p.nchunk - 1) / (2 * p.nchunk) >= 16) p.nchunk *= 2;

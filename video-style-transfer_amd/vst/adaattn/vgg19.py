@@ -39,12 +39,13 @@ class VGG19(nn.Module):
         out = {}
         for s, name in enumerate(FEATURES, 1):
             last = s == len(FEATURES)
-            if _SPLIT and not last and torch.is_grad_enabled() and x.requires_grad:
-                # slice boundary with a gradient: the feature's two consumers (losses, next slice)
-                # meet in FeatureSplitFn's fused backward, so the producing conv runs premasked
-                x = run_vgg_slice(getattr(self, f"slice{s}"), x, premasked_out=True)
-                out[name], x = ops.feature_split(x)
-            else:
-                x = run_vgg_slice(getattr(self, f"slice{s}"), x)
-                out[name] = x
+            with ops.gemm_scope(f"s{s}"):  # (policy keys may name a slice: "<scope>.s<k>.<role>")
+                if _SPLIT and not last and torch.is_grad_enabled() and x.requires_grad:
+                    # slice boundary with a gradient: the feature's two consumers (losses, next slice)
+                    # meet in FeatureSplitFn's fused backward, so the producing conv runs premasked
+                    x = run_vgg_slice(getattr(self, f"slice{s}"), x, premasked_out=True)
+                    out[name], x = ops.feature_split(x)
+                else:
+                    x = run_vgg_slice(getattr(self, f"slice{s}"), x)
+                    out[name] = x
         return out
