@@ -34,7 +34,10 @@ constexpr int WH_CB = 32;  // input channels per block (one MFMA column tile per
 // twice the resident blocks does not help: fp16 decoder shapes (tools/wgrad_bench.py, one box) at 3 /
 // 5 / 6 waves per SIMD: 512 ch 1.46 / 1.46 / 1.30 ms, 256 ch 1.43 / 1.43 / 1.65, 128 ch 1.69 / 1.68 /
 // 2.00, 64 ch 3.62 / 5.09 / 5.26 (twice the slabs to write and reduce, and the blocks' rows no longer
-// share one XCD's L2); config 5 139.0 -> 142.8 ms at 6.
+// share one XCD's L2); config 5 139.0 -> 142.8 ms at 6.  Nor does a barrier per two output rows
+// (6 MFMAs per wave per step instead of 3, an eight-slot source ring): 512 / 256 / 128 / 64 ch 1.46 /
+// 1.60 / 1.78 / 3.64 ms against 1.46 / 1.54 / 1.68 / 3.65 -- the 64-byte dY and source row pieces of a
+// 16-column strip, half a cache line each, are what the waves wait on.
 constexpr int WH_WAVES = 3;
 
 template <int WM, int PREC, int GMODE>
