@@ -268,6 +268,15 @@ int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W
  * (AA/network.py:59,80,85,90,94 decoder upsampling backward) */
 int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
                             void* stream);
+/* the same pair with explicit coordinate scales (input pixels per output pixel, > 0): output pixel d
+ * reads source (d + 0.5) * scale - 0.5.  vst_resize_bilinear uses H / Ho and W / Wo; F.interpolate
+ * with scale_factor=s (AA/network.py:49-60 ConvReluInterpolate, any s) uses 1 / s with
+ * Ho = floor(H s), which differs from H / Ho when H s is not a whole number */
+int vst_resize_bilinear_scaled(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo, float scale_y,
+                               float scale_x, const float* chscale, int binarize, long out_bs, const float* addend,
+                               void* stream);
+int vst_resize_bilinear_scaled_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo,
+                                   float scale_y, float scale_x, long gout_bs, void* stream);
 /* adjoint of the x2 upsample (Ho = 2H, Wo = 2W) of the decoder (AA/network.py:59,80,85,90,94), with
  * the fixed 4-tap weights per axis; ymask (optional, the upsample's input = a ReLU output): gx = 0
  * where ymask <= 0, i.e. the producer ConvReLU's ReLU backward fused in (AA/network.py:28-33).  W odd or

@@ -54,9 +54,14 @@ def test_conv_relu_interpolate_scales(scale):
                                             align_corners=False), x, 1e-4)
 
 
-def test_conv_relu_interpolate_rejects_inexact_sizes():
+@pytest.mark.parametrize("scale", [1.5, 0.7, 3.3, 0.25])
+def test_conv_relu_interpolate_inexact_sizes(scale):
+    """Scale factors whose output is not H*s x W*s exactly (7 x 9 maps): output floor(H s) x floor(W s),
+    source coordinate (d + 0.5) / s - 0.5 -- F.interpolate's own mapping, forward and backward."""
     from vst.adaattn.network import ConvReluInterpolate
 
-    m = ConvReluInterpolate(16, 16, 3, 1, 1.5).to(DEV)
-    with pytest.raises(NotImplementedError):
-        m(torch.randn(1, 16, 7, 9, device=DEV))
+    torch.manual_seed(2)
+    m = ConvReluInterpolate(16, 16, 3, 1, scale).to(DEV)
+    x = torch.randn(2, 16, 7, 9)
+    _check(m, lambda x, w, b: F.interpolate(F.relu(_ref_conv(x, w, b)), scale_factor=scale, mode="bilinear",
+                                            align_corners=False), x, 1e-4)

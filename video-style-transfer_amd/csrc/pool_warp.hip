@@ -529,8 +529,10 @@ __global__ void flow_mask_kernel(const float* __restrict__ flo01, const float* _
   mask[idx] = err < thr ? 1.f : 0.f;
 }
 
-__device__ __forceinline__ void resize_axis(int d, int n_in, int n_out, int& i0, int& i1, float& l1) {
-  float scale = (float)n_in / (float)n_out;
+// scale: input pixels per output pixel along the axis -- n_in / n_out for a size-given resize, 1 / s for
+// F.interpolate(scale_factor=s) (ATen's area_pixel_compute_scale; the two differ when n_in * s is not
+// a whole number)
+__device__ __forceinline__ void resize_axis(int d, int n_in, float scale, int& i0, int& i1, float& l1) {
   float src = ((float)d + 0.5f) * scale - 0.5f;
   src = src < 0.f ? 0.f : src;
   i0 = (int)src;
@@ -542,7 +544,8 @@ __device__ __forceinline__ void resize_axis(int d, int n_in, int n_out, int& i0,
 // out[n][c] = resize(x[nc]) * chscale[c] (+ addend[n][c]); binarize: out = out > 0
 // out/addend images are out_bs floats apart (channel-concat targets, AA/utilities.py:98-109)
 __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ out, long NC, int C, int H, int W, int Ho,
-                              int Wo, const float* chscale, int binarize, long out_bs, const float* __restrict__ addend) {
+                              int Wo, float sy, float sx, const float* chscale, int binarize, long out_bs,
+                              const float* __restrict__ addend) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NC * Ho * Wo) return;
   int ox = (int)(idx % Wo);
@@ -551,8 +554,8 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
   long nc = t / Ho;
   int y0, y1, x0, x1;
   float ly, lx;
-  resize_axis(oy, H, Ho, y0, y1, ly);
-  resize_axis(ox, W, Wo, x0, x1, lx);
+  resize_axis(oy, H, sy, y0, y1, ly);
+  resize_axis(ox, W, sx, x0, x1, lx);
   const float* p = x + nc * H * W;
   float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
             ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
@@ -567,15 +570,16 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
 // per-element 64-bit (plane, row, column) division of the flat form made it VALU-bound (config 5:
 // 22 launches, 268 us each); same arithmetic per output element
 __global__ __launch_bounds__(256) void resize_plane_kernel(const float* __restrict__ x, float* __restrict__ out, int C,
-                                                           int H, int W, int Ho, int Wo, const float* chscale,
-                                                           int binarize, long out_bs, const float* __restrict__ addend) {
+                                                           int H, int W, int Ho, int Wo, float sy, float sx,
+                                                           const float* chscale, int binarize, long out_bs,
+                                                           const float* __restrict__ addend) {
   const int ox = blockIdx.x * 64 + threadIdx.x, oy = blockIdx.y * 4 + threadIdx.y;
   if (ox >= Wo || oy >= Ho) return;
   const int nc = blockIdx.z, n = nc / C, c = nc - n * C;
   int y0, y1, x0, x1;
   float ly, lx;
-  resize_axis(oy, H, Ho, y0, y1, ly);
-  resize_axis(ox, W, Wo, x0, x1, lx);
+  resize_axis(oy, H, sy, y0, y1, ly);
+  resize_axis(ox, W, sx, x0, x1, lx);
   const float* p = x + (long)nc * H * W;
   float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
             ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
@@ -587,16 +591,16 @@ __global__ __launch_bounds__(256) void resize_plane_kernel(const float* __restri
 }
 
 // weight with which input index i enters output index d along one axis (0 if it does not)
-__device__ __forceinline__ float resize_weight(int d, int i, int n_in, int n_out) {
+__device__ __forceinline__ float resize_weight(int d, int i, int n_in, float scale) {
   int i0, i1;
   float l1;
-  resize_axis(d, n_in, n_out, i0, i1, l1);
+  resize_axis(d, n_in, scale, i0, i1, l1);
   return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
 }
 
 // output index range [lo, hi] that can read input index i (src(d) in [i-1, i+1], with slack)
-__device__ __forceinline__ void resize_span(int i, int n_in, int n_out, int& lo, int& hi) {
-  const float inv = (float)n_out / (float)n_in;
+__device__ __forceinline__ void resize_span(int i, int n_out, float scale, int& lo, int& hi) {
+  const float inv = 1.f / scale;
   lo = (int)floorf(((float)i - 0.5f) * inv - 0.5f) - 1;
   hi = (int)ceilf(((float)i + 1.5f) * inv - 0.5f) + 1;
   lo = lo < 0 ? 0 : lo;
@@ -606,7 +610,7 @@ __device__ __forceinline__ void resize_span(int i, int n_in, int n_out, int& lo,
 // adjoint of the bilinear resize as a gather: each input element sums the output gradients that
 // read it, with the forward's own weights (deterministic, no atomics, every gx written once)
 __global__ void resize_bwd_kernel(const float* __restrict__ gout, float* __restrict__ gx, long NC, int C, int H, int W,
-                                  int Ho, int Wo, long gout_bs) {
+                                  int Ho, int Wo, float sy, float sx, long gout_bs) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NC * H * W) return;
   int ix = (int)(idx % W);
@@ -614,16 +618,16 @@ __global__ void resize_bwd_kernel(const float* __restrict__ gout, float* __restr
   int iy = (int)(t % H);
   long nc = t / H;
   int ylo, yhi, xlo, xhi;
-  resize_span(iy, H, Ho, ylo, yhi);
-  resize_span(ix, W, Wo, xlo, xhi);
+  resize_span(iy, Ho, sy, ylo, yhi);
+  resize_span(ix, Wo, sx, xlo, xhi);
   const float* g = gout + (nc / C) * gout_bs + (nc % C) * (long)Ho * Wo;
   float acc = 0.f;
   for (int oy = ylo; oy <= yhi; ++oy) {
-    const float wy = resize_weight(oy, iy, H, Ho);
+    const float wy = resize_weight(oy, iy, H, sy);
     if (wy == 0.f) continue;
     float row = 0.f;
     for (int ox = xlo; ox <= xhi; ++ox) {
-      const float wx = resize_weight(ox, ix, W, Wo);
+      const float wx = resize_weight(ox, ix, W, sx);
       if (wx != 0.f) row += wx * g[(long)oy * Wo + ox];
     }
     acc += wy * row;
@@ -696,7 +700,8 @@ int vst_upsample2x_bwd(const float* gout, const float* ymask, float* gx, long NC
   const bool vec = (W % 2 == 0) && (gout_bs % 4 == 0) && (((uintptr_t)gout | (uintptr_t)gx | (uintptr_t)ymask) % 16 == 0);
   if (!vec) {
     if (ymask) return VST_EUNSUPPORTED;  // the generic gather has no mask epilogue
-    resize_bwd_kernel<<<ceil_div(NC * H * W, 256), 256, 0, st>>>(gout, gx, NC, C, H, W, (int)Ho, (int)Wo, gout_bs);
+    resize_bwd_kernel<<<ceil_div(NC * H * W, 256), 256, 0, st>>>(gout, gx, NC, C, H, W, (int)Ho, (int)Wo, 0.5f, 0.5f,
+                                                                  gout_bs);
     return vst_launch_status();
   }
   const long total = NC * H * (W / 2);
@@ -801,29 +806,47 @@ int vst_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int 
   return vst_launch_status();
 }
 
-int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
-                        const float* chscale, int binarize, long out_bs, const float* addend, void* stream) {
+int vst_resize_bilinear_scaled(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo, float scale_y,
+                               float scale_x, const float* chscale, int binarize, long out_bs, const float* addend,
+                               void* stream) {
   VST_CHECK_ARG(x && out && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
+  VST_CHECK_ARG(scale_y > 0.f && scale_x > 0.f);
   long total = NC * Ho * Wo;
   if (out_bs <= 0) out_bs = (long)C * Ho * Wo;
   if (NC <= 65535 && Ho <= 4 * 65535) {
     const dim3 g((unsigned)ceil_div(Wo, 64), (unsigned)ceil_div(Ho, 4), (unsigned)NC);
-    resize_plane_kernel<<<g, dim3(64, 4), 0, (hipStream_t)stream>>>(x, out, C, H, W, Ho, Wo, chscale, binarize,
-                                                                    out_bs, addend);
+    resize_plane_kernel<<<g, dim3(64, 4), 0, (hipStream_t)stream>>>(x, out, C, H, W, Ho, Wo, scale_y, scale_x, chscale,
+                                                                    binarize, out_bs, addend);
     return vst_launch_status();
   }
-  resize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, NC, C, H, W, Ho, Wo, chscale,
-                                                                       binarize, out_bs, addend);
+  resize_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(x, out, NC, C, H, W, Ho, Wo, scale_y, scale_x,
+                                                                       chscale, binarize, out_bs, addend);
+  return vst_launch_status();
+}
+
+int vst_resize_bilinear(const float* x, float* out, long NC, int C, int H, int W, int Ho, int Wo,
+                        const float* chscale, int binarize, long out_bs, const float* addend, void* stream) {
+  VST_CHECK_ARG(Ho > 0 && Wo > 0);
+  return vst_resize_bilinear_scaled(x, out, NC, C, H, W, Ho, Wo, (float)H / (float)Ho, (float)W / (float)Wo, chscale,
+                                    binarize, out_bs, addend, stream);
+}
+
+int vst_resize_bilinear_scaled_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo,
+                                   float scale_y, float scale_x, long gout_bs, void* stream) {
+  VST_CHECK_ARG(gout && gx && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
+  VST_CHECK_ARG(scale_y > 0.f && scale_x > 0.f);
+  long total = NC * H * W;
+  if (gout_bs <= 0) gout_bs = (long)C * Ho * Wo;
+  resize_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, gx, NC, C, H, W, Ho, Wo, scale_y,
+                                                                           scale_x, gout_bs);
   return vst_launch_status();
 }
 
 int vst_resize_bilinear_bwd(const float* gout, float* gx, long NC, int C, int H, int W, int Ho, int Wo, long gout_bs,
                             void* stream) {
-  VST_CHECK_ARG(gout && gx && NC > 0 && C > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && NC % C == 0);
-  long total = NC * H * W;
-  if (gout_bs <= 0) gout_bs = (long)C * Ho * Wo;
-  resize_bwd_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(gout, gx, NC, C, H, W, Ho, Wo, gout_bs);
-  return vst_launch_status();
+  VST_CHECK_ARG(Ho > 0 && Wo > 0);
+  return vst_resize_bilinear_scaled_bwd(gout, gx, NC, C, H, W, Ho, Wo, (float)H / (float)Ho, (float)W / (float)Wo,
+                                        gout_bs, stream);
 }
 
 }  // extern "C"

@@ -78,15 +78,9 @@ class ConvReluInterpolate(nn.Module):
         y = self.conv.run(x, act="relu")
         if self.scale_factor == 2:
             return ops.upsample2x(y)
-        # F.interpolate(scale_factor=s, bilinear, align_corners=False) maps output pixel i to source
-        # (i + 0.5) / s - 0.5 with the output floor(H s) pixels tall; the size-based resize kernel maps
-        # with H / Ho, the same thing whenever H s is a whole number
-        H, W = y.shape[2:]
-        s = float(self.scale_factor)
-        Ho, Wo = int(np.floor(H * s)), int(np.floor(W * s))
-        if Ho != H * s or Wo != W * s or Ho < 1 or Wo < 1:
-            raise NotImplementedError(f"scale_factor {s} on a {H}x{W} map: the output size is not H*s x W*s exactly")
-        return ops.resize(y, (Ho, Wo))
+        # F.interpolate(scale_factor=s, bilinear, align_corners=False): output floor(H s) x floor(W s),
+        # output pixel i reads source (i + 0.5) / s - 0.5 -- any s, whole-number output or not
+        return ops.interpolate_scale(y, self.scale_factor)
 
 
 class Decoder(nn.Module):

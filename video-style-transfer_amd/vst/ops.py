@@ -8,6 +8,7 @@ import os
 import threading
 import weakref
 
+import numpy as np
 import torch
 from torch.autograd import Function
 
@@ -1213,9 +1214,10 @@ def tv_loss(s, weight):
 
 
 # ------------------------------------------------------------------ resize / concat
-def resize_bilinear(x, size, chscale=None, binarize=False, out=None, addend=None):
+def resize_bilinear(x, size, chscale=None, binarize=False, out=None, addend=None, scale=None):
     """F.interpolate(x, size, mode='bilinear', align_corners=False) [* chscale[c]] [> 0] [+ addend].
-    `out` may be a per-sample-contiguous slice of a larger buffer (channel concat)."""
+    `out` may be a per-sample-contiguous slice of a larger buffer (channel concat).  `scale` = (sy, sx):
+    explicit coordinate scales (input pixels per output pixel; F.interpolate(scale_factor=s) uses 1/s)."""
     x = _check(x, "resize input", 4)
     N, C, H, W = x.shape
     Ho, Wo = size
@@ -1228,8 +1230,13 @@ def resize_bilinear(x, size, chscale=None, binarize=False, out=None, addend=None
         addend = _check(addend, "resize addend", 4)
         if tuple(addend.shape) != (N, C, Ho, Wo) or obs != C * Ho * Wo:
             raise VstError("resize: addend must match a dense output")
-    lib.vst_resize_bilinear(ptr(x), optr, N * C, C, H, W, Ho, Wo, ptr(chscale), int(binarize),
-                            obs if obs != C * Ho * Wo else 0, ptr(addend), stream())
+    if scale is None:
+        lib.vst_resize_bilinear(ptr(x), optr, N * C, C, H, W, Ho, Wo, ptr(chscale), int(binarize),
+                                obs if obs != C * Ho * Wo else 0, ptr(addend), stream())
+    else:
+        lib.vst_resize_bilinear_scaled(ptr(x), optr, N * C, C, H, W, Ho, Wo, float(scale[0]), float(scale[1]),
+                                       ptr(chscale), int(binarize), obs if obs != C * Ho * Wo else 0, ptr(addend),
+                                       stream())
     return out
 
 
@@ -1237,27 +1244,46 @@ class ResizeFn(Function):
     """F.interpolate(x, size, mode='bilinear', align_corners=False) with its adjoint (gather form)."""
 
     @staticmethod
-    def forward(ctx, x, size):
+    def forward(ctx, x, size, scale=None):
         ctx.x_shape = x.shape
-        return resize_bilinear(x.contiguous(), size)
+        ctx.scale = scale
+        return resize_bilinear(x.contiguous(), size, scale=scale)
 
     @staticmethod
     def backward(ctx, g):
-        return resize_bilinear_bwd(g.contiguous(), ctx.x_shape), None
+        return resize_bilinear_bwd(g.contiguous(), ctx.x_shape, ctx.scale), None, None
 
 
-def resize(x, size):
-    """Differentiable bilinear resize (align_corners=False) to `size` = (Ho, Wo)."""
-    return ResizeFn.apply(x, tuple(int(v) for v in size))
+def resize(x, size, scale=None):
+    """Differentiable bilinear resize (align_corners=False) to `size` = (Ho, Wo); `scale` = (sy, sx)
+    coordinate scales when they are not H / Ho, W / Wo (see resize_bilinear)."""
+    return ResizeFn.apply(x, tuple(int(v) for v in size), scale)
 
 
-def resize_bilinear_bwd(gout, x_shape):
+def interpolate_scale(x, s):
+    """F.interpolate(x, scale_factor=s, mode='bilinear', align_corners=False) for any s > 0
+    (AA/network.py:57-59): output floor(H s) x floor(W s), source coordinate (d + 0.5) / s - 0.5 with
+    1 / s rounded to fp32 as ATen's area_pixel_compute_scale does."""
+    N, C, H, W = x.shape
+    s = float(s)
+    Ho, Wo = int(np.floor(H * s)), int(np.floor(W * s))
+    if Ho < 1 or Wo < 1:
+        raise VstError(f"interpolate: scale_factor {s} on a {H}x{W} map gives an empty output")
+    inv = float(np.float32(1.0 / s))
+    return resize(x, (Ho, Wo), scale=(inv, inv))
+
+
+def resize_bilinear_bwd(gout, x_shape, scale=None):
     """Adjoint of resize_bilinear w.r.t. x; gout may be a per-sample-contiguous slice."""
     N, C, H, W = x_shape
     Ho, Wo = gout.shape[2:]
     gptr, gbs = ptr_rows(gout)
     gx = _empty(x_shape, gout)
-    lib.vst_resize_bilinear_bwd(gptr, ptr(gx), N * C, C, H, W, Ho, Wo, gbs if gbs != C * Ho * Wo else 0, stream())
+    if scale is None:
+        lib.vst_resize_bilinear_bwd(gptr, ptr(gx), N * C, C, H, W, Ho, Wo, gbs if gbs != C * Ho * Wo else 0, stream())
+    else:
+        lib.vst_resize_bilinear_scaled_bwd(gptr, ptr(gx), N * C, C, H, W, Ho, Wo, float(scale[0]), float(scale[1]),
+                                           gbs if gbs != C * Ho * Wo else 0, stream())
     return gx
 
 
