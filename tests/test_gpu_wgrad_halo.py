@@ -38,8 +38,11 @@ def _ref(dy, x, gmode):
 
 
 # (N, Cin, H, W, Cout): residual 192 (ragged rows, several strips), decoder widths, tall (row chunks)
+# (the single-product modes walk 32-column strips on 64-row tiles and 64-column strips on 128-row ones:
+# other widths fall back to the row-tiled kernel)
 SHAPES = [(2, 192, 20, 48, 192), (2, 192, 20, 48, 64), (1, 64, 9, 32, 64), (2, 128, 16, 64, 128), (1, 256, 8, 16, 256),
-          (1, 32, 70, 16, 64), (3, 96, 13, 32, 192)]
+          (1, 32, 70, 16, 64), (3, 96, 13, 32, 192), (2, 64, 11, 96, 64), (1, 128, 7, 128, 64), (1, 64, 6, 192, 256),
+          (2, 32, 5, 128, 128)]
 
 
 @pytest.mark.parametrize("mode", [BF16X6, F16, BF16])

@@ -1076,7 +1076,7 @@ long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, 
                               int stride, int pad, int up, int mode) {
   if (N <= 0 || Cin <= 0 || Cout <= 0 || Ho <= 0 || Wo <= 0 || KH <= 0 || KW <= 0 || !vst_mode_ok(mode)) return 0;
   if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
-    return wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws));
+    return wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws, mode));
   return vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
 }
 
@@ -1087,7 +1087,7 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
   if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode)) {
-    const WhPlan p = wgrad_halo_plan(N, Cout, Cin, Hs, Ws);
+    const WhPlan p = wgrad_halo_plan(N, Cout, Cin, Hs, Ws, mode);
     hipStream_t st = (hipStream_t)stream;
     int rc = wgrad_halo_launch(p, dy, x, workspace, N, Cout, Cin, Hs, Ws, gmode, mode, st);
     if (rc) return rc;

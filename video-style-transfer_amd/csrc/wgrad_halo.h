@@ -16,7 +16,7 @@ struct WhPlan {
 };
 
 bool wgrad_halo_ok(int M, int Cs, int H, int W, int KH, int KW, int stride, int pad, int up, int gmode, int mode);
-WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W);
+WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W, int mode);
 long wgrad_halo_slab_floats(int N, int Cs, const WhPlan& p);
 int wgrad_halo_launch(const WhPlan& p, const float* dy, const float* x, float* slab, int N, int M, int Cs, int H,
                       int W, int gmode, int mode, hipStream_t st);

@@ -9,10 +9,12 @@
 // The row-tiled kernel (wgrad2_kernel) owns one tap per GEMM column: for every 16-pixel k-tile each
 // of the nine taps gathers its own shifted copy of the source window and splits it into bf16 pieces,
 // so every input element is loaded and split nine times per output row that reads it.  Here a block
-// owns ALL nine taps of a 32-channel block (288 GEMM columns) and walks a 16-column strip of the
-// output DOWN its rows, one k-tile (16 pixels of one output row y) per step:
+// owns ALL nine taps of a 32-channel block (288 GEMM columns) and walks a strip of the output DOWN its
+// rows, one strip row (KT k-tiles of 16 pixels: 16 columns under bf16x6, 32 / 64 under the single
+// products, wh_kt) per step:
 //   * the source rows y - 1, y, y + 1 sit in a four-slot LDS ring, so each step loads and splits ONE
-//     new source row (18 columns) per channel -- the other two were staged by the previous steps;
+//     new source row (strip width + 2 columns) per channel -- the other two were staged by the previous
+//     steps;
 //   * each staged row is written as three copies shifted by kw = 0, 1, 2 columns, so every tap's B
 //     fragment is an aligned 16-byte LDS read (the odd shift re-pairs the split bf16 dwords with
 //     v_alignbit, no second split);
@@ -34,11 +36,20 @@ constexpr int WH_CB = 32;  // input channels per block (one MFMA column tile per
 // twice the resident blocks does not help: fp16 decoder shapes (tools/wgrad_bench.py, one box) at 3 /
 // 5 / 6 waves per SIMD: 512 ch 1.46 / 1.46 / 1.30 ms, 256 ch 1.43 / 1.43 / 1.65, 128 ch 1.69 / 1.68 /
 // 2.00, 64 ch 3.62 / 5.09 / 5.26 (twice the slabs to write and reduce, and the blocks' rows no longer
-// share one XCD's L2); config 5 139.0 -> 142.8 ms at 6.  Nor does a barrier per two output rows
-// (6 MFMAs per wave per step instead of 3, an eight-slot source ring): 512 / 256 / 128 / 64 ch 1.46 /
-// 1.60 / 1.78 / 3.64 ms against 1.46 / 1.54 / 1.68 / 3.65 -- the 64-byte dY and source row pieces of a
-// 16-column strip, half a cache line each, are what the waves wait on.
+// share one XCD's L2); config 5 139.0 -> 142.8 ms at 6.  Nor does a barrier per two output rows of a
+// 16-column strip (6 MFMAs per wave per step instead of 3, an eight-slot source ring): 512 / 256 / 128
+// / 64 ch 1.46 / 1.60 / 1.78 / 3.64 ms against 1.46 / 1.54 / 1.68 / 3.65 -- the 64-byte dY and source
+// row pieces of a 16-column strip, half a cache line each, are what the waves wait on: wider strips
+// for the single products (wh_kt below) are what helps.
 constexpr int WH_WAVES = 3;
+
+// k-tiles (16-pixel column groups) per strip row: bf16x6 one; the single-product modes two on the 6-wave
+// 64-row blocks and four on the 12-wave 128-row ones -- a 32-column strip row is a whole 128-byte line
+// of dY and of x, and 3 KT MFMAs per wave per barrier instead of 3.  fp16 decoder shapes
+// (tools/wgrad_bench.py, one box; 16 / 32 / 64 columns): 512 ch 1.46 / 1.50 / 1.41 ms, 256 ch 1.53 /
+// 1.46 / 1.37, 128 ch 1.67 / 1.55 / 1.45, 64 ch (64 rows) 3.65 / 2.68 / 2.76, 128 -> 64 ch (64 rows)
+// 1.11 / 0.81 / 1.16 (the 64-column strips' LDS leaves one 6-wave block per CU)
+constexpr int wh_kt(int prec, int wm) { return prec == 3 ? 1 : (wm == 4 ? 4 : 2); }
 
 template <int WM, int PREC, int GMODE>
 __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhParams P) {
@@ -47,13 +58,15 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
   constexpr int BM = WM * 32;
   constexpr int NPC = PREC == 3 ? 3 : 1;   // bf16 pieces per value
   constexpr int LS = NPC * 8 + 4;          // LDS dwords per (row | channel) of a k-tile (+4: conflict-free)
-  constexpr int A_TASKS = 4 * BM;          // (row, 4-pixel quarter): waves 0 .. 2 WM - 1
+  constexpr int KT = wh_kt(PREC, WM);     // k-tiles per strip row (strip = 16 KT columns)
+  constexpr int A_TASKS = 4 * BM;          // (row, 4-pixel quarter) per k-tile: waves 0 .. 2 WM - 1
   constexpr int B_WAVE = A_TASKS / 64;     // the 128 (channel, 4-pixel quarter) B tasks: the next two waves
+  constexpr int NRV = KT * 6 > 10 ? KT * 6 : 10;  // staged floats per thread (A 4 per k-tile, B 6)
   constexpr int OOR = 0x7ffffff0;
   static_assert(B_WAVE + 2 <= WM * 3, "staging waves");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BM][LS];
-  __shared__ __attribute__((aligned(16))) float Bs[4][3][WH_CB][LS];  // [ring slot][kw copy][channel]
+  __shared__ __attribute__((aligned(16))) float As[2][KT][BM][LS];
+  __shared__ __attribute__((aligned(16))) float Bs[4][3][KT][WH_CB][LS];  // [ring slot][kw copy][k-tile][channel]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -91,7 +104,7 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-  float rv0[10], rv1[10];  // staged values of one tile (A uses 4, B 6); bf16x6 keeps two tiles in flight
+  float rv0[NRV], rv1[NRV];  // staged values of one step; bf16x6 keeps two steps in flight
 
   // source row / column maps (reflect or zero border); -1 = zero
   auto src_row = [&](int yy) -> int {
@@ -109,15 +122,18 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
     return (xx >= 0 && xx < W) ? xx : -1;
   };
 
-  // global loads of one k-tile's staging: the dY quarter row (A task) of output row y, or the 6
-  // source values x[c][row(yb)][ox0 + 4q - 1 .. ox0 + 4q + 4] (B task) of logical source row yb
-  auto load_a = [&](float (&rv)[10], int y, int ox0) {
-    const int soff = __builtin_amdgcn_readfirstlane((y * W + ox0) * 4);
-    const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff, soff, 0));
+  // global loads of one step's staging, per k-tile t: the dY quarter row (A task) of output row y, or
+  // the 6 source values x[c][row(yb)][ox0 + 16 t + 4q - 1 .. + 4] (B task) of logical source row yb
+  auto load_a = [&](float (&rv)[NRV], int y, int ox0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) rv[e] = v[e];
+    for (int t = 0; t < KT; ++t) {
+      const int soff = __builtin_amdgcn_readfirstlane((y * W + ox0 + WH_BK * t) * 4);
+      const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, a_voff, soff, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rv[4 * t + e] = v[e];
+    }
   };
-  auto load_b = [&](float (&rv)[10], int yb, int ox0) {
+  auto load_b1 = [&](float* rv, int yb, int ox0) {
     const int sy = src_row(yb);
     const int x0 = ox0 + 4 * b_q - 1;
     if (sy >= 0 && x0 >= 0 && x0 + 5 < W) {
@@ -137,7 +153,11 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
       }
     }
   };
-  auto load_stage = [&](float (&rv)[10], int y, int yb, int ox0) {
+  auto load_b = [&](float (&rv)[NRV], int yb, int ox0) {
+#pragma unroll
+    for (int t = 0; t < KT; ++t) load_b1(rv + 6 * t, yb, ox0 + WH_BK * t);
+  };
+  auto load_stage = [&](float (&rv)[NRV], int y, int yb, int ox0) {
     if (is_b) load_b(rv, yb, ox0);
     else if (a_ok) load_a(rv, y, ox0);
   };
@@ -151,50 +171,58 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
       split2<PREC>(u, v, d[0], l);
     }
   };
-  auto store_a = [&](const float (&rv)[10], int buf) {
+  auto store_a = [&](const float (&rv)[NRV], int buf) {
     if (!a_ok) return;
-    uint32_t p0[3], p1[3];
-    split_pair(rv[0], rv[1], p0);
-    split_pair(rv[2], rv[3], p1);
-    uint32_t* d = reinterpret_cast<uint32_t*>(&As[buf][a_row][0]) + 2 * a_q;
 #pragma unroll
-    for (int pc = 0; pc < NPC; ++pc) *reinterpret_cast<u32x2*>(d + 8 * pc) = u32x2{p0[pc], p1[pc]};
+    for (int t = 0; t < KT; ++t) {
+      uint32_t p0[3], p1[3];
+      split_pair(rv[4 * t], rv[4 * t + 1], p0);
+      split_pair(rv[4 * t + 2], rv[4 * t + 3], p1);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&As[buf][t][a_row][0]) + 2 * a_q;
+#pragma unroll
+      for (int pc = 0; pc < NPC; ++pc) *reinterpret_cast<u32x2*>(d + 8 * pc) = u32x2{p0[pc], p1[pc]};
+    }
   };
   // copy kw holds x[ox0 + i + kw - 1], i = 4q .. 4q + 3: from the quarter's 6 values v = x[ox0 + 4q - 1 ..]
   // copies 0 and 2 are the pairs (v0 v1)(v2 v3) and (v2 v3)(v4 v5); copy 1 re-pairs them
-  auto store_b = [&](const float (&rv)[10], int slot) {
-    uint32_t p[3][3];
+  auto store_b = [&](const float (&rv)[NRV], int slot) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) split_pair(rv[2 * q], rv[2 * q + 1], p[q]);
+    for (int t = 0; t < KT; ++t) {
+      uint32_t p[3][3];
 #pragma unroll
-    for (int pc = 0; pc < NPC; ++pc) {
-      const int o = 8 * pc + 2 * b_q;
-      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][0][b_c][0]) + o) = u32x2{p[0][pc], p[1][pc]};
-      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][2][b_c][0]) + o) = u32x2{p[1][pc], p[2][pc]};
-      *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][1][b_c][0]) + o) =
-          u32x2{__builtin_amdgcn_alignbit(p[1][pc], p[0][pc], 16), __builtin_amdgcn_alignbit(p[2][pc], p[1][pc], 16)};
+      for (int q = 0; q < 3; ++q) split_pair(rv[6 * t + 2 * q], rv[6 * t + 2 * q + 1], p[q]);
+#pragma unroll
+      for (int pc = 0; pc < NPC; ++pc) {
+        const int o = 8 * pc + 2 * b_q;
+        *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][0][t][b_c][0]) + o) = u32x2{p[0][pc], p[1][pc]};
+        *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][2][t][b_c][0]) + o) = u32x2{p[1][pc], p[2][pc]};
+        *reinterpret_cast<u32x2*>(reinterpret_cast<uint32_t*>(&Bs[slot][1][t][b_c][0]) + o) =
+            u32x2{__builtin_amdgcn_alignbit(p[1][pc], p[0][pc], 16), __builtin_amdgcn_alignbit(p[2][pc], p[1][pc], 16)};
+      }
     }
   };
-  auto store_stage = [&](const float (&rv)[10], int buf, int slot) {
+  auto store_stage = [&](const float (&rv)[NRV], int buf, int slot) {
     if (is_b) store_b(rv, slot);
     else store_a(rv, buf);
   };
 
-  // the three taps (kh, kw = 0..2) of this wave for k-tile y (A buffer buf)
+  // the three taps (kh, kw = 0..2) of this wave for strip row y, k-tiles t = 0 .. KT-1 (A buffer buf)
   auto compute = [&](int y, int buf) {
     const int slot = (y + kh + 3) & 3;  // logical source row y + kh - 1
-    const float* ap = &As[buf][wm * 32 + lo][4 * hi];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+    const float* ap = &As[buf][t][wm * 32 + lo][4 * hi];
     bf16x8_t af[3];
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) af[pc] = *reinterpret_cast<const bf16x8_t*>(ap + 8 * pc);
     bf16x8_t bfr[3][3];
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
-      const float* bp = &Bs[slot][kw][lo][4 * hi];
+      const float* bp = &Bs[slot][kw][t][lo][4 * hi];
 #pragma unroll
       for (int pc = 0; pc < NPC; ++pc) bfr[kw][pc] = *reinterpret_cast<const bf16x8_t*>(bp + 8 * pc);
     }
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KT == 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       f32x16 c = acc[kw];
@@ -213,12 +241,13 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
       }
       acc[kw] = c;
     }
+    }
   };
 
   // this block's segments: its share [T bz / NB, T (bz + 1) / NB) of the T = N x strips x row chunks
   // segments of the tile pair, image-major, then strip, then chunk (consecutive segments of a block
   // are neighbouring strips of one image)
-  const int nstrip = W / WH_BK;
+  const int nstrip = W / (WH_BK * KT);
   const int nseg = nstrip * P.nchunk;
   const int T = P.N * nseg;
   const int g0 = __builtin_amdgcn_readfirstlane((int)((long)T * bz / P.NB));
@@ -228,7 +257,7 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
     const int strip = gi / P.nchunk, chunk = gi - strip * P.nchunk;
     asrd = uniform_rsrc(P.a + (long)n * P.M * HW, (uint32_t)((long)P.M * HW * 4));
     xsrd = uniform_rsrc(P.x + (long)n * P.Cs * HW, (uint32_t)((long)P.Cs * HW * 4));
-    const int ox0 = __builtin_amdgcn_readfirstlane(strip * WH_BK);
+    const int ox0 = __builtin_amdgcn_readfirstlane(strip * WH_BK * KT);
     const int y0 = __builtin_amdgcn_readfirstlane(chunk * P.rch);
     const int y1 = __builtin_amdgcn_readfirstlane(min(H, y0 + P.rch));
     // prologue: source rows y0 - 1 and y0 into their ring slots, A(y0) and row y0 + 1; the registers
@@ -259,7 +288,7 @@ __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhPar
         __syncthreads();
       }
     } else {
-      auto step = [&](int y, float (&cur)[10], float (&nxt)[10]) {
+      auto step = [&](int y, float (&cur)[NRV], float (&nxt)[NRV]) {
         if (y + 2 < y1) load_stage(nxt, y + 2, y + 3, ox0);
         compute(y, y & 1);
         if (y + 1 < y1) store_stage(cur, (y + 1) & 1, (y + 2) & 3);
@@ -310,7 +339,7 @@ static int wgrad_halo_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 bool wgrad_halo_ok(int M, int Cs, int H, int W, int KH, int KW, int stride, int pad, int up, int gmode, int mode) {
   const int am = vst_mode_arith(mode);
   return KH == 3 && KW == 3 && stride == 1 && pad == 1 && up == 1 && (gmode == 0 || gmode == 1) &&
-         Cs % WH_CB == 0 && W % WH_BK == 0 && H >= 2 && W >= 2 &&
+         Cs % WH_CB == 0 && W % (WH_BK * wh_kt(am, wgrad_halo_bm(M) / 32)) == 0 && H >= 2 && W >= 2 &&
          (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
 }
 
@@ -319,11 +348,11 @@ bool wgrad_halo_ok(int M, int Cs, int H, int W, int KH, int KW, int stride, int 
 // (image, strip, row chunk) segments into its own slab -- NB slabs of Mpad x 9 Cs whatever the batch
 // and image size.  Row chunks halve (down to 16 rows; each costs a two-row ring prologue) until
 // every block has >= 4 segments, so the shares differ by at most a quarter.
-WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W) {
+WhPlan wgrad_halo_plan(int N, int M, int Cs, int H, int W, int mode) {
   WhPlan p;
   const int bm = wgrad_halo_bm(M);
   p.Mpad = (M + bm - 1) / bm * bm;
-  const int nstrip = W / WH_BK;
+  const int nstrip = W / (WH_BK * wh_kt(vst_mode_arith(mode), bm / 32));
   const int pairs = (Cs / WH_CB) * (p.Mpad / bm);
   const int slots = 256 * (4 * WH_WAVES / (3 * (bm / 32)));
   p.NB = slots / pairs > 1 ? slots / pairs : 1;
