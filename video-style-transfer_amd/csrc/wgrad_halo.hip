@@ -43,13 +43,15 @@ constexpr int WH_CB = 32;  // input channels per block (one MFMA column tile per
 // for the single products (wh_kt below) are what helps.
 constexpr int WH_WAVES = 3;
 
-// k-tiles (16-pixel column groups) per strip row: bf16x6 one; the single-product modes two on the 6-wave
-// 64-row blocks and four on the 12-wave 128-row ones -- a 32-column strip row is a whole 128-byte line
-// of dY and of x, and 3 KT MFMAs per wave per barrier instead of 3.  fp16 decoder shapes
-// (tools/wgrad_bench.py, one box; 16 / 32 / 64 columns): 512 ch 1.46 / 1.50 / 1.41 ms, 256 ch 1.53 /
-// 1.46 / 1.37, 128 ch 1.67 / 1.55 / 1.45, 64 ch (64 rows) 3.65 / 2.68 / 2.76, 128 -> 64 ch (64 rows)
-// 1.11 / 0.81 / 1.16 (the 64-column strips' LDS leaves one 6-wave block per CU)
-constexpr int wh_kt(int prec, int wm) { return prec == 3 ? 1 : (wm == 4 ? 4 : 2); }
+// k-tiles (16-pixel column groups) per strip row: two (bf16x6, and the single-product modes on the
+// 6-wave 64-row blocks), four (single products on the 12-wave 128-row blocks) -- a 32-column strip row
+// is a whole 128-byte line of dY and of x, and 3 KT (x the mode's products) MFMAs per wave per barrier.
+// fp16 decoder shapes (tools/wgrad_bench.py, one box; 16 / 32 / 64 columns): 512 ch 1.46 / 1.50 / 1.41
+// ms, 256 ch 1.53 / 1.46 / 1.37, 128 ch 1.67 / 1.55 / 1.45, 64 ch (64 rows) 3.65 / 2.68 / 2.76, 128 -> 64
+// ch (64 rows) 1.11 / 0.81 / 1.16 (the 64-column strips' LDS leaves one 6-wave block per CU); bf16x6
+// (16 / 32 columns): residual 192 ch 0.595 / 0.578 (row-tiled 0.619), decoder 512 ch 2.87 / 2.75,
+// 256 ch 2.87 / 2.78, 128 ch 3.18 / 2.96, 64 ch 5.71 / 4.52
+constexpr int wh_kt(int prec, int wm) { return prec == 3 ? 2 : (wm == 4 ? 4 : 2); }
 
 template <int WM, int PREC, int GMODE>
 __global__ __launch_bounds__(WM * 3 * 64, WH_WAVES) void wgrad_halo_kernel(WhParams P) {

@@ -505,9 +505,10 @@ _WGRAD_UP2 = os.environ.get("VST_WGRAD_UP2", "1") != "0"  # A/B switch for the p
 
 
 # ReCoNet's bf16x6 residual weight gradients (192 rows) stay on the row-tiled kernel: the halo weight
-# gradient only ties it in isolation (0.629 vs 0.624 ms, tools/wgrad_bench.py) and, on the side stream
-# beside the data-gradient GEMMs, overlaps them worse (two 57-KB-LDS blocks per CU): config 3 45.97 vs
-# 44.80 ms per step with it, 46.39 vs 46.28 with the side streams off (one box, tools/gpu_r05_l.sh).
+# gradient is a little faster in isolation (32-column strips: 0.578 vs 0.619 ms, tools/wgrad_bench.py)
+# but, on the side stream beside the data-gradient GEMMs, overlaps them worse (its blocks hold up to
+# 115 KB of LDS): config 3 45.00 / 45.02 ms per step with it vs 44.75 / 44.76 (one box,
+# tools/gpu_r05_k3.sh; the 16-column form: 45.97 vs 44.80).
 # Everywhere else the halo form wins (AdaAttN decoder shapes 0.69-0.75 of the row-tiled time under
 # bf16x6, 0.46-0.65 under fp16).
 WGRAD_HALO_RES = os.environ.get("VST_WGRAD_HALO_RES", "0") != "0"  # A/B
