@@ -329,3 +329,81 @@ def test_halo2_up2_forward_bitwise(mode, shape):
     y = F.conv2d(F.pad(xu, (1, 1, 1, 1), mode="reflect"), w.double(), b.double())
     err = float((res[0].double() - y).abs().max() / y.abs().max())
     assert err < TOL[mode], err
+
+
+def _pack_kwu(w, mode, transposed):
+    Cout, Cin, K, _ = w.shape
+    C = Cout if transposed else Cin
+    Cu = (C * K + 15) // 16 * 16
+    M = Cin if transposed else Cout
+    Mpad, Kpad = _dims(M, K * Cu)
+    p = torch.empty(Mpad * Kpad * 3 // 2 if (mode & 7) == BF16X6 else Mpad * Kpad, device=DEV)
+    assert lib.vst_pack_weight_kwu(w.data_ptr(), p.data_ptr(), Cout, Cin, K, Cu, int(transposed), Mpad, Kpad, mode,
+                                   torch.cuda.current_stream().cuda_stream) == 0
+    return p, Cu
+
+
+def _unfold(x, K, off, sgn, Wout, reflect, Cu):
+    N, C, H, W = x.shape
+    out = torch.full((N, Cu, H, Wout), float("nan"), device=DEV)
+    assert lib.vst_unfold_kw(x.data_ptr(), out.data_ptr(), N, C, H, W, Wout, K, Cu, sgn, off, int(reflect),
+                             torch.cuda.current_stream().cuda_stream) == 0
+    return out
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 3, 40, 64, 48), (1, 3, 17, 96, 32), (1, 3, 33, 32, 64)])
+def test_halo91_kwu_forward_bitwise(mode, shape):
+    """9x9 reflect-pad conv of a 3-channel frame (ReCoNet conv1, RC/network.py:158) as a 9 x 1 conv over
+    the kw-unfolded input (vst_unfold_kw: 27 -> 32 channels): the halo kernel's 9 x 1 form against the
+    per-tap kernel (bitwise) and float64."""
+    N, Cin, H, W, Cout = shape
+    K, pad = 9, 4
+    x = _rand(N, Cin, H, W, seed=70, scale=50.0)
+    w = _rand(Cout, Cin, K, K, seed=71, scale=0.02)
+    b = _rand(Cout, seed=72)
+    st = torch.cuda.current_stream().cuda_stream
+    res = []
+    for mm in (mode | KBLOCK, mode | KBLOCK | PERTAP):
+        wp, Cu = _pack_kwu(w, mm, False)
+        xu = _unfold(x, K, -pad, 1, W, True, Cu)
+        out = torch.full((N, Cout, H, W), float("nan"), device=DEV)
+        assert lib.vst_conv_gemm_padx(xu.data_ptr(), wp.data_ptr(), b.data_ptr(), None, out.data_ptr(), N, Cu, H, W,
+                                      Cout, K * Cu, H, W, K, 1, GM_REFLECT, 1, pad, 0, 1, EPI_BIAS, 0, None, None, None,
+                                      0, mm, st) == 0
+        res.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    y = F.conv2d(F.pad(x.double(), (pad,) * 4, mode="reflect"), w.double(), b.double())
+    err = float((res[0].double() - y).abs().max() / y.abs().max())
+    assert err < TOL[mode], err
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 48, 24, 64, 3), (1, 32, 13, 32, 3)])
+def test_halo91_kwu_padout_dgrad_bitwise(mode, shape):
+    """ConvTanh's data gradient (48 -> 3 channels, 9x9 reflect pad 4, RC/network.py:78-85): the output
+    gradient kw-unfolded over the padded width, a 9 x 1 transposed GEMM over the padded grid (interior
+    into dx, border into the side buffer, EPI_PADOUT), then vst_fold_border -- halo vs per-tap bitwise,
+    and float64."""
+    N, Cin, H, W, Cout = shape
+    K, pad = 9, 4
+    dy = _rand(N, Cout, H, W, seed=73)
+    w = _rand(Cout, Cin, K, K, seed=74, scale=0.02)
+    st = torch.cuda.current_stream().cuda_stream
+    res = []
+    for mm in (mode | KBLOCK, mode | KBLOCK | PERTAP):
+        wp, Cu = _pack_kwu(w, mm, True)
+        dyu = _unfold(dy, K, 0, -1, W + 2 * pad, False, Cu)
+        dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
+        border = torch.zeros(N, Cin, H + 2 * pad, W + 2 * pad, device=DEV)
+        assert lib.vst_conv_dgrad_padout_kwu(dyu.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N,
+                                             Cu, H, Cin, H, W, K, pad, mm, st) == 0
+        assert lib.vst_fold_border(border.data_ptr(), None, dx.data_ptr(), N * Cin, H, W, pad, st) == 0
+        res.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    x = torch.zeros(N, Cin, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
+    F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w.double()).backward(dy.double())
+    err = float((res[0].double() - x.grad).abs().max() / x.grad.abs().max())
+    assert err < TOL[mode], err

@@ -359,10 +359,14 @@ static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, 
   // 3x3 taps (stride 1, reflect / zero / transposed gathers), or the 2x2 phase-stacked GEMMs
   // (EPI_PHASE2: the stride-2 data gradient's transposed gather, the up2 forward's edge clamp)
   const bool ph2 = (epi & EPI_PHASE2) != 0;
+  // 9 x 1 over a kw-unfolded operand (column pad 0): the 64- / 128-row block selections only
+  const bool k91 = !ph2 && KH == 9 && KW == 1 && pad_x == 0 && gmask_free && (hcfg == HALO_M64 || hcfg == HALO_M128) &&
+                   (gmode == GM_REFLECT || gmode == GM_TRANSPOSED);
   const bool taps_ok = ph2 ? (KH == 2 && KW == 2 && (gmode == GM_TRANSPOSED || gmode == GM_CLAMP) && gmask_free)
-                           : (KH == 3 && KW == 3 && (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED));
+                       : k91 ? true
+                             : (KH == 3 && KW == 3 && (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED));
   const bool halo = hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
-                    stride == 1 && up == 1 && Cs % 16 == 0 && pad_x == pad && a_batch_stride == 0 &&
+                    stride == 1 && up == 1 && Cs % 16 == 0 && (pad_x == pad || k91) && a_batch_stride == 0 &&
                     !(epi & EPI_AFFINE) &&
                     (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
   if (!halo) return hp;
@@ -449,7 +453,7 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
     P.gmode = gmode;
     P.stride = 1;
     P.pad = pad;
-    P.pad_x = pad;
+    P.pad_x = pad_x;
     P.up = 1;
     P.epi = epi;
     P.ep_ra = P.ep_rb = P.ep_rd = P.ep_cg = nullptr;

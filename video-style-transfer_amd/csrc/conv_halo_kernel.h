@@ -76,12 +76,16 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // the single-product modes' first-touch gathers, measured slower -- fp16 VGG + residual shapes 2.38 ms
 // at one block, 2.58 at 2, 2.61 at 4: the larger stage halves the resident blocks per CU,
 // profiles/r04_halo_kc.txt -- and was removed in round 5.)
-template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int PD = 1, int KS = 3>
+// KH x KW taps: 3 x 3 (the 3x3 stride-1 convs); 2 x 2 (the phase-stacked GEMMs of the stride-2 data
+// gradient and the nearest-x2 upsample forward, EPI_PHASE2 -- patch (TH + 1) x 33, four taps); 9 x 1
+// (the 9x9 layers over a kw-unfolded operand: ReCoNet conv1's forward and ConvTanh's data gradient,
+// RC/network.py:78-85,158 -- patch (TH + 8) x 32, nine row taps, column pad P.pad_x = 0).
+template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int PD = 1, int KH = 3, int KW = KH>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC >= 1 && PREC <= 4, "halo kernel: bf16x3, bf16x6, bf16 or fp16 products");
-  static_assert(KS == 2 || KS == 3, "halo kernel: 2x2 or 3x3 taps");
-  constexpr int TM = 1, TN = 4, NTAP = KS * KS;
-  constexpr int TH = 4 * WN, HPH = TH + KS - 1, HPW = HTW + KS - 1, HPP = HPH * HPW;
+  static_assert((KH == KW && (KH == 2 || KH == 3)) || (KH == 9 && KW == 1), "halo kernel: 2x2, 3x3 or 9x1 taps");
+  constexpr int TM = 1, TN = 4, NTAP = KH * KW;
+  constexpr int TH = 4 * WN, HPH = TH + KH - 1, HPW = HTW + KW - 1, HPP = HPH * HPW;
   constexpr int NTT = WM * WN * 64;
   constexpr int BM = WM * 32;
   constexpr int AW = PREC == 3 ? 24 : 16;  // packed A dwords per (k-tile, row) (vst_common.h apack_store)
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   const int oy0 = ty * TH, ox0 = (tile - ty * tiles_x) * HTW;
   // forward: source row oy - pad + kh; data gradient (transposed, stride 1): dY row oy + pad - kh
   const bool tr = P.gmode == GM_TRANSPOSED;
-  const int y0 = oy0 + (tr ? P.pad - (KS - 1) : -P.pad), x0 = ox0 + (tr ? P.pad - (KS - 1) : -P.pad);
+  const int y0 = oy0 + (tr ? P.pad - (KH - 1) : -P.pad), x0 = ox0 + (tr ? P.pad_x - (KW - 1) : -P.pad_x);
 
   const int plane = P.Hs * P.Ws;
   const long plane_l = (long)plane;
@@ -208,8 +212,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
   auto taps = [&](int cb, int buf) {
 #pragma unroll
     for (int t = 0; t < NTAP; ++t) {
-      const int kh = t / KS, kw = t % KS;
-      const int ph = tr ? KS - 1 - kh : kh, pw = tr ? KS - 1 - kw : kw;  // (tr is block-uniform)
+      const int kh = t / KW, kw = t % KW;
+      const int ph = tr ? KH - 1 - kh : kh, pw = tr ? KW - 1 - kw : kw;  // (tr is block-uniform)
       const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : NTAP * (cb + 1);
       if (t < NTAP - 1 || cb + 1 < nst) load_a(kt_next, arN);
       // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
@@ -316,7 +320,7 @@ inline int halo_cfg(int M, int pack_mpad) {
 
 constexpr int HALO_SMINW_SP = 4;  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
 constexpr int HALO_PD = 2;        // patches in flight for the single-product double-buffered tiles
-template <int C, int PR, bool GM, int KS = 3>
+template <int C, int PR, bool GM, int KH = 3, int KW = KH>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
   // waves per SIMD the registers must allow: one-buffer tiles 4 for the single-product modes (their
@@ -331,7 +335,7 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
   // bf16x6 (MFMA-bound, registers spoken for)
   constexpr int PD = (PR != 3 && halo_db_c(C) && WM * WN >= 8) ? HALO_PD : 1;
-  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), PD, KS><<<grid, WM * WN * 64, 0, st>>>(P);
+  conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), PD, KH, KW><<<grid, WM * WN * 64, 0, st>>>(P);
 }
 
 // only the block shapes the build's selection can reach are instantiated
@@ -353,9 +357,17 @@ void launch_halo2(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
   else launch_halo_c<HALO_M256, PR, false, 2>(grid, st, P);
 }
 
+// the 9 x 1 GEMMs over kw-unfolded operands (48 weight rows: the 64-row selection; 128 for other widths)
 template <int PR>
-void launch_halo_prec(bool gm, int c, int ks, dim3 grid, hipStream_t st, const ConvParams& P) {
-  if (ks == 2) launch_halo2<PR>(c, grid, st, P);
+void launch_halo91(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (c == HALO_M64) launch_halo_c<HALO_M64, PR, false, 9, 1>(grid, st, P);
+  else launch_halo_c<HALO_M128, PR, false, 9, 1>(grid, st, P);
+}
+
+template <int PR>
+void launch_halo_prec(bool gm, int c, int kh, dim3 grid, hipStream_t st, const ConvParams& P) {
+  if (kh == 2) launch_halo2<PR>(c, grid, st, P);
+  else if (kh == 9) launch_halo91<PR>(c, grid, st, P);
   else gm ? launch_halo<PR, true>(c, grid, st, P) : launch_halo<PR, false>(c, grid, st, P);
 }
 

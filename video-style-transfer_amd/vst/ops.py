@@ -48,6 +48,11 @@ KBLOCK_ON = _KB != "0"
 KBLOCK_STYLIZER = _KB == "2"
 KBLOCK_RES = _KB in ("2", "res")
 KBLOCK_UP2 = KBLOCK_ON and os.environ.get("VST_KBLOCK_UP2", "1") != "0"  # A/B: the up2 phase forward blocked
+# the kw-unfolded 9x9 forward (ReCoNet conv1) in the channel-blocked order, i.e. on the halo kernel's 9 x 1
+# form: off -- like the stylizer's other forwards (above), the blocked order moves the ragged golden
+# step's conv1 InstanceNorm-weight gradient past its bar under bf16x6 (margin 1.05); its data gradient
+# (ConvTanh's, in the backward) takes the 9 x 1 halo form
+KBLOCK_KWU = KBLOCK_ON and os.environ.get("VST_KBLOCK_KWU", "0") != "0"
 # The C ABI is stateless: every GEMM / pack entry takes its arithmetic mode as an argument.  This
 # module chooses that argument per call from a named policy (base mode + per-role overrides,
 # optionally per model scope); _CUR holds the mode chosen by the latest gemm_role() call, which
@@ -438,6 +443,9 @@ def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dmask=None):
     return dx
 
 
+HALO91 = os.environ.get("VST_HALO91", "1") != "0"  # A/B: ConvTanh's data gradient on the 9 x 1 halo form
+
+
 def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dmask=None):
     """conv_dgrad_padout for a thin output gradient (ConvTanh 48->3): dy is kw-unfolded first,
     dyu[co*K + kw][y][v] = dy[co][y][v - kw] over the padded width, so the transposed GEMM is a
@@ -452,7 +460,7 @@ def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dmask=None):
                       (N, dyu.shape[1], Ho, W + 2 * pad, Cin, H + 2 * pad, W + 2 * pad, 1, ks, GM_TRANSPOSED, 1, 0, 1),
                       gemm_mode())
     lib.vst_conv_dgrad_padout_kwu(ptr(dyu), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, dyu.shape[1], Ho, Cin, H, W,
-                                  ks, pad, gemm_mode(), stream())
+                                  ks, pad, gemm_mode() | (0 if HALO91 else PERTAP), stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dmask), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -795,7 +803,10 @@ class Conv2dFn(Function):
             lib.vst_conv_up2_fwd(ptr(x), ptr(wp), ptr(bias), ptr(out), N, Cin, H, W, Cout, gemm_mode(), stream())
             kprof.end(tok)
         elif kwu_ok(Cin, ks, stride, up, W) and 0 < pad < min(H, W) and Ho == H and Wo == W:
-            # thin input (3-channel frames): kw-unfold, then a Kx1 conv on the 16-channel k-tile path
+            # thin input (3-channel frames): kw-unfold, then a Kx1 conv on the 16-channel k-tile path, in
+            # the channel-blocked K order (the halo-tiled kernel's 9 x 1 form)
+            if KBLOCK_KWU:
+                _CUR[0] |= KBLOCK
             xu = unfold_kw(x, ks, -pad, 1, W, pad_mode == "reflect")
             out = conv_gemm(xu, packed_weight(w, False, kwu=True), Cout, 1, Ho, Wo,
                             GM_REFLECT if pad_mode == "reflect" else GM_ZERO, 1, pad, 1, epi=epi, bias=bias, aux=aux,
