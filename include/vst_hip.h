@@ -229,8 +229,8 @@ int vst_symmetrize(const float* g, float* S, int N, int C, int Kpad, int Mpad, f
 int vst_instnorm_fwd(const float* x, const float* w, const float* b, const float* res, float* y, float* stats, int N,
                      int C, int HW, float eps, int relu, void* stream);
 /* partial: N*C*3 floats; gw, gb, gbias_prev (sum of gx = grad of the feeding conv's bias) may be NULL.
- * relu: the ReLU mask is y > 0 when y is given, else the pre-activation recomputed from x and b
- * (bit-identical to the forward's; valid only when the forward had no residual add). */
+ * relu: the ReLU mask is the pre-activation recomputed from x and b (bit-identical to the forward's)
+ * when y is NULL, else y > 0 -- valid only when the forward had no residual add (y = relu(.) + res). */
 int vst_instnorm_bwd(const float* gy, const float* x, const float* y, const float* b, const float* stats,
                      const float* w, float* gx, float* gw, float* gb, float* gbias_prev, float* partial, int N, int C,
                      int HW, int relu, int accumulate, void* stream);

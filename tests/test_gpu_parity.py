@@ -255,7 +255,13 @@ def test_vgg_slice_fused_relu_backward():
 
 
 @pytest.mark.parametrize("relu,res,shape", [(True, False, (2, 48, 16, 20)), (False, True, (2, 192, 9, 15)),
-                                            (True, False, (1, 96, 64, 128))])
+                                            (True, False, (1, 96, 64, 128)),
+                                            # the one-pass LDS backward (8192 < HW <= 32768, HW % 4 == 0):
+                                            # recomputed ReLU mask, mask from y (residual), partial last column
+                                            (True, False, (2, 8, 128, 256)), (True, True, (2, 6, 96, 200)),
+                                            (False, False, (1, 5, 100, 120)),
+                                            # the two-pass kernels: HW > 32768, and HW % 4 != 0
+                                            (True, False, (1, 4, 256, 260)), (True, False, (1, 3, 101, 103))])
 def test_instance_norm(relu, res, shape):
     from vst import ops
 

@@ -884,8 +884,9 @@ class InstanceNormFn(Function):
         ctx.relu = relu
         ctx.has_res = res is not None
         ctx.params = (w, b, conv_bias)
-        # the backward recomputes the ReLU mask from x and b unless a residual was added after it
-        keep_y = relu and (res is not None or _IN_YMASK)
+        # the backward recomputes the ReLU mask from x and b; y > 0 is the mask only without a
+        # residual added after the ReLU (y = relu(.) + res)
+        keep_y = relu and _IN_YMASK and res is None
         # b is saved (not read live from ctx.params) so an in-place update of it before this
         # backward -- the recomputed ReLU mask depends on it -- trips autograd's version check
         # (FlatParams.adam bumps the flat buffer's version after its kernel)
