@@ -125,12 +125,6 @@ int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, f
 /* mask (optional, dx-shaped): the fold adds only where mask > 0 (the producer's ReLU backward fused
  * into a masked data gradient: the GEMM epilogue already zeroed dx there) */
 int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream);
-/* vst_conv_dgrad_padout (no mask) ADDING its interior into dx: dx holds a gradient already (the
- * ResidualBlock skip's, RC/network.py:150 `out + residual`), so dx = g_skip + dgrad after
- * vst_fold_border -- autograd's separate sum of the two gradients removed.  Same workspace query. */
-int vst_conv_dgrad_padout_accum(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout,
-                                int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* workspace, long ws_bytes,
-                                int mode, void* stream);
 /* Thin-channel convolutions (RC/network.py:155 conv1 = ConvLayer(3, 48, 9), :169 deconv3 =
  * ConvTanh(48, 3, 9) backward, VGG conv1_1): a tensor with C*K <= Cu channels is kw-unfolded,
  *   out[n][c*K + kw][y][v] = src[n][c][y][v + sgn*kw + off]  (reflect or zero outside; zero channels

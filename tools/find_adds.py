@@ -18,7 +18,6 @@ def main():
     ops.use_policy("bf16x6")
     args = bench.parse()
     args.warmup, args.steps, args.prof_steps = 0, 1, 0
-    args.batch = args.batch or 8
     step = bench.build_reconet(args, torch.device("cuda"), 0)
     step()
     torch.cuda.synchronize()

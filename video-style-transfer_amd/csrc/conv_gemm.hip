@@ -739,18 +739,6 @@ int vst_conv_dgrad_padout(const float* dy, const float* wpack, const float* mask
                           ws_bytes);
 }
 
-int vst_conv_dgrad_padout_accum(const float* dy, const float* wpack, float* dx, float* border, int N, int Cout,
-                                int Ho, int Wo, int Cin, int H, int W, int KS, int pad, void* workspace, long ws_bytes,
-                                int mode, void* stream) {
-  VST_CHECK_ARG(vst_mode_ok(mode));
-  VST_CHECK_ARG(ws_bytes >= 0 && (workspace || ws_bytes == 0));
-  VST_CHECK_ARG(dy && wpack && dx && border && N > 0 && Cout > 0 && Cin > 0 && KS > 0 && pad >= 0 && pad < H &&
-                pad < W && Ho == H + 2 * pad - KS + 1 && Wo == W + 2 * pad - KS + 1);
-  return conv_gemm_launch(dy, wpack, nullptr, nullptr, dx, N, Cout, Ho, Wo, Cin, KS * KS * Cout, H + 2 * pad,
-                          W + 2 * pad, KS, KS, GM_TRANSPOSED, 1, 0, 0, 1, EPI_PADOUT | EPI_ACCUM, 0, nullptr, nullptr,
-                          mode, stream, nullptr, nullptr, nullptr, nullptr, border, H, W, pad, workspace, ws_bytes);
-}
-
 int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream) {
   VST_CHECK_ARG(border && dx && NC > 0 && H > 0 && W > 0 && pad >= 0 && pad < H && pad < W);
   if (pad == 0) return VST_OK;

@@ -118,11 +118,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int ci = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (ci < Cx) {
-              // EPI_ACCUM (no mask): interior values added to dx (a residual skip's gradient already there)
-              const float v = (mk && !(mk[ci * cstride] > 0.f)) ? 0.f : acc[i][j][r];
-              base[ci * cstride] = (in && (P.epi & EPI_ACCUM)) ? base[ci * cstride] + v : v;
-            }
+            if (ci < Cx) base[ci * cstride] = (mk && !(mk[ci * cstride] > 0.f)) ? 0.f : acc[i][j][r];
           }
         continue;
       }
@@ -189,8 +185,7 @@ __device__ __forceinline__ void conv_epilogue_elem(const ConvParams& P, int n, i
     const int y = I - P.ph_pad, x = J - P.ph_pad;
     if (y >= 0 && y < P.ph_H && x >= 0 && x < P.ph_W) {
       const long o = ((long)n * P.M + m) * P.ph_H * P.ph_W + (long)y * P.ph_W + x;
-      const float u = ((P.epi & EPI_MASK) && !(P.mask[o] > 0.f)) ? 0.f : v;
-      P.out[o] = (P.epi & EPI_ACCUM) ? P.out[o] + u : u;
+      P.out[o] = ((P.epi & EPI_MASK) && !(P.mask[o] > 0.f)) ? 0.f : v;
     } else {
       const int Hp = P.ph_H + 2 * P.ph_pad, Wp = P.ph_W + 2 * P.ph_pad;
       P.ph_border[(((long)n * P.M + m) * Hp + I) * Wp + J] = v;

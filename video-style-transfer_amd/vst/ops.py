@@ -380,21 +380,10 @@ def splitk_workspace(like, *geom):
     return _empty(((nb + 3) // 4,), like), nb
 
 
-def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=None, acc=None):
+def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=None):
     """Input gradient of (upsample x`up` -> pad -> conv(stride)) given the conv-output grad gz;
     dmask: multiply the result by (dmask > 0) in the GEMM epilogue (zero-pad path, and the
-    stride-1 reflect-pad padded-grid path with its border fold).  acc: an x-shaped gradient the
-    result is added to (and returned in): on the padded-grid path the GEMM epilogue and the border
-    fold add into it, elsewhere one explicit add."""
-    if acc is not None:
-        N, Cin, H, W = x_shape
-        if (dmask is None and gmask is None and pad_mode == "reflect" and stride == 1 and up == 1 and
-                0 < pad < min(H, W) and not (kwu_ok(w.shape[0], ks, stride, up, W + 2 * pad) and w.shape[2] == ks)
-                and acc.is_contiguous() and acc.shape == tuple(x_shape)):
-            gemm_role("dgrad")
-            return conv_dgrad_padout(gz, w, x_shape, ks, pad, 2.0 * N * w.shape[0] * gz.shape[2] * gz.shape[3] * Cin *
-                                     ks * ks, acc=acc)
-        return acc.add_(conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask, dmask))
+    stride-1 reflect-pad padded-grid path with its border fold)."""
     gemm_role("dgrad")
     N, Cin, H, W = x_shape
     Cout = w.shape[0]
@@ -434,27 +423,21 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
     return dx
 
 
-def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dmask=None, acc=None):
+def conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dmask=None):
     """Stride-1 reflect-pad conv input gradient: the transposed GEMM over the padded grid writes
-    its interior straight into dx and its border into a side buffer, folded into dx's border band.
-    acc (no dmask): dx is acc, a gradient the interior epilogue and the fold add into."""
+    its interior straight into dx and its border into a side buffer, folded into dx's border band."""
     N, Cin, H, W = x_shape
     Cout, Ho, Wo = w.shape[0], gz.shape[2], gz.shape[3]
     wp = packed_weight(w, transposed=True)
-    dx = acc if acc is not None else _empty(x_shape, gz)
+    dx = _empty(x_shape, gz)
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
     mode = gemm_mode()
-    epi = EPI_PADOUT | (EPI_MASK if dmask is not None else 0) | (EPI_ACCUM if acc is not None else 0)
-    ws, nws = splitk_workspace(gz, N, Cout, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 0, 1, epi, 0,
-                               mode)
-    tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel() * (2 if acc is not None else 1)),
+    ws, nws = splitk_workspace(gz, N, Cout, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 0, 1,
+                               EPI_PADOUT | (EPI_MASK if dmask is not None else 0), 0, mode)
+    tok = kprof.begin(flops, 4.0 * (gz.numel() + wp.numel() + dx.numel()),
                       (N, Cout, Ho, Wo, Cin, H + 2 * pad, W + 2 * pad, ks, ks, GM_TRANSPOSED, 1, 0, 1), mode)
-    if acc is not None:
-        lib.vst_conv_dgrad_padout_accum(ptr(gz), ptr(wp), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
-                                        ptr(ws), nws, mode, stream())
-    else:
-        lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks,
-                                  pad, ptr(ws), nws, mode, stream())
+    lib.vst_conv_dgrad_padout(ptr(gz), ptr(wp), ptr(dmask), ptr(dx), ptr(border), N, Cout, Ho, Wo, Cin, H, W, ks, pad,
+                              ptr(ws), nws, mode, stream())
     kprof.end(tok)
     lib.vst_fold_border(ptr(border), ptr(dmask), ptr(dx), N * Cin, H, W, pad, stream())
     return dx
@@ -777,16 +760,13 @@ class Conv2dFn(Function):
     torchvision VGG Conv2d+ReLU pairs (RC/network.py:17-24, AA/vgg19.py:19-37)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act, bias_const=None, mask_dx=False, premasked=False,
-                skip=None):
+    def forward(ctx, x, w, b, stride, pad, pad_mode, up, act, bias_const=None, mask_dx=False, premasked=False):
         """bias_const: a bias added in the epilogue whose gradient another Function produces
         (conv -> InstanceNorm: the norm's backward already sums the conv-output gradient).
         mask_dx: x is a ReLU output consumed only by this conv -> the data gradient is written
         masked by x > 0 (the ReLU backward of the producer, fused into this dgrad's epilogue);
         premasked: this conv's ReLU output is consumed only by such a masking consumer, so the
-        incoming gradient is already masked and the separate ReLU-backward pass is skipped.
-        skip: a SkipGrad that a later InstanceNormFn(res=x) fills with the residual skip's gradient
-        of x; the data gradient is then accumulated into it (ResidualBlock, RC/network.py:150)."""
+        incoming gradient is already masked and the separate ReLU-backward pass is skipped."""
         x = _check(x, "conv input", 4)
         w = w.contiguous()
         N, Cin, H, W = x.shape
@@ -839,7 +819,6 @@ class Conv2dFn(Function):
         ctx.geom = (ks, stride, pad, pad_mode, up, act)
         ctx.scope = _SCOPE[0]
         ctx.relu_flags = (bool(mask_dx), bool(premasked))
-        ctx.skip = skip
         ctx.has_bias = b is not None and bias_const is None
         ctx.params = (w, b)  # leaves: weight gradients go straight into their .grad when possible
         ctx.save_for_backward(x, w, out if act == "relu" else None, aux)
@@ -866,9 +845,8 @@ class Conv2dFn(Function):
             lib.vst_relu_bwd(ptr(gy), ptr(y), ptr(gz), gy.numel(), stream())
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            acc = ctx.skip.take() if ctx.skip is not None else None
             dx = conv_dgrad(gz, w, x.shape, ks, stride, pad, pad_mode, up, gmask=gmask,
-                            dmask=x if ctx.relu_flags[0] else None, acc=acc)
+                            dmask=x if ctx.relu_flags[0] else None)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.params[0])
             if rowsplit_wgrad_ok(w.shape[0], w.shape[1], ks, stride, pad_mode, up, x.shape[3]) and pad == ks // 2:
@@ -882,7 +860,7 @@ class Conv2dFn(Function):
             sink = grad_sink(ctx.params[1])
             db = channel_sum(gz, out=sink)
             db = None if sink is not None else db
-        return dx, dw, db, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, pad_mode="zero", up=1, act=None, mask_dx=False, premasked=False):
@@ -893,11 +871,9 @@ class InstanceNormFn(Function):
     """InstanceNorm2d(C, affine=True) [-> ReLU] [+ residual] (RC/network.py:91-97, 126-132, 140-150)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res, relu, eps, conv_bias=None, skip=None):
+    def forward(ctx, x, w, b, res, relu, eps, conv_bias=None):
         """conv_bias: bias of the conv producing x (added in that conv's epilogue); its gradient,
-        sum of dx over (n, h, w), falls out of this backward's per-plane partials.  skip: a SkipGrad
-        shared with the conv that also reads res; the backward hands res's gradient to it instead of
-        returning it, and that conv's data gradient adds into it (no autograd sum)."""
+        sum of dx over (n, h, w), falls out of this backward's per-plane partials."""
         x = _check(x, "instance_norm input", 4)
         N, C, H, W = x.shape
         y = _empty(x.shape, x)
@@ -907,7 +883,6 @@ class InstanceNormFn(Function):
                              H * W, float(eps), int(relu), stream())
         ctx.relu = relu
         ctx.has_res = res is not None
-        ctx.skip = skip if res is not None else None
         ctx.params = (w, b, conv_bias)
         # the backward recomputes the ReLU mask from x and b; y > 0 is the mask only without a
         # residual added after the ReLU (y = relu(.) + res)
@@ -936,51 +911,24 @@ class InstanceNormFn(Function):
                              ptr(gx), ptr(gw), ptr(gb), ptr(gc), ptr(part), N, C, H * W, int(ctx.relu), int(direct),
                              stream())
         gres = gy if ctx.has_res else None
-        if gres is not None and ctx.skip is not None and ctx.needs_input_grad[3]:
-            ctx.skip.put(gres)
-            gres = None
         if direct:
             gw = gb = gc = None
-        return gx, gw, gb, gres, None, None, gc, None
+        return gx, gw, gb, gres, None, None, gc
 
 
 def instance_norm(x, w, b, relu=False, res=None, eps=1e-5):
     return InstanceNormFn.apply(x, w, b, res, relu, eps)
 
 
-class SkipGrad:
-    """The residual skip's gradient of a ResidualBlock input x (RC/network.py:150 `out + residual`),
-    passed from the block's second InstanceNormFn backward (which runs first) to the backward of the
-    conv that also reads x, whose data gradient is accumulated into it in place of autograd's sum of
-    the two gradients.  The tensor is the gradient autograd handed that backward (consumed there)."""
-
-    __slots__ = ("g",)
-
-    def __init__(self):
-        self.g = None
-
-    def put(self, g):
-        self.g = g if g.is_contiguous() else g.contiguous()
-
-    def take(self):
-        g, self.g = self.g, None
-        return g
-
-
-SKIP_ACCUM = os.environ.get("VST_SKIP_ACCUM", "1") != "0"  # A/B: residual skip gradient summed by autograd
-
-
 def conv_instance_norm(x, w, b, gamma, beta, stride=1, pad=0, pad_mode="reflect", up=1, relu=False, res=None,
-                       eps=1e-5, dx_skip=None, res_skip=None):
+                       eps=1e-5):
     """conv [+bias] -> InstanceNorm(affine) [-> ReLU] [+ res] (ConvInstRelu, UpsampleConvInstRelu,
     ResidualBlock halves).  The conv bias gradient comes out of the norm's backward partials, so
-    no separate channel-sum pass re-reads the gradient.  dx_skip / res_skip: one SkipGrad given to
-    the block's first half (its conv reads x) and second half (res = x)."""
+    no separate channel-sum pass re-reads the gradient."""
     if b is None:
-        y = Conv2dFn.apply(x, w, None, stride, pad, pad_mode, up, None, None, False, False, dx_skip)
-        return InstanceNormFn.apply(y, gamma, beta, res, relu, eps, None, res_skip)
-    y = Conv2dFn.apply(x, w, None, stride, pad, pad_mode, up, None, b.detach(), False, False, dx_skip)
-    return InstanceNormFn.apply(y, gamma, beta, res, relu, eps, b, res_skip)
+        return instance_norm(conv2d(x, w, None, stride, pad, pad_mode, up), gamma, beta, relu, res, eps)
+    y = Conv2dFn.apply(x, w, None, stride, pad, pad_mode, up, None, b.detach())
+    return InstanceNormFn.apply(y, gamma, beta, res, relu, eps, b)
 
 
 class MaxPool2x2Fn(Function):

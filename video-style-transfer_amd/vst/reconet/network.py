@@ -228,13 +228,11 @@ class ResidualBlock(nn.Module):
     def forward(self, x):
         c1, c2 = self.conv1.conv2d, self.conv2.conv2d
         p1, p2 = self.conv1.reflection_padding, self.conv2.reflection_padding
-        # the skip's gradient of x is added inside conv1's data gradient (ops.SkipGrad)
-        skip = ops.SkipGrad() if ops.SKIP_ACCUM else None
         with ops.gemm_scope("res"):
             out = ops.conv_instance_norm(x, c1.weight, c1.bias, self.in1.weight, self.in1.bias, c1.stride[0], p1,
-                                         relu=True, eps=self.in1.eps, dx_skip=skip)
+                                         relu=True, eps=self.in1.eps)
             return ops.conv_instance_norm(out, c2.weight, c2.bias, self.in2.weight, self.in2.bias, c2.stride[0], p2,
-                                          relu=False, res=x, eps=self.in2.eps, res_skip=skip)
+                                          relu=False, res=x, eps=self.in2.eps)
 
 
 class ReCoNet(nn.Module):
