@@ -616,9 +616,6 @@ inline int widen_cfg(int c, long HWo) {
 
 // waves per SIMD the tiles' registers must allow (occupancy targets, measured per tile)
 constexpr int MINW_T128 = 4, MINW_T256 = 2, MINW_T192 = 2, MINW_SMALL = 4;
-// bf16x3 (hi + lo of both operands): the 4x2-accumulator tile needs more than the 256 registers two
-// waves per SIMD leave (it spilled 63 VGPRs, or moved its accumulators to scratch), so one wave
-constexpr int MINW_T256_X3 = 1;
 constexpr int MINW_T128_BF = 3;  // bf16 paths: the hi/lo conversion temporaries push the 2x2-accumulator tile past 128 VGPRs
 constexpr int MINW_ADIR = 3, MINW_A256 = 4;  // A-direct tiles (one wave per 32 weight rows, 128 pixels per block)
 
@@ -654,8 +651,7 @@ static void launch_cfg(int cfg, dim3 grid, hipStream_t st, const ConvParams& P) 
       if constexpr (AD) launch_k<4, 1, 1, 4, CF, GMK, MINW_ADIR, PR, true, true>(grid, st, P);
       break;
     case T256:  // bf16x3 / bf16 / fp16 only (launch side): 4x2 accumulators per wave, twice the MFMAs per gathered B element
-      if constexpr (PR == 1 || PR == 2 || PR == 4)
-        launch_k<2, 4, 2, 2, CF, GMK, PR == 1 ? MINW_T256_X3 : MINW_T256, PR, false, true>(grid, st, P);
+      if constexpr (PR == 1 || PR == 2 || PR == 4) launch_k<2, 4, 2, 2, CF, GMK, MINW_T256, PR, false, true>(grid, st, P);
       break;
     default: launch_k<2, 3, 2, 2, CF, GMK, MINW_T192, PR>(grid, st, P); break;
   }
