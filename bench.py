@@ -384,13 +384,16 @@ def build_reconet(args, dev, rank):
     trainer = ReCoNetTrainer.for_script(script, model, vgg, style)
 
     def stage(parts):
-        img1, img2, f01, f10, motion = (t.to(dev) for t in parts)
-        frames = torch.stack([img1, img2]).contiguous()
+        # (staged before the timed region; the frame stack and the motion product on the host, so the
+        # device runs only the library's kernels)
+        img1, img2, f01, f10, motion = parts
+        frames = torch.stack([img1, img2]).contiguous().to(dev)
         if trainer.single:  # config 2: the 2B frames of the B pairs as single images
             return (frames.reshape(2 * B, 3, H, W),)
-        # occlusion mask on the device (RC/utilities.py:60-90) x the motion stand-in
-        mask = torch.stack([ops.flow_warp_mask(f01[b], f10[b]) for b in range(B)]) * motion
-        return frames, f10.contiguous(), mask.contiguous()
+        # occlusion mask on the device (RC/utilities.py:60-90, batched) x the motion stand-in
+        occ = ops.flow_warp_mask(f01.contiguous().to(dev), f10.contiguous().to(dev))
+        mask = (occ.cpu() * motion).contiguous().to(dev)
+        return frames, f10.contiguous().to(dev), mask
 
     batches = per_step_batches(args, rank, lambda seed: frame_pair_parts(seed, B, H, W), stage)
     return cycle_steps(trainer.step, batches)
@@ -460,7 +463,7 @@ def build_adaattn(args, dev, rank):
     trainer = AdaAttNTrainer(model, vgg, activation="cosine")
     B, H, W = args.batch, args.height, args.width
     batches = per_step_batches(args, rank, lambda seed: content_style_batch(seed, B, H, W),
-                               lambda cs: (torch.stack([c.to(dev) for c in cs]).contiguous(),))
+                               lambda cs: (torch.stack(cs).contiguous().to(dev),))
     return cycle_steps(trainer.step, batches)
 
 

@@ -48,8 +48,9 @@ const char* vst_build_id(void);
  *   VST_GEMM_F16     one fp16 product per fp32 product (v_mfma_f32_32x32x16_f16, 11-bit significand,
  *                    ~2^-11 per operand rounding, fp32 accumulate): BASELINE config 5's fp16 MFMA
  *                    path.  fp16's range ends at 65504 and its normal range at 6.1e-5, so the caller
- *                    keeps operands inside it (the AdaAttN trainer scales the loss, hence every
- *                    backward operand, by a static power of two and unscales in Adam).
+ *                    keeps operands inside it (the trainers scale the loss, hence every backward
+ *                    operand, by a dynamic power of two -- initial 2^12, halved on an Inf / NaN
+ *                    gradient, doubled after 2000 clean steps -- and vst_adam_loss_scaled unscales).
  * VST_GEMM_KBLOCK may be or-ed into the mode of a conv pack + GEMM pair (both must carry it):
  * channel-block-major, tap-minor K order (16 channels x every tap, then the next 16 channels), which
  * keeps each block's re-read source rows L2-resident; the sums then run in a different order.
@@ -58,9 +59,11 @@ const char* vst_build_id(void);
  * results are bitwise those of the per-tap kernel.  VST_GEMM_PERTAP or-ed into a GEMM call's mode
  * selects the per-tap kernel instead (an explicit per-call choice for A/B measurement and the
  * equivalence test; pack entries ignore it).
- * A bf16x6 / bf16 halo launch whose grid would not fill the chip (fewer than 512 blocks: AdaAttN
- * config 4's decoder, VGG19 conv4 / conv5) is split over the 16-channel blocks (split-K; fp16 launches
- * stay unsplit): the slices' raw sums go to the CALLER's `workspace` (vst_conv_splitk_workspace bytes,
+ * A bf16x6 / bf16x3 / bf16 / fp16 halo launch whose grid would not fill the chip (fewer than 512 blocks:
+ * AdaAttN config 4's decoder, VGG19 conv4 / conv5) is split over the 16-channel blocks (split-K) when the
+ * caller passes a workspace (fp16 launches too since round 5; tests/test_gpu_adaattn.py
+ * test_f16_step_order_insensitive holds the fp16 step's tolerance under that summation-order change):
+ * the slices' raw sums go to the CALLER's `workspace` (vst_conv_splitk_workspace bytes,
  * 16-byte aligned), and a reduce kernel on the same stream adds them in slice order (deterministic)
  * and applies the epilogue -- equal to the unsplit result up to fp32 summation order.  A launch given
  * a smaller (or NULL) workspace runs unsplit, so ws_bytes = 0 is always valid.
@@ -182,7 +185,9 @@ int vst_fold_ring(const float* ring, float* dx, long NC, int Hs, int Ws, int KS,
 int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int pad, int up, int accumulate,
                      void* stream);
 /* weight gradient, split-K over output pixels with deterministic slab reduction;
- * workspace floats = vst_conv_wgrad_workspace(same geometry and mode).  3x3 stride-1 pad-1 convs over
+ * workspace / ws_floats: at least vst_conv_wgrad_workspace(same geometry and mode) floats.  A workspace
+ * smaller than that but at least vst_wgrad_workspace(N, Cout, KH*KW*Cin, Ho*Wo) (the row-tiled kernel's
+ * need) runs the row-tiled kernel; a smaller one returns VST_EINVAL.  3x3 stride-1 pad-1 convs over
  * 32-channel multiples with 16-multiple widths (ResidualBlock, the AdaAttN decoder) run on the halo
  * weight gradient under the split-product modes (bf16x6 / bf16 / fp16): one block owns all nine taps
  * of 32 input channels and walks a 16-column strip down the rows, the source rows in an LDS ring (each
@@ -191,9 +196,9 @@ int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int 
 long vst_wgrad_workspace(int N, int M, int J, int HWo);
 long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
                               int stride, int pad, int up, int mode);
-int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
-                   int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
-                   int mode, void* stream);
+int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, long ws_floats, int N, int Cin,
+                   int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up,
+                   int accumulate, int mode, void* stream);
 /* same for a stride-1 reflect-padded KxK conv with tiny Cout (row-split, GEMM rows (co,kh));
  * workspace floats = vst_wgrad_workspace(N, Cout*K, K*Cin, (H+K-1)*W) */
 int vst_conv_wgrad_rowsplit(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int H,
@@ -480,10 +485,29 @@ int vst_pfm_read_header(const char* path, int* width, int* height, int* channels
                         float* scale);
 int vst_pfm_read(const char* path, void* dst, long bytes, int offset);
 
+/* ---- gradient sums / fills -----------------------------------------------------------------
+ * out[i] = ((a[i] + b[i]) + c[i]) + d[i] over n floats, NULL addends skipped (a..d: at least one);
+ * out may be one of the addends.  The autograd gradient sum of a tensor with several consumers
+ * (vst/ops.py ForkFn: ResidualBlock's input, RC/network.py:136-150; the feature map and the stylised
+ * frame, RC/train_single/train_candy.py:100-145; loss-term sums) -- the ATen add it replaces summed
+ * two at a time.  vst_fill: x[i] = value (the flat gradient's zeroing before each step). */
+int vst_sum4(const float* a, const float* b, const float* c, const float* d, float* out, long n, void* stream);
+int vst_fill(float* x, long n, float value, void* stream);
+
 /* ---- profiling ---------------------------------------------------------------------------
  * an empty kernel (vst_marker_kernel) on `stream`: marks a region boundary in rocprofv3 traces
  * (bench.py launches one before its timed steps; tools/pmc_traffic.py --after-marker) */
 int vst_marker(void* stream);
+/* test only: one wave on `stream` that sleeps iters x 8128 cycles (about 3.5 us each at 2.4 GHz), so
+ * the work enqueued after it on that stream starts late; the stream-ordering tests
+ * (tests/test_gpu_streams.py) put it in front of each cross-stream hand-off of the training step.
+ * iters < 0: VST_EINVAL. */
+int vst_test_delay(long iters, void* stream);
+/* test only: `blocks` x 256 lanes of three kernels with 256 B / 1280 B / 4608 B private (scratch)
+ * segments each write `value` over their whole private array on `stream`, so the scratch slots the
+ * next kernels with register spills get on that stream hold `value` (a NaN) -- a kernel that read a
+ * private slot before writing it would then show it (tools/f16_repro.py --poison-scratch). */
+int vst_test_scratch_poison(long blocks, float value, void* stream);
 
 #ifdef __cplusplus
 }

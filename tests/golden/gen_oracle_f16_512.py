@@ -1,9 +1,10 @@
 """Fixture for tests/test_gpu_adaattn.py::test_train_video_f16_512x1024: the ORACLE's fp32 loss terms
-of one train_video forward (AA/train_video.py:84-114) at config 5's frame size, 512x1024 (B = 1), on
+of one train_video step (AA/train_video.py:84-121) at config 5's frame size, 512x1024 (B = 1), on
 the seeded weights (stylizer 61, VGG19 62) and the seeded triple (vst.synthetic.content_style_batch
-63).  The oracle itself is pinned against the reference's own train_video step at 64x128
-(tests/golden/aa_step.npz, tests/test_oracle_golden.py); this fixture only moves its CPU forward at
-the full frame size (about a minute on 8 cores) out of the GPU test.
+63), and its backward: every stylizer parameter's gradient norm (float64 of the fp32 gradient) and 256
+elements per tensor at seeded positions.  The oracle itself is pinned against the reference's own
+train_video step at 64x128 (tests/golden/aa_step.npz, tests/test_oracle_golden.py); this fixture only
+moves its CPU step at the full frame size (a few minutes on 8 cores) out of the GPU test.
 
     python tests/golden/gen_oracle_f16_512.py      (CPU; writes tests/golden/aa_f16_512.npz)
 """
@@ -25,6 +26,7 @@ from vst.synthetic import content_style_batch  # noqa: E402
 
 SEEDS = (61, 62, 63)
 B, H, W = 1, 512, 1024
+SAMPLES = 256
 
 
 def main():
@@ -32,15 +34,26 @@ def main():
     c1, c2, s = content_style_batch(SEEDS[2], B, H, W)
     P = oracle.seeded_params(shapes.stylizing_network(), SEEDS[0])
     VP = oracle.seeded_params(shapes.vgg19(), SEEDS[1])
+    for t in P.values():
+        t.requires_grad_(True)
     t0 = time.time()
-    with torch.no_grad():
-        L = A.adaattn_losses(P, VP, c1, c2, s)
+    L = A.adaattn_losses(P, VP, c1, c2, s)
     out = {k: np.float64(L[k].item()) for k in ("loss", "loss_gs", "loss_lf", "loss_is")}
+    L["loss"].backward()
+    names = [n for n, _ in shapes.stylizing_network()]
+    g = np.random.default_rng(SEEDS[0])
+    out["grad_names"] = np.array(names)
+    for n in names:
+        gr = P[n].grad.detach().double().reshape(-1)
+        idx = np.sort(g.choice(gr.numel(), size=min(SAMPLES, gr.numel()), replace=False))
+        out[f"gnorm:{n}"] = np.float64(gr.norm())
+        out[f"gidx:{n}"] = idx.astype(np.int64)
+        out[f"gval:{n}"] = gr.numpy()[idx]
     out["seeds"] = np.array(SEEDS)
     out["shape"] = np.array([B, H, W])
     out["input_sums"] = np.array([float(t.double().sum()) for t in (c1, c2, s)])
     np.savez(os.path.join(HERE, "aa_f16_512.npz"), **out)
-    print({k: float(v) for k, v in out.items() if v.ndim == 0}, f"{time.time() - t0:.1f} s")
+    print({k: float(v) for k, v in out.items() if v.ndim == 0 and ":" not in k}, f"{time.time() - t0:.1f} s")
 
 
 if __name__ == "__main__":

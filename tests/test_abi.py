@@ -59,7 +59,16 @@ def test_host_side_argument_validation_without_gpu():
     for bad in (-1, 5, 7, 8):
         assert lib.vst_pack_weight(1, 1, 4, 3, 3, 3, 0, 0, 64, 32, bad, None) == -1
         assert lib.vst_gemm_abt(1, 1, 1, 1, 1, 4, 4, 16, 1.0, bad, None) == -1
-        assert lib.vst_conv_wgrad(1, 1, 1, 1, 1, 3, 8, 8, 4, 8, 8, 3, 3, 0, 1, 1, 1, 0, bad, None) == -1
+        assert lib.vst_conv_wgrad(1, 1, 1, 1, 1 << 20, 1, 3, 8, 8, 4, 8, 8, 3, 3, 0, 1, 1, 1, 0, bad, None) == -1
+    # a workspace below both the halo slabs and the row-tiled kernel's need is refused before any
+    # launch (ResidualBlock 192 -> 192 under bf16x6, whose halo slab exceeds the row-tiled workspace)
+    geom = (2, 192, 64, 128, 192, 64, 128, 3, 3, 0, 1, 1, 1)
+    need = lib.vst_conv_wgrad_workspace(*geom, 3)
+    rowtiled = lib.vst_wgrad_workspace(2, 192, 9 * 192, 64 * 128)
+    assert need > 0 and rowtiled > 0
+    n, cin, h, w, cout, ho, wo, kh, kw, gm, st, pd, up = geom
+    small = min(need, rowtiled) - 1
+    assert lib.vst_conv_wgrad(1, 1, 1, 1, small, n, cin, h, w, cout, ho, wo, kh, kw, gm, st, pd, up, 0, 3, None) == -1
 
 
 @pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libvst_hip.so not built")

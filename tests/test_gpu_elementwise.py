@@ -258,3 +258,56 @@ def test_adaattn_elementwise_vec_and_flat(misalign):
     ref = torch.cat([(dout - 2 * M * dvar) * s, dvar * s], 1)
     assert rel_err(C(dMV).numpy(), ref.numpy()) < 1e-5
     assert rel_err(C(nrm).numpy(), xs.double().norm(dim=1).float().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("shape,B,halves", [((4, 3, 8, 16), 2, (1, 1)), ((4, 5, 7, 9), 2, (3, 1)),
+                                            ((2, 6, 4, 4), 0, (1, 1)), ((6, 2, 5, 8), 3, (2, 0))])
+@pytest.mark.parametrize("n", [0, 1, 2, 5])
+def test_fork_gradient_sums(shape, B, halves, n):
+    """ops.fork (ForkFn): every consumer's gradient arrives separately and vst_sum4 adds them per batch
+    half (the residual skip, feature map, stylised frame and loss-feature sums of the two training
+    steps) -- against the gradient autograd's own additions give for the same consumers (torch fp32,
+    CPU), 1e-6 relative; vst_sum4 covers 1..4 addends per pass, n = 5 chains two passes."""
+    from vst import ops
+
+    if n == 0 and not B:
+        pytest.skip("no consumers")
+    g = torch.Generator().manual_seed(n + 10 * B)
+    x = torch.randn(*shape, generator=g)
+    h1, h2 = halves if B else (0, 0)
+    ws = [torch.randn(*shape, generator=g) for _ in range(n)]
+    w1 = [torch.randn(B, *shape[1:], generator=g) for _ in range(h1)]
+    w2 = [torch.randn(shape[0] - B, *shape[1:], generator=g) for _ in range(h2)]
+    xd = G(x).requires_grad_(True)
+    outs = ops.fork(xd, n, B, halves)
+    assert len(outs) == n + h1 + h2
+    terms = [(o * G(w)).sum() for o, w in zip(outs, ws + w1 + w2)]
+    torch.stack(terms).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    ref = [(xr * w).sum() for w in ws] + [(xr[:B] * w).sum() for w in w1] + [(xr[B:] * w).sum() for w in w2]
+    torch.stack(ref).sum().backward()
+    assert rel_err(C(xd.grad), xr.grad) < 1e-6
+
+
+def test_sum_scalars_and_backward_seed():
+    """ops.sum_scalars (SumScalarsFn): the loss-term sums of both trainers in vst_sum4 passes; the
+    gradient reaches every term unchanged.  ops.backward_seed: the cached 0-d 1.0 the trainers seed
+    backward with."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(3)
+    xs = [G(torch.randn(5, generator=g)).requires_grad_(True) for _ in range(7)]
+    terms = [(x * x).sum() for x in xs]
+    for k in (1, 2, 4, 5, 7):
+        tot = ops.sum_scalars(*terms[:k])
+        ref = sum(float(t.detach()) for t in terms[:k])
+        assert abs(float(tot) - ref) <= 1e-6 * abs(ref)
+    for x in xs:
+        x.grad = None
+    tot = ops.sum_scalars(*terms)
+    seed = ops.backward_seed(tot)
+    assert seed.shape == () and float(seed) == 1.0
+    tot.backward(seed)
+    for x in xs:
+        assert torch.equal(C(x.grad), C(2 * x.detach()))
+    assert float(ops.backward_seed(tot)) == 1.0  # backward left the cached seed unchanged

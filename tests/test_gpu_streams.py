@@ -7,6 +7,8 @@ every run here starts from emptied caches.  The HIP step has no float atomics on
 streams on and off -- and on again -- must give BITWISE equal loss terms, flat gradients and
 post-Adam parameters (ReCoNet train_candy step, RC/train_single/train_candy.py:77-152; AdaAttN
 train_video step, AA/train_video.py:78-122, under the fp32-class and the fp16 policy)."""
+import contextlib
+
 import pytest
 import torch
 
@@ -19,6 +21,7 @@ def _fresh_caches():
 
     ops._PACK_CACHE.clear()
     ops._CONST_FILL.clear()
+    ops._SEED.clear()
     attention._ONES.clear()
     attention._AFFINE_ID.clear()
 
@@ -87,6 +90,111 @@ def test_side_streams_bitwise(kind, policy):
         assert l == l0, (i, l, l0)
         assert torch.equal(g, g0), (i, float((g - g0).abs().max() / g0.abs().max()))
         assert torch.equal(p, p0), i
+
+
+@contextlib.contextmanager
+def _poisoned_allocations():
+    """Every float HIP tensor made through torch.empty (the library's outputs, workspaces, packs and
+    constants) is filled with NaN on the allocating stream first: a read of memory before its
+    producer wrote it -- on another stream that skipped a wait -- then shows as a NaN instead of
+    silently reading what an earlier run left in a recycled block."""
+    orig = torch.empty
+
+    def empty(*a, **k):
+        t = orig(*a, **k)
+        if t.is_cuda and t.is_floating_point():
+            t.fill_(float("nan"))
+        return t
+
+    torch.empty = empty
+    try:
+        yield
+    finally:
+        torch.empty = orig
+
+
+# vst_test_delay iterations (~3.5 us each): 1500 ~ 5 ms, far longer than any kernel of these steps
+_DELAY = 1500
+_PLACES = ("side_branch", "wgrad_side", "pack", "persistent")
+
+
+def _run(kind, side, places=(), poison=False):
+    from vst import ops
+
+    _fresh_caches()
+    ops.WGRAD_SIDE = ops.CONTENT_SIDE = side
+    ops.TEST_DELAY.clear()
+    ops.TEST_DELAY.update({p: _DELAY for p in places})
+    try:
+        with _poisoned_allocations() if poison else contextlib.nullcontext():
+            tr = _trainer(kind)
+            out = tr.step(*_batch(kind))
+            torch.cuda.synchronize()
+    finally:
+        ops.TEST_DELAY.clear()
+    return {k: float(v) for k, v in out.items()}, tr.flat.g.clone(), tr.flat.p.clone()
+
+
+@pytest.mark.parametrize("kind,policy", [("reconet", "bf16x6"), ("adaattn", "f16")])
+def test_side_streams_delay_injected(kind, policy):
+    """Each cross-stream hand-off of the step widened by a 5 ms stall on the stream at that point
+    (vst_test_delay): the head of the input-only side branch (its reads of the main stream's data
+    features start late), the head of each side-stream weight gradient (its reads of gz / x start
+    late, the join before Adam is tested against a late writer), each weight pack kernel (a reader on
+    the other stream that skipped the pack's event would run first), each lazily created constant's
+    fill (ditto for constant()) -- one placement at a time, then all four, every allocation poisoned
+    with NaN.  Each run must equal, bitwise, the step with the side streams off, no stalls and no
+    poison (which itself must equal the poisoned in-line step: no kernel reads memory it did not
+    write)."""
+    from vst import ops
+
+    ops.gemm_role("fwd")
+    saved = (ops.WGRAD_SIDE, ops.CONTENT_SIDE, ops.POLICY_NAME[0])
+    try:
+        ops.use_policy(policy)
+        ref = _run(kind, False)
+        cases = [("inline-poisoned", False, (), True)]
+        cases += [(p, True, (p,), True) for p in _PLACES]
+        cases += [("all", True, _PLACES, True)]
+        bad = []
+        for name, side, places, poison in cases:
+            l, g, p = _run(kind, side, places, poison)
+            if not (l == ref[0] and torch.equal(g, ref[1]) and torch.equal(p, ref[2])):
+                gd = float((g - ref[1]).abs().max() / ref[1].abs().max())
+                bad.append((name, {k: l[k] - ref[0][k] for k in l}, gd))
+    finally:
+        ops.WGRAD_SIDE, ops.CONTENT_SIDE = saved[:2]
+        ops.use_policy(saved[2])
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("kind,policy", [("reconet", "bf16x6"), ("adaattn", "f16")])
+def test_step_bitwise_under_scratch_poison(kind, policy):
+    """Kernels with register spills keep them in per-wave private (scratch) slots that the next
+    dispatch on the same queue reuses.  A kernel that read a private slot before writing it would pick
+    up whatever the previous kernel left there -- in a repeated step usually the same bits, which hides
+    it.  vst_test_scratch_poison fills every scratch slot of both streams with NaN first (three slot
+    sizes up to 4.5 KB per lane, 4096 x 256 lanes each); the step must still equal, bitwise, the step
+    run without the poison (the one-off f16 difference of round 5 came from a
+    build whose spilling conv tile held 576 B of private memory per lane)."""
+    from vst import ops
+    from vst._lib import lib
+
+    ops.gemm_role("fwd")
+    saved = (ops.WGRAD_SIDE, ops.CONTENT_SIDE, ops.POLICY_NAME[0])
+    try:
+        ops.use_policy(policy)
+        ref = _run(kind, True)
+        dev = torch.device("cuda")
+        for st in (torch.cuda.current_stream(dev), ops._side_stream(dev)):
+            lib.vst_test_scratch_poison(4096, float("nan"), st.cuda_stream)
+        torch.cuda.synchronize()
+        l, g, p = _run(kind, True)
+    finally:
+        ops.WGRAD_SIDE, ops.CONTENT_SIDE = saved[:2]
+        ops.use_policy(saved[2])
+    assert l == ref[0], (l, ref[0])
+    assert torch.equal(g, ref[1]) and torch.equal(p, ref[2])
 
 
 def test_warp_backward_deterministic_under_converging_flow():

@@ -26,7 +26,7 @@ def _wgrad(dy, x, Cout, gmode, mode, out=None):
     ws = torch.empty(nf, device=DEV)
     acc = out is not None
     dw = torch.full((Cout, Cin, 3, 3), float("nan"), device=DEV) if out is None else out
-    lib.vst_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), N, Cin, H, W, Cout, H, W, 3, 3,
+    lib.vst_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), nf, N, Cin, H, W, Cout, H, W, 3, 3,
                        gmode, 1, 1, 1, int(acc), mode, torch.cuda.current_stream().cuda_stream)
     return dw
 
@@ -91,3 +91,31 @@ def test_halo_wgrad_workspace_query():
                                                                            1, 1, BF16X6 | PERTAP)
     assert q(2, 192, 9, 15, 192, 9, 15, 3, 3, 0, 1, 1, 1, BF16X6) == lib.vst_wgrad_workspace(2, 192, 1728, 135)
     assert q(2, 192, 8, 16, 192, 8, 16, 3, 3, 0, 1, 1, 1, 0) == lib.vst_wgrad_workspace(2, 192, 1728, 128)
+
+
+def test_halo_wgrad_undersized_workspace_runs_rowtiled():
+    """vst_conv_wgrad takes the workspace's size: a caller that sizes it by the row-tiled
+    kernel's rule (vst_wgrad_workspace) below the halo slabs gets the row-tiled kernel -- bitwise the
+    VST_GEMM_PERTAP result -- instead of an out-of-bounds slab write; below both sizes the call is
+    refused."""
+    from vst._lib import VstError
+
+    # (a shape whose halo slabs outgrow the row-tiled workspace: few channel blocks, many strips)
+    N, Cin, H, W, Cout = 1, 32, 128, 256, 32
+    x = _rand(N, Cin, H, W, seed=6)
+    dy = _rand(N, Cout, H, W, seed=7)
+    st = torch.cuda.current_stream().cuda_stream
+    for mode in (BF16X6, F16):
+        halo_nf = lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, H, W, 3, 3, 0, 1, 1, 1, mode)
+        rt_nf = lib.vst_wgrad_workspace(N, Cout, 9 * Cin, H * W)
+        assert halo_nf > rt_nf > 0, (halo_nf, rt_nf)
+        ws = torch.empty(rt_nf, device=DEV)
+        dw = torch.full((Cout, Cin, 3, 3), float("nan"), device=DEV)
+        lib.vst_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), rt_nf, N, Cin, H, W, Cout, H, W,
+                           3, 3, 0, 1, 1, 1, 0, mode, st)
+        ref = _wgrad(dy, x, Cout, 0, mode | PERTAP)
+        torch.cuda.synchronize()
+        assert torch.equal(dw, ref)
+        with pytest.raises(VstError):
+            lib.vst_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), rt_nf - 1, N, Cin, H, W,
+                               Cout, H, W, 3, 3, 0, 1, 1, 1, 0, mode, st)

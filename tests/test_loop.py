@@ -122,9 +122,25 @@ def test_train_state_roundtrip_restores_adam_and_scaler():
     buf = io.BytesIO()
     torch.save(_flat.train_state(src), buf)
     buf.seek(0)
-    dst = _Tr()
-    dst.flat, dst.step_count, dst.scaler = _Flat(), 0, None
-    dst.flat.m.zero_(), dst.flat.v.zero_()
-    _flat.load_train_state(dst, torch.load(buf, weights_only=True))
-    assert dst.step_count == 7 and torch.equal(dst.flat.m, src.flat.m) and torch.equal(dst.flat.v, src.flat.v)
-    assert dst.scaler.state_dict() == src.scaler.state_dict()
+    from vst import ops
+
+    ops.gemm_role("fwd")
+    saved = ops.POLICY_NAME[0]
+    try:
+        for policy in ("f16", "bf16x6"):
+            ops.use_policy(policy)
+            buf.seek(0)
+            dst = _Tr()
+            dst.flat, dst.step_count, dst.scaler = _Flat(), 0, None
+            dst.flat.m.zero_(), dst.flat.v.zero_()
+            if policy == "f16":
+                _flat.load_train_state(dst, torch.load(buf, weights_only=True))
+                assert dst.scaler.state_dict() == src.scaler.state_dict()
+            else:
+                # a loss-scaled checkpoint resumed under an unscaled policy: the scaler is not restored
+                with pytest.warns(UserWarning, match="loss scaler"):
+                    _flat.load_train_state(dst, torch.load(buf, weights_only=True))
+                assert dst.scaler is None
+            assert dst.step_count == 7 and torch.equal(dst.flat.m, src.flat.m) and torch.equal(dst.flat.v, src.flat.v)
+    finally:
+        ops.use_policy(saved)

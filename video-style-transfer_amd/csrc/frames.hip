@@ -201,3 +201,45 @@ extern "C" int vst_marker(void* stream) {
   vst_marker_kernel<<<1, 64, 0, (hipStream_t)stream>>>();
   return vst_launch_status();
 }
+
+// test-only stall (tests/test_gpu_streams.py): one wave that sleeps `iters` x 127·64 cycles on
+// `stream`, so whatever the caller enqueues after it on that stream starts late.  The stream-
+// ordering tests put it in front of each cross-stream producer / consumer to widen the window a
+// missing event or record_stream would leave open.
+namespace {
+__global__ void vst_test_delay_kernel(long iters) {
+  for (long i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+extern "C" int vst_test_delay(long iters, void* stream) {
+  if (iters < 0) return VST_EINVAL;
+  vst_test_delay_kernel<<<1, 64, 0, (hipStream_t)stream>>>(iters);
+  return vst_launch_status();
+}
+
+// test-only private-memory poison (tools/f16_repro.py --poison-scratch, tests/test_gpu_streams.py):
+// every lane writes `value` over a P-float private array (dynamically indexed, so it lives in the
+// wave's scratch slot) and never reads it back (`sink` is written only if `stride` < 0).  Launched
+// with many waves on a stream before a step, it overwrites the scratch slots that the step's kernels
+// with a private segment (register spills) then get, so a kernel that read a private slot before
+// writing it would pick up `value` (a NaN) instead of a stale copy of the same data.
+namespace {
+template <int P>
+__global__ __launch_bounds__(256) void vst_scratch_poison_kernel(float value, int stride, float* sink) {
+  float buf[P];
+  for (int i = 0; i < P; ++i) buf[(i * stride + (int)threadIdx.x) % P] = value;
+  if (stride < 0) sink[threadIdx.x] = buf[((int)threadIdx.x * 7) % P];
+}
+}  // namespace
+
+extern "C" int vst_test_scratch_poison(long blocks, float value, void* stream) {
+  if (blocks <= 0) return VST_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  // three per-lane sizes (256 B, 1280 B, 4608 B): a slot's offset is its wave index times the
+  // dispatch's per-wave size, so each size lays the poison on that size's slot grid
+  vst_scratch_poison_kernel<64><<<blocks, 256, 0, s>>>(value, 1, nullptr);
+  vst_scratch_poison_kernel<320><<<blocks, 256, 0, s>>>(value, 1, nullptr);
+  vst_scratch_poison_kernel<1152><<<blocks, 256, 0, s>>>(value, 1, nullptr);
+  return vst_launch_status();
+}

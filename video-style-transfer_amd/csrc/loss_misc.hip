@@ -476,6 +476,63 @@ static int nblocks(long work) {
 
 }  // namespace
 
+// Gradient sums of a tensor with several consumers (vst_sum4): out = ((a + b) + c) + d, absent
+// addends skipped (out may be one of the addends: each element is read before it is written); four elements per thread when every pointer is 16-byte aligned and n % 4 == 0.
+template <int K>
+__global__ __launch_bounds__(256) void sum4_vec_kernel(const float4* a, const float4* b,
+                                                       const float4* c, const float4* d,
+                                                       float4* out, long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 s = a[i];
+  if (K > 1) {
+    const float4 t = b[i];
+    s = make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+  }
+  if (K > 2) {
+    const float4 t = c[i];
+    s = make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+  }
+  if (K > 3) {
+    const float4 t = d[i];
+    s = make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+  }
+  out[i] = s;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void sum4_kernel(const float* a, const float* b,
+                                                   const float* c, const float* d,
+                                                   float* out, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = a[i];
+  if (K > 1) s += b[i];
+  if (K > 2) s += c[i];
+  if (K > 3) s += d[i];
+  out[i] = s;
+}
+
+__global__ __launch_bounds__(256) void fill_vec_kernel(float4* __restrict__ x, long n4, float v) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) x[i] = make_float4(v, v, v, v);
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ x, long n, float v) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+
+template <int K>
+static void launch_sum4(const float* a, const float* b, const float* c, const float* d, float* out, long n,
+                        bool vec, hipStream_t s) {
+  if (vec)
+    sum4_vec_kernel<K><<<ceil_div(n / 4, 256), 256, 0, s>>>((const float4*)a, (const float4*)b, (const float4*)c,
+                                                           (const float4*)d, (float4*)out, n / 4);
+  else
+    sum4_kernel<K><<<ceil_div(n, 256), 256, 0, s>>>(a, b, c, d, out, n);
+}
+
 extern "C" {
 
 // workspace: >= 2*1024 floats; out: 3 floats (loss, weight/denom, count)
@@ -655,6 +712,39 @@ int vst_adam_loss_scaled(float* p, const float* g, float* m, float* v, long n, f
   grad_nonfinite_kernel<<<nb, 256, 0, st>>>(g, n, ws);
   loss_scale_update_kernel<<<1, 256, 0, st>>>(ws, nb, state, lr, b1, b2, world_scale, growth_interval, growth, backoff);
   adam_scaled_kernel<<<ceil_div(n, 256), 256, 0, st>>>(p, g, m, v, n, b1, b2, eps, state);
+  return vst_launch_status();
+}
+
+int vst_sum4(const float* a, const float* b, const float* c, const float* d, float* out, long n, void* stream) {
+  // compact the present addends to the front, keeping their order
+  const float* src[4] = {a, b, c, d};
+  const float* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  int k = 0;
+  uintptr_t align = (uintptr_t)out;
+  for (int i = 0; i < 4; ++i)
+    if (src[i]) {
+      p[k++] = src[i];
+      align |= (uintptr_t)src[i];
+    }
+  VST_CHECK_ARG(out && n > 0 && k > 0);
+  const bool vec = (n & 3) == 0 && (align & 15) == 0;
+  hipStream_t s = (hipStream_t)stream;
+  switch (k) {
+    case 1: launch_sum4<1>(p[0], p[1], p[2], p[3], out, n, vec, s); break;
+    case 2: launch_sum4<2>(p[0], p[1], p[2], p[3], out, n, vec, s); break;
+    case 3: launch_sum4<3>(p[0], p[1], p[2], p[3], out, n, vec, s); break;
+    default: launch_sum4<4>(p[0], p[1], p[2], p[3], out, n, vec, s); break;
+  }
+  return vst_launch_status();
+}
+
+int vst_fill(float* x, long n, float value, void* stream) {
+  VST_CHECK_ARG(x && n > 0);
+  hipStream_t s = (hipStream_t)stream;
+  if ((n & 3) == 0 && ((uintptr_t)x & 15) == 0)
+    fill_vec_kernel<<<ceil_div(n / 4, 256), 256, 0, s>>>((float4*)x, n / 4, value);
+  else
+    fill_kernel<<<ceil_div(n, 256), 256, 0, s>>>(x, n, value);
   return vst_launch_status();
 }
 

@@ -1080,13 +1080,19 @@ long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, 
   return vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
 }
 
-int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, int N, int Cin, int Hs, int Ws,
-                   int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up, int accumulate,
-                   int mode, void* stream) {
+int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace, long ws_floats, int N, int Cin,
+                   int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode, int stride, int pad, int up,
+                   int accumulate, int mode, void* stream) {
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
-  if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode)) {
+  const long rowtiled_floats = vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
+  bool halo = use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode);
+  // a workspace sized for the row-tiled kernel (the pre-halo rule) but smaller than the halo slabs
+  // runs row-tiled; one smaller than both is refused
+  if (halo && ws_floats < wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws, mode))) halo = false;
+  VST_CHECK_ARG(halo || ws_floats >= rowtiled_floats);
+  if (halo) {
     const WhPlan p = wgrad_halo_plan(N, Cout, Cin, Hs, Ws, mode);
     hipStream_t st = (hipStream_t)stream;
     int rc = wgrad_halo_launch(p, dy, x, workspace, N, Cout, Cin, Hs, Ws, gmode, mode, st);

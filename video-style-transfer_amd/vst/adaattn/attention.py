@@ -96,8 +96,7 @@ def _ones(n, like):
     key = (like.device, n)
     v = _ONES.get(key)
     if v is None:
-        v = ops.persistent(torch.ones(n, device=like.device, dtype=torch.float32))
-        _ONES[key] = v
+        v = _ONES[key] = ops.persistent_full(like, (n, 1.0))[0]
     return ops.constant(v)
 
 
@@ -462,7 +461,5 @@ def instance_norm_plain(x, eps=1e-5):
     key = (x.device, C)
     wb = _AFFINE_ID.get(key)
     if wb is None:
-        # (one event after both fills: the zeros are enqueued last)
-        wb = (torch.ones(C, device=x.device), ops.persistent(torch.zeros(C, device=x.device)))
-        _AFFINE_ID[key] = wb
-    return ops.instance_norm(x, wb[0], ops.constant(wb[1]), eps=eps)
+        wb = _AFFINE_ID[key] = tuple(ops.persistent_full(x, (C, 1.0), (C, 0.0)))
+    return ops.instance_norm(x, ops.constant(wb[0]), ops.constant(wb[1]), eps=eps)

@@ -18,7 +18,6 @@ Multi-GPU: one process per GPU, (content1, content2, style) triples sharded acro
 RCCL all-reduce of the flat gradient per step; Adam applies the 1/world average.  Every loss term
 is a per-rank mean or per-rank sum exactly as the reference computes it on its own batch.
 """
-import os
 
 import torch
 
@@ -53,38 +52,6 @@ def _cat2(x, y):
     ops.copy_into(x.contiguous(), out[:x.shape[0]])
     ops.copy_into(y.contiguous(), out[x.shape[0]:])
     return out
-
-
-class _Halves(torch.autograd.Function):
-    """(x[:B], x[B:]) along the batch, whose backward writes the two halves' gradients straight into
-    one buffer (autograd's slice backward zero-fills a full-size tensor per half and then adds the
-    two: two fills, two copies and an add per VGG feature)."""
-
-    @staticmethod
-    def forward(ctx, x, B):
-        ctx.B = B
-        ctx.shape = x.shape
-        return x[:B].view_as(x[:B]), x[B:].view_as(x[B:])
-
-    @staticmethod
-    def backward(ctx, g1, g2):
-        B = ctx.B
-        gx = torch.empty(ctx.shape, device=(g1 if g1 is not None else g2).device, dtype=torch.float32)
-        for g, dst in ((g1, gx[:B]), (g2, gx[B:])):
-            if g is None:
-                dst.zero_()
-            else:
-                ops.copy_into(g.contiguous(), dst)
-        return gx, None
-
-
-_HALVES = os.environ.get("VST_HALVES", "1") != "0"
-
-
-def _halves(v, B):
-    if not (_HALVES and v.requires_grad):
-        return v[:B], v[B:]
-    return _Halves.apply(v, B)
 
 
 def _down_sampled(fc, fs):
@@ -148,23 +115,23 @@ class AdaAttNTrainer:
         cs = self.model(fc12, fs2, down=down)  # cs1 ++ cs2
         with ops.gemm_scope("lossnet"):
             fcs = self.vgg(cs)
-        halves = {k: _halves(v, B) for k, v in fcs.items()}
-        fcs1 = {k: h[0] for k, h in halves.items()}
-        fcs2 = {k: h[1] for k, h in halves.items()}
-        gs = None
-        for k in FEATURES[1:]:
-            t = global_stylized_loss(fcs1[k], fs[k], weight=w["LAMBDA_G"])
-            gs = t if gs is None else gs + t
+        # each loss feature of the stylised pair is read by up to three loss terms (frame 1) and one
+        # (frame 2): one autograd output per reader (ops.fork), their gradients summed per frame in one
+        # pass -- no ATen adds, no slice zero-fills
+        g_k, l_k, i_k = FEATURES[1:], FEATURES[2:5], FEATURES[1:4]
+        views = {}
+        for k, v in fcs.items():
+            n1, n2 = (k in g_k) + (k in l_k) + (k in i_k), int(k in i_k)
+            if n1 + n2:
+                views[k] = list(ops.fork(v, 0, B, (n1, n2)))
+        first = lambda k: views[k].pop(0)  # noqa: E731  (frame-1 views lead the list)
+        second = lambda k: views[k].pop()  # noqa: E731  (the frame-2 view ends it)
+        gs = ops.sum_scalars(*[global_stylized_loss(first(k), fs[k], weight=w["LAMBDA_G"]) for k in g_k])
         side.join()
-        lf = None
-        for i in range(3):
-            t = local_feature_loss(fcs1[FEATURES[i + 2]], targets[i], weight=w["LAMBDA_L"])
-            lf = t if lf is None else lf + t
-        isl = None
-        for k in FEATURES[1:4]:
-            t = image_similarity_loss(fc1[k], fc2[k], fcs1[k], fcs2[k], weight=w["LAMBDA_IS"])
-            isl = t if isl is None else isl + t
-        return {"loss": gs + lf + isl, "loss_gs": gs, "loss_lf": lf, "loss_is": isl}
+        lf = ops.sum_scalars(*[local_feature_loss(first(l_k[i]), targets[i], weight=w["LAMBDA_L"]) for i in range(3)])
+        isl = ops.sum_scalars(*[image_similarity_loss(fc1[k], fc2[k], first(k), second(k), weight=w["LAMBDA_IS"])
+                                for k in i_k])
+        return {"loss": ops.sum_scalars(gs, lf, isl), "loss_gs": gs, "loss_lf": lf, "loss_is": isl}
 
     def image_losses(self, c, s):
         """Loss terms of one train_image step (AA/train_image.py:76-106): content / style images,

@@ -224,6 +224,13 @@ def policy_scope(name):
 def gemm_role(role):
     """Choose the mode for a GEMM of `role` (call before packing its A operand); the first call
     applies the VST_GEMM_POLICY environment variable (default "f32")."""
+    m = role_mode(role)
+    _CUR[0] = m
+    return m
+
+
+def role_mode(role):
+    """The mode gemm_role(role) would choose here, without making it the current one."""
     _ensure_policy()
     m = None
     sc = _PSCOPE[0] if _PSCOPE[0] is not None else _SCOPE[0]
@@ -242,7 +249,6 @@ def gemm_role(role):
     if KBLOCK_ON and (KBLOCK_STYLIZER or not in_stylizer or
                       (KBLOCK_RES and (sc.startswith("stylizer.res") or "dec" in sc.split(".")))):
         m |= KBLOCK
-    _CUR[0] = m
     return m
 
 
@@ -300,6 +306,7 @@ def packed_weight(w, transposed, split_kh=False, kwu=False):
         M, K = (Cin, KH * KW * Cout) if transposed else (Cout, KH * KW * Cin)
     Mpad, Kpad = pack_dims(M, K)
     out = _empty((pack_floats(Mpad, Kpad),), w)
+    inject_delay("pack")
     if kwu:
         lib.vst_pack_weight_kwu(ptr(w), ptr(out), Cout, Cin, KW, Cu, int(transposed), Mpad, Kpad, gemm_mode(), stream())
     else:
@@ -533,13 +540,14 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     mode = gemm_mode()
     if not WGRAD_HALO_RES and (mode & 7) == GEMM_MODES["bf16x6"] and Cout % 192 == 0 and Cout % 128 != 0:
         mode |= PERTAP
-    ws = _empty((lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up, mode),), x)
+    nws = lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up, mode)
+    ws = _empty((nws,), x)
     acc = out is not None
     dw = _empty(w_shape, x) if out is None else out
     tok = kprof.begin(2.0 * N * Cout * Ho * Wo * Cin * ks * ks, 4.0 * (gz.numel() + x.numel() + dw.numel()),
                       ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), mode)
-    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up,
-                       int(acc), mode, stream())
+    lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), nws, N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad,
+                       up, int(acc), mode, stream())
     kprof.end(tok, family="wgrad")
     return dw
 
@@ -580,9 +588,11 @@ def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
         return False
     # the halo weight gradient (vst_conv_wgrad: 32-channel multiples, split-product modes) beats the
     # row-split GEMM on these shapes (fp16 decoder conv6 1.12 vs 1.41 ms, conv7 3.6 vs 4.5 ms at config 5,
-    # tools/wgrad_bench.py); the row-split form stays for the f32 / bf16x3 modes and other widths
-    return not (Cin % 32 == 0 and (gemm_role("wgrad") & 7) in (GEMM_MODES["bf16x6"], GEMM_MODES["bf16"],
-                                                               GEMM_MODES["f16"]))
+    # tools/wgrad_bench.py); the row-split form stays for the f32 / bf16x3 modes and the widths the halo
+    # kernel does not take (csrc/wgrad_halo.hip wgrad_halo_ok: its 64-row blocks walk 32-column strips
+    # in every split-product mode, so W % 32 == 0)
+    return not (Cin % 32 == 0 and W % 32 == 0 and (role_mode("wgrad") & 7) in (
+        GEMM_MODES["bf16x6"], GEMM_MODES["bf16"], GEMM_MODES["f16"]))
 
 
 def conv_fwd_rowsplit(x, w, b, epi, aux):
@@ -672,6 +682,7 @@ def wgrad_into_sink(compute, sink, *used, overlap=True):
     side = _side_stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
+        inject_delay("wgrad_side")
         compute()
     for t in used:
         t.record_stream(side)
@@ -704,6 +715,7 @@ class _SideBranch:
                 t.record_stream(self.side)
             self.ctx = torch.cuda.stream(self.side)
             self.ctx.__enter__()
+            inject_delay("side_branch")
         return self
 
     def __exit__(self, *exc):
@@ -739,6 +751,38 @@ def persistent(t):
         ev.record(cur)
         _CONST_FILL[id(t)] = (ev, {cur})
     return t
+
+
+def persistent_full(like, *fills):
+    """persistent() constants [n] filled with `value` for each (n, value) in `fills`, all covered by
+    one event recorded after the last fill."""
+    ts = [torch.empty(n, device=like.device, dtype=torch.float32) for n, _ in fills]
+    inject_delay("persistent")
+    for t, (_, v) in zip(ts, fills):
+        if t.is_cuda:
+            lib.vst_fill(ptr(t), t.numel(), float(v), stream())
+        else:
+            t.fill_(v)
+    if like.is_cuda:
+        cur = torch.cuda.current_stream(like.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        for t in ts:
+            _CONST_FILL[id(t)] = (ev, {cur})
+    return ts
+
+
+# Test hooks (tests/test_gpu_streams.py): {placement: iterations} -> vst_test_delay(iterations) is
+# enqueued on the current stream at that cross-stream hand-off ("side_branch": head of the input-only
+# side branch; "wgrad_side": head of each side-stream weight gradient; "pack": before each weight pack
+# kernel; "persistent": before the fill of each lazily created constant).  Empty in normal runs.
+TEST_DELAY = {}
+
+
+def inject_delay(place):
+    it = TEST_DELAY.get(place)
+    if it:
+        lib.vst_test_delay(int(it), stream())
 
 
 def constant(t):
@@ -1159,6 +1203,103 @@ class MSEFn(Function):
 
 def mse(a, b, weight=1.0):
     return MSEFn.apply(a, b, weight)
+
+
+def sum_into(out, parts):
+    """out = sum of `parts` (same-shape contiguous tensors; None skipped; zeros when none) with
+    vst_sum4, four addends per pass, left to right."""
+    parts = [p.contiguous() for p in parts if p is not None]
+    n = out.numel()
+    if not parts:
+        lib.vst_fill(ptr(out), n, 0.0, stream())
+        return out
+    src = parts[:4]
+    lib.vst_sum4(*[ptr(p) for p in src + [None] * (4 - len(src))], ptr(out), n, stream())
+    for i in range(4, len(parts), 3):
+        src = parts[i:i + 3]
+        lib.vst_sum4(ptr(out), *[ptr(p) for p in src + [None] * (3 - len(src))], ptr(out), n, stream())
+    return out
+
+
+class ForkFn(Function):
+    """A tensor read by several ops (the gradient sums of RC/network.py:136-150's residual skip, the
+    ReCoNet feature map read by deconv1 and the feature temporal loss, the stylised frame read by the
+    VGG pass, the output temporal loss and TV, train_candy.py:91-145; the AdaAttN loss features read
+    by two or three loss terms, AA/train_video.py:103-118): `n` aliases of x plus, with B > 0,
+    `h1` aliases of its batch half x[:B] and `h2` of x[B:] -- each a separate autograd output, so
+    backward receives every consumer's gradient on its own and sums them in one vst_sum4 pass per
+    batch half.  Autograd would add them two at a time with ATen kernels, and each slice's backward
+    would zero-fill and copy a full-size tensor."""
+
+    @staticmethod
+    def forward(ctx, x, n, B, h1, h2):
+        ctx.n, ctx.B, ctx.h, ctx.shape = n, B, (h1, h2), x.shape
+        outs = [x.view_as(x) for _ in range(n)]
+        if B:
+            outs += [x[:B].view_as(x[:B]) for _ in range(h1)] + [x[B:].view_as(x[B:]) for _ in range(h2)]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        n, B, (h1, h2) = ctx.n, ctx.B, ctx.h
+        full = gs[:n]
+        like = next(g for g in gs if g is not None)
+        gx = _empty(ctx.shape, like)
+        if not B:
+            sum_into(gx, full)
+        else:
+            parts = (gs[n:n + h1], gs[n + h1:n + h1 + h2])
+            for h, sl in enumerate((slice(0, B), slice(B, ctx.shape[0]))):
+                sum_into(gx[sl], [None if g is None else g[sl] for g in full] + list(parts[h]))
+        return gx, None, None, None, None
+
+
+FORK = os.environ.get("VST_FORK", "1") != "0"  # A/B: autograd's own gradient sums and scalar adds
+
+
+def fork(x, n, B=0, halves=(1, 1)):
+    """(x as `n` separate autograd outputs [, halves[0] x x[:B], halves[1] x x[B:]]) -- see ForkFn;
+    plain views when no gradient is recorded (and for host tensors: the CPU data-parallel tests run
+    the module structure over oracle layers, and autograd sums there)."""
+    h1, h2 = halves if B else (0, 0)
+    if not (FORK and torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
+        return tuple([x] * n + [x[:B]] * h1 + [x[B:]] * h2)
+    return ForkFn.apply(x, n, B, h1, h2)
+
+
+class SumScalarsFn(Function):
+    """Sum of 0-d loss terms (train_candy.py:148, the style term's layer sum :132-138, AA/train_video.py
+    :118) in vst_sum4 passes instead of one ATen add per term; backward hands the incoming gradient to
+    every term."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        ctx.k = len(ts)
+        out = _empty((), ts[0])
+        return sum_into(out, list(ts))
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g,) * ctx.k
+
+
+def sum_scalars(*ts):
+    ts = [t for t in ts if t is not None]
+    if not FORK:
+        return sum(ts[1:], ts[0])
+    return ts[0] if len(ts) == 1 else SumScalarsFn.apply(*ts)
+
+
+_SEED = {}
+
+
+def backward_seed(like):
+    """A cached 0-d 1.0 on like's device: the seed of loss.backward() without the fill kernel
+    torch.ones_like would launch every step (persistent: created once, read by autograd only)."""
+    t = _SEED.get(like.device)
+    if t is None:
+        t = _SEED[like.device] = persistent_full(like, (1, 1.0))[0]
+    return constant(t).view(())
 
 
 class MaskedTemporalFn(Function):

@@ -10,6 +10,8 @@ batch, AA/train_video.py:121-122): a device-resident dynamic loss scale with
 torch.cuda.amp.GradScaler's rule (skip the step and halve the scale on an Inf / NaN gradient, double
 it after `growth_interval` clean steps), applied by `vst_adam_loss_scaled` without a host sync.
 """
+import warnings
+
 import torch
 from torch.autograd.graph import increment_version
 
@@ -39,7 +41,10 @@ class FlatParams:
         self.numel = n
 
     def zero_grad(self):
-        self.g.zero_()
+        if self.g.is_cuda:
+            lib.vst_fill(ptr(self.g), self.numel, 0.0, stream())
+        else:  # (the CPU data-parallel tests' host stand-in of the flat buffers)
+            self.g.zero_()
         for prm, (off, k) in zip(self.params, self._spans()):
             if prm.grad is None or prm.grad.data_ptr() != self.g[off:off + k].data_ptr():
                 prm.grad = self.g[off:off + k].view_as(prm)
@@ -134,6 +139,14 @@ def load_train_state(trainer, sd):
     trainer.flat.m.copy_(sd["adam_m"])
     trainer.flat.v.copy_(sd["adam_v"])
     if sd.get("scaler") is not None:
+        from .. import ops  # (ops imports this module's siblings)
+
+        if ops.loss_scale() == 1.0:
+            # a loss-scaled (fp16) checkpoint resumed under an unscaled policy: the scaler, once
+            # created, would stay in use and run loss-scaled Adam with skip-on-overflow there
+            warnings.warn("train state holds a loss scaler but the current GEMM policy has no loss scale: "
+                          "its state is ignored")
+            return
         if trainer.scaler is None:
             trainer.scaler = LossScaler(trainer.flat.p.device)
         trainer.scaler.load_state_dict(sd["scaler"])
@@ -153,7 +166,7 @@ def backward_and_adam(trainer, loss):
         trainer.scaler = LossScaler(loss.device, init_scale=s, step=trainer.step_count)
     trainer.step_count += 1
     if trainer.scaler is None:
-        loss.backward()
+        loss.backward(ops.backward_seed(loss) if loss.is_cuda else None)
         trainer.flat.adam(trainer.step_count, trainer.lr, trainer.betas, trainer.eps, trainer.dp.finish())
         return
     loss.backward(trainer.scaler.seed)

@@ -228,11 +228,13 @@ class ResidualBlock(nn.Module):
     def forward(self, x):
         c1, c2 = self.conv1.conv2d, self.conv2.conv2d
         p1, p2 = self.conv1.reflection_padding, self.conv2.reflection_padding
+        # x feeds conv1 and the skip: their gradients meet in one vst_sum4 pass (ops.fork)
+        xc, xs = ops.fork(x, 2)
         with ops.gemm_scope("res"):
-            out = ops.conv_instance_norm(x, c1.weight, c1.bias, self.in1.weight, self.in1.bias, c1.stride[0], p1,
+            out = ops.conv_instance_norm(xc, c1.weight, c1.bias, self.in1.weight, self.in1.bias, c1.stride[0], p1,
                                          relu=True, eps=self.in1.eps)
             return ops.conv_instance_norm(out, c2.weight, c2.bias, self.in2.weight, self.in2.bias, c2.stride[0], p2,
-                                          relu=False, res=x, eps=self.in2.eps)
+                                          relu=False, res=xs, eps=self.in2.eps)
 
 
 class ReCoNet(nn.Module):
@@ -265,7 +267,7 @@ class ReCoNet(nn.Module):
         x = self.res3(x)
         x = self.res4(x)
         x = self.res5(x)
-        features = x
+        x, features = ops.fork(x, 2)  # read by deconv1 and by the caller's feature temporal loss
         x = self.deconv1(x)
         sd1 = x
         x = self.deconv2(x)
@@ -304,7 +306,7 @@ class ReCoNetSD1(nn.Module):
         x = self.res3_sd(x)
         x = self.res4_sd(x)
         x = self.res5_sd(x)
-        features = x
+        x, features = ops.fork(x, 2)
         x = self.deconv1_sd(x)
         sd = x
         x = self.deconv2(x)
@@ -343,7 +345,7 @@ class ReCoNetSD2(nn.Module):
         x = self.res3_sd(x)
         x = self.res4_sd(x)
         x = self.res5_sd(x)
-        features = x
+        x, features = ops.fork(x, 2)
         x = self.deconv1_sd2(x)
         x = self.deconv2_sd2(x)
         x = self.deconv3_sd2(x)

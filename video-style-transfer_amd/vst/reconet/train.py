@@ -133,31 +133,31 @@ class ReCoNetTrainer:
         mout = self.model(x)
         fmap, styled = mout[-2], mout[-1]
         s_n = ops.VggNormalizeFn.apply(styled)
-        sf = self.vgg(s_n)
+        # the normalised stylised frames are read by the VGG pass, TV and (per frame) the output
+        # temporal loss: one autograd output per consumer, their gradients summed in one pass
+        s_vgg, s_tv, s_1, s_2 = ops.fork(s_n, 2, B) if nf == 2 else ops.fork(s_n, 2) + (None, None)
+        sf = list(self.vgg(s_vgg))
+        # relu3_3 feeds the content loss and its Gram matrix
+        sf[2], f3_content = ops.fork(sf[2], 2)
         side.join()
         out = {}
         if "FTL" in self.terms:
             Hf, Wf = fmap.shape[2:]
+            f_1, f_2 = ops.fork(fmap, 0, B)
             fflow = ops.resize_bilinear(flow, (Hf, Wf), chscale=self._chscale(Hf, Wf, H, W, flow.device))
-            warped_f = ops.warp(fmap[:B], fflow)
+            warped_f = ops.warp(f_1, fflow)
             fmask = ops.resize_bilinear(mask.unsqueeze(1), (Hf, Wf), binarize=True)
-            out["FTL"] = ops.feature_temporal_loss(fmap[B:], warped_f, fmask, w["LAMBDA_F"])
+            out["FTL"] = ops.feature_temporal_loss(f_2, warped_f, fmask, w["LAMBDA_F"])
         if "OTL" in self.terms:
-            warped_s = ops.warp(s_n[:B], flow)
-            out["OTL"] = ops.output_temporal_loss(s_n[B:], warped_s, i_n[B:], warped_i, mask, w["LAMBDA_O"])
+            warped_s = ops.warp(s_1, flow)
+            out["OTL"] = ops.output_temporal_loss(s_2, warped_s, i_n[B:], warped_i, mask, w["LAMBDA_O"])
         # mean over the nf*B batch x nf = the reference's sum of nf per-frame means
-        out["CL"] = ops.mse(sf[2], cf[2], nf * w["ALPHA"])
-        sl = None
-        for f, gs in zip(sf, self.style_grams):
-            term = ops.mse(ops.gram_matrix(f), gs, nf * w["BETA"])
-            sl = term if sl is None else sl + term
-        out["SL"] = sl
+        out["CL"] = ops.mse(f3_content, cf[2], nf * w["ALPHA"])
+        out["SL"] = ops.sum_scalars(*[ops.mse(ops.gram_matrix(f), gs, nf * w["BETA"])
+                                      for f, gs in zip(sf, self.style_grams)])
         if "RL" in self.terms:
-            out["RL"] = ops.tv_loss(s_n, w["GAMMA"])
-        total = None
-        for k in self.terms:
-            total = out[k] if total is None else total + out[k]
-        out["loss"] = total
+            out["RL"] = ops.tv_loss(s_tv, w["GAMMA"])
+        out["loss"] = ops.sum_scalars(*[out[k] for k in self.terms])
         if self.teacher is not None:
             ti, si = self.sd_index
             with torch.no_grad():
