@@ -673,8 +673,9 @@ def test_f16_step_order_insensitive(size):
 def test_train_video_f16_512x1024(golden):
     """Config 5's frame size (512x1024, B = 1; Ns = 32,768 style positions at relu3_1, where the
     linear-form attention's E2 - M^2 cancels hardest): the f16 step's loss terms against the oracle's
-    fp32 forward (tests/golden/aa_f16_512.npz, gen_oracle_f16_512.py) and each attention level's M / S
-    against the float64 exact moments of the same Q, K, V (bars as the mid-size test's)."""
+    fp32 forward (tests/golden/aa_f16_512.npz, gen_oracle_f16_512.py), its gradient against the oracle's
+    fp32 backward (per-tensor norms at the fp32-class bar, seeded samples), and each attention level's
+    M / S against the float64 exact moments of the same Q, K, V (bars as the mid-size test's)."""
     import bench
     from vst import ops
     from vst.adaattn.train import AdaAttNTrainer
@@ -689,14 +690,33 @@ def test_train_video_f16_512x1024(golden):
     try:
         model, vgg = _mid_models(int(s["seeds"][0]), int(s["seeds"][1]))
         tr = AdaAttNTrainer(model, vgg, activation="cosine")
-        with torch.no_grad():
-            out = tr.losses(torch.stack([G(c1), G(c2), G(st)]))
+        tr.flat.zero_grad()
+        out = tr.losses(torch.stack([G(c1), G(c2), G(st)]))
         lerr = {k: rel_err(out[k].item(), float(s[k])) for k in ("loss", "loss_gs", "loss_lf", "loss_is")}
+        unscale = tr.backward(out["loss"])
+        torch.cuda.synchronize()
+        g = {n: p.grad.detach().double().cpu().reshape(-1) * unscale for n, p in model.named_parameters()}
+        del out
         levels = bench.adaattn_level_parity(model, vgg, G(c1), G(st), ref_form=False)
     finally:
         ops.use_policy(old if old in ops.POLICIES else ops.DEFAULT_POLICY)
     print(f"f16 512x1024: loss rel err {lerr}")
     assert max(lerr.values()) <= LOSS_TOL["f16"], lerr
+    # the backward (AA/train_video.py:121) at the full frame size against the oracle's fp32 gradient:
+    # every tensor's norm within the fp32-class golden bar of bench.full_size_parity_adaattn
+    # (1e-3 of its own norm + 1e-4 of the largest), and the 256 seeded samples per tensor
+    names = [str(n) for n in s["grad_names"]]
+    assert sorted(names) == sorted(g)
+    gn = {n: float(s[f"gnorm:{n}"]) for n in names}
+    gmax = max(gn.values())
+    margin = {n: abs(float(g[n].norm()) - gn[n]) / (1e-3 * gn[n] + 1e-4 * gmax) for n in names}
+    a = torch.cat([g[n][torch.from_numpy(s[f"gidx:{n}"])] / gn[n] for n in names])
+    b = torch.cat([torch.from_numpy(s[f"gval:{n}"]) / gn[n] for n in names])
+    cos = float(a @ b / (a.norm() * b.norm()))
+    worst = max(margin, key=margin.get)
+    print(f"f16 512x1024 backward: worst norm margin {margin[worst]:.3f} ({worst}), sampled cosine {cos:.6f}")
+    assert margin[worst] <= 1.0, (worst, margin[worst])
+    assert cos >= 0.999, cos
     assert levels[0]["Ns"] == 32768
     for e in levels:
         print(f"f16 512x1024 {e['level']} Nc={e['Nc']} Ns={e['Ns']}: M {e['hip']['M']['max']:.3e} "
