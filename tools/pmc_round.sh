@@ -1,7 +1,7 @@
 #!/bin/bash
 # counter passes (one per run, --kernel-trace only, each under its own time limit) over bench.py's
 # timed steps: FETCH_SIZE / WRITE_SIZE (HBM traffic, tools/pmc_traffic.py) and two SQ/GRBM sets
-# (MFMA busy and instruction mix, tools/pmc_busy.py).  usage: pmc_r04.sh <tag> [traffic|busy|both]
+# (MFMA busy and instruction mix, tools/pmc_busy.py).  usage: pmc_round.sh <model tag> [traffic|busy|both]
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 model=${1:-reconet}
