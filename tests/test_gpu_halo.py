@@ -407,3 +407,39 @@ def test_halo91_kwu_padout_dgrad_bitwise(mode, shape):
     F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w.double()).backward(dy.double())
     err = float((res[0].double() - x.grad).abs().max() / x.grad.abs().max())
     assert err < TOL[mode], err
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 48, 24, 64, 3), (1, 32, 13, 40, 3), (1, 16, 37, 96, 3)])
+def test_halo19_rowsplit_forward_bitwise(mode, shape):
+    """ConvTanh's forward (48 -> 3 channels, 9x9 reflect pad 4, RC/network.py:78-85) as the row-split
+    GEMM: rows (co, kh) = 27 of a 32-row pack, a 1 x 9 conv over the reflect-padded rows (output
+    (H + 8) x W).  The halo kernel's 1 x 9 form (32-row block, 16 output rows per tile, ragged rows and
+    columns) against the per-tap kernel (bitwise, unsplit) and float64 (F.conv2d over the padded frame
+    with the (co, kh) rows as output channels)."""
+    N, Cin, H, W, Cout = shape
+    K, pad = 9, 4
+    x = _rand(N, Cin, H, W, seed=80, scale=3.0)
+    w = _rand(Cout, Cin, K, K, seed=81, scale=0.02)
+    st = torch.cuda.current_stream().cuda_stream
+    M, Hq = Cout * K, H + K - 1
+    Mpad, Kpad = _dims(M, K * Cin)
+    res = []
+    for mm in (mode | KBLOCK | NOSPLIT, mode | KBLOCK | PERTAP, mode | KBLOCK):
+        n = Mpad * Kpad * 3 // 2 if (mm & 7) == BF16X6 else Mpad * Kpad
+        wp = torch.empty(n, device=DEV)
+        assert lib.vst_pack_weight(w.data_ptr(), wp.data_ptr(), Cout, Cin, K, K, 0, 1, Mpad, Kpad, mm, st) == 0
+        nb = lib.vst_conv_splitk_workspace(N, Cin, M, Hq, W, 1, K, GM_REFLECT, 1, pad, pad, 1, 0, 0, mm)
+        wsb = torch.empty((nb + 3) // 4, device=DEV) if nb else None
+        out = torch.full((N, M, Hq, W), float("nan"), device=DEV)
+        assert lib.vst_conv_gemm_padx(x.data_ptr(), wp.data_ptr(), None, None, out.data_ptr(), N, Cin, H, W, M, K * Cin,
+                                      Hq, W, 1, K, GM_REFLECT, 1, pad, pad, 1, 0, 0, None, None,
+                                      None if wsb is None else wsb.data_ptr(), nb, mm, st) == 0
+        res.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+    w2 = w.double().permute(0, 2, 1, 3).reshape(M, Cin, 1, K)  # row (co, kh), taps (0, kw)
+    y = F.conv2d(F.pad(x.double(), (pad,) * 4, mode="reflect"), w2)
+    for r in (res[0], res[2]):  # unsplit and (where the grid is small) split-K
+        err = float((r.double() - y).abs().max() / y.abs().max())
+        assert err < TOL[mode], err

@@ -1,4 +1,5 @@
-"""MFMA-busy / stall summary per kernel family from the SQ / GRBM passes of tools/pmc_busy_r02.sh.
+"""MFMA-busy / stall summary per kernel family (and per GEMM instantiation) from the SQ / GRBM passes of
+tools/pmc_round.sh.
 
 Per family, over the dispatches after bench.py's vst_marker_kernel (the timed steps):
   mfma_busy      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dispatch cycles), dispatch cycles =
@@ -40,17 +41,21 @@ def fam(name):
     return n
 
 
+def short(name):
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").replace("vstk::", "").split("(")[0]
+
+
 def main():
     args = sys.argv[1:]
     model = args[0] if args else "reconet"
     p1, p2 = load(model, 1), load(model, 2)
     out = {"model": model, "method": "rocprofv3 --pmc (two passes, --kernel-trace only) of bench.py --steps 2 --warmup 2 "
                                      "--prof-steps 0, dispatches after bench.py's vst_marker_kernel", "families": {}}
-    for f in FAMILIES:
+    def summary(match):
         a = collections.defaultdict(float)
         n = 0
         for d, r in p1.items():
-            if fam(r["_name"]) != f:
+            if not match(r["_name"]):
                 continue
             n += 1
             for k, v in r.items():
@@ -58,18 +63,18 @@ def main():
                     a[k] += v
             a["_ns"] += r["_ns"]
         for d, r in p2.items():
-            if fam(r["_name"]) != f:
+            if not match(r["_name"]):
                 continue
             for k, v in r.items():
                 if not k.startswith("_"):
                     a[k] += v
         if not n:
-            continue
+            return None
         cyc = a["GRBM_GUI_ACTIVE"] / 8
         wc = a["SQ_WAVE_CYCLES"]
         mf = max(a["SQ_INSTS_MFMA"], 1.0)  # (the reduce kernels issue no MFMA: their ratios are per instruction)
-        out["families"][f] = {
-            "launches": n,
+        return {
+            "launches": n, "ms": a["_ns"] / 1e6,
             "mfma_busy": a["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc),
             "clock_ghz": cyc / a["_ns"],
             "wait_any": a["SQ_WAIT_ANY"] / wc, "wait_inst": a["SQ_WAIT_INST_ANY"] / wc, "active": a["SQ_ACTIVE_INST_ANY"] / wc,
@@ -77,7 +82,22 @@ def main():
             "vmem_rd_per_mfma": a["SQ_INSTS_VMEM_RD"] / mf, "salu_per_mfma": a["SQ_INSTS_SALU"] / mf,
             "lds_conflict_cycles_per_lds_inst": a["SQ_LDS_BANK_CONFLICT"] / max(a["SQ_INSTS_LDS"], 1.0),
         }
-        print(f, {k: round(v, 3) for k, v in out["families"][f].items()})
+
+    for f in FAMILIES:
+        res = summary(lambda name, f=f: fam(name) == f)
+        if res is None:
+            continue
+        out["families"][f] = res
+        print(f, {k: round(v, 3) for k, v in res.items()})
+    # the GEMM instantiations (template arguments) one by one, largest total time first
+    names = collections.Counter()
+    for r in p1.values():
+        if fam(r["_name"]) in FAMILIES:
+            names[short(r["_name"])] += r["_ns"]
+    out["kernels"] = {}
+    for nm, _ in names.most_common(16):
+        out["kernels"][nm] = summary(lambda name, nm=nm: short(name) == nm)
+        print(" ", nm, {k: round(v, 3) for k, v in out["kernels"][nm].items()})
     if len(args) > 1:
         json.dump(out, open(args[1], "w"), indent=1)
 

@@ -362,16 +362,20 @@ static HaloPlan halo_plan(int N, int Cs, int M, int Ho, int Wo, int KH, int KW, 
   // 9 x 1 over a kw-unfolded operand (column pad 0): the 64- / 128-row block selections only
   const bool k91 = !ph2 && KH == 9 && KW == 1 && pad_x == 0 && gmask_free && (hcfg == HALO_M64 || hcfg == HALO_M128) &&
                    (gmode == GM_REFLECT || gmode == GM_TRANSPOSED);
+  // 1 x 9 over the reflect-padded rows (ConvTanh's row-split forward: 27 rows in a 32-row pack)
+  const bool k19 = !ph2 && KH == 1 && KW == 9 && pad_x == pad && gmask_free && hp.mpad == 32 && gmode == GM_REFLECT &&
+                   epi == 0;
+  const int hcfg19 = k19 ? H1x4S : hcfg;
   const bool taps_ok = ph2 ? (KH == 2 && KW == 2 && (gmode == GM_TRANSPOSED || gmode == GM_CLAMP) && gmask_free)
-                       : k91 ? true
+                       : (k91 || k19) ? true
                              : (KH == 3 && KW == 3 && (gmode == GM_REFLECT || gmode == GM_ZERO || gmode == GM_TRANSPOSED));
-  const bool halo = hcfg && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
+  const bool halo = hcfg19 && !(mode & VST_GEMM_PERTAP) && (mode & VST_GEMM_KBLOCK) && taps_ok &&
                     stride == 1 && up == 1 && Cs % 16 == 0 && (pad_x == pad || k91) && a_batch_stride == 0 &&
                     !(epi & EPI_AFFINE) &&
                     (am == VST_GEMM_BF16X6 || am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16);
   if (!halo) return hp;
-  hp.hcfg = hcfg;
-  const int bm = 32 * halo_wm(hcfg), th = 4 * halo_wn(hcfg);
+  hp.hcfg = hcfg19;
+  const int bm = 32 * halo_wm(hcfg19), th = 4 * halo_wn(hcfg19);
   hp.tiles = ((Wo + HTW - 1) / HTW) * ((Ho + th - 1) / th);
   // split-K when the grid is too small for the chip (AdaAttN config 4's decoder and VGG19 conv4 /
   // conv5 layers: 128-384 blocks); every split launch matches its unsplit launch to <= 3e-6

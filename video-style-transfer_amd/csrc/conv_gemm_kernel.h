@@ -221,6 +221,16 @@ __device__ __forceinline__ int a_slot2(int idx) {
   return row * 2 + quad;
 }
 
+// bf16x6 A slots (six float4 per 96-B packed row, LDS rows 28 dwords apart): slot = row*6 + six with
+// 8 consecutive lanes on 8 consecutive rows of one float4 column (28 r mod 32 = 0, 28, 24, .., 4:
+// distinct 4-bank groups per 8-lane ds_write_b128).  The plain row-major order (idx / 6, idx % 6) put
+// lane 7 of each group back on lane 0's banks (profiles/r06_mfma_busy_reconet.json: 1.6 conflict
+// cycles per LDS instruction on the 192-row LDS-A tile).  A wave still loads whole 768-B runs of rows.
+__device__ __forceinline__ int a_slot6(int idx) {
+  const int row = (idx & 7) | ((idx / 48) << 3), six = (idx >> 3) % 6;
+  return row * 6 + six;
+}
+
 // ADIR (bf16x6 only): the packed weights go straight from memory into each wave's MFMA A operand
 // registers (one buffer_load_b128 per 32-row fragment and piece, next tile prefetched a k-step
 // ahead) instead of through LDS: no A stores to LDS (the stores were the largest non-MFMA cost of
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
     const int idx = tid + i * NT;
     a_voff[i] = (A_F4 % NT == 0 || idx < A_F4)
                     ? (AWL == 8 ? (a_slot2(idx) >> 1) * AW * 4 + (a_slot2(idx) & 1) * 16
-                                : 16 * (AW == 16 ? a_slot(idx) : idx))
+                                : 16 * (AW == 16 ? a_slot(idx) : a_slot6(idx)))
                     : OOR;
   }
   // A-direct: lane (r, h) of fragment i, piece p reads the 16 B at dword 8p + 4h of packed row
@@ -435,7 +445,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_kernel(ConvParam
           const int sl = a_slot(idx);
           *reinterpret_cast<f32x4*>(&Asb[sl >> 2][(sl & 3) * 4]) = ra[i];
         } else {
-          *reinterpret_cast<f32x4*>(&Asb[idx / 6][(idx % 6) * 4]) = ra[i];
+          const int sl = a_slot6(idx);
+          *reinterpret_cast<f32x4*>(&Asb[sl / 6][(sl % 6) * 4]) = ra[i];
         }
       }
     }

@@ -79,11 +79,14 @@ __device__ __forceinline__ void halo_tap(f32x16 (&acc)[1][TN], const bf16x8_t (&
 // KH x KW taps: 3 x 3 (the 3x3 stride-1 convs); 2 x 2 (the phase-stacked GEMMs of the stride-2 data
 // gradient and the nearest-x2 upsample forward, EPI_PHASE2 -- patch (TH + 1) x 33, four taps); 9 x 1
 // (the 9x9 layers over a kw-unfolded operand: ReCoNet conv1's forward and ConvTanh's data gradient,
-// RC/network.py:78-85,158 -- patch (TH + 8) x 32, nine row taps, column pad P.pad_x = 0).
+// RC/network.py:78-85,158 -- patch (TH + 8) x 32, nine row taps, column pad P.pad_x = 0); 1 x 9
+// (ConvTanh's row-split forward, RC/network.py:78-85: GEMM rows (co, kh), nine column taps over the
+// reflect-padded rows -- patch TH x 40, on the 32-row block H1x4S).
 template <int WM, int WN, int MINW, int PREC, bool GM, bool DB, int PD = 1, int KH = 3, int KW = KH>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParams P) {
   static_assert(PREC >= 1 && PREC <= 4, "halo kernel: bf16x3, bf16x6, bf16 or fp16 products");
-  static_assert((KH == KW && (KH == 2 || KH == 3)) || (KH == 9 && KW == 1), "halo kernel: 2x2, 3x3 or 9x1 taps");
+  static_assert((KH == KW && (KH == 2 || KH == 3)) || (KH == 9 && KW == 1) || (KH == 1 && KW == 9),
+                "halo kernel: 2x2, 3x3, 9x1 or 1x9 taps");
   constexpr int TM = 1, TN = 4, NTAP = KH * KW;
   constexpr int TH = 4 * WN, HPH = TH + KH - 1, HPW = HTW + KW - 1, HPP = HPH * HPW;
   constexpr int NTT = WM * WN * 64;
@@ -299,11 +302,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 // block shape of 64-, 128-, 192-row and 256-multiple layers (HaloCfg below)
 constexpr int HALO_M64 = 3, HALO_M128 = 4, HALO_M192 = 3, HALO_M256 = 8;
 // WM x WN waves (S: one patch buffer)
-enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S, H4x2S };
-constexpr int halo_wm_c(int c) { return c == H2x1 || c == H2x2 || c == H2x2S || c == H2x4S ? 2
+enum HaloCfg { H2x1 = 1, H2x2, H2x2S, H4x1, H4x2, H6x1, H3x2, H8x1, H2x4S, H3x1S, H3x2S, H4x2S, H1x4S };
+constexpr int halo_wm_c(int c) { return c == H1x4S ? 1 : c == H2x1 || c == H2x2 || c == H2x2S || c == H2x4S ? 2
                                       : c == H4x1 || c == H4x2 || c == H4x2S ? 4 : c == H6x1 ? 6 : c == H8x1 ? 8 : 3; }
-constexpr int halo_wn_c(int c) { return c == H2x4S ? 4 : (c == H2x2 || c == H2x2S || c == H4x2 || c == H3x2 || c == H3x2S || c == H4x2S) ? 2 : 1; }
-constexpr bool halo_db_c(int c) { return !(c == H2x2S || c == H2x4S || c == H3x1S || c == H3x2S || c == H4x2S); }
+constexpr int halo_wn_c(int c) { return c == H2x4S || c == H1x4S ? 4 : (c == H2x2 || c == H2x2S || c == H4x2 || c == H3x2 || c == H3x2S || c == H4x2S) ? 2 : 1; }
+constexpr bool halo_db_c(int c) { return !(c == H2x2S || c == H2x4S || c == H3x1S || c == H3x2S || c == H4x2S || c == H1x4S); }
 inline int halo_wm(int c) { return halo_wm_c(c); }
 inline int halo_wn(int c) { return halo_wn_c(c); }
 // 0: the per-tap kernel (the M tile would not divide the pack's Mpad).  (The bf16x6 residual data
@@ -364,10 +367,18 @@ void launch_halo91(int c, dim3 grid, hipStream_t st, const ConvParams& P) {
   else launch_halo_c<HALO_M128, PR, false, 9, 1>(grid, st, P);
 }
 
+// the 1 x 9 GEMM of the row-split forward (27 weight rows (co, kh) in a 32-row pack): one 32-row wave
+// column, four wave rows (16 output rows per tile), one patch buffer
+template <int PR>
+void launch_halo19(dim3 grid, hipStream_t st, const ConvParams& P) {
+  launch_halo_c<H1x4S, PR, false, 1, 9>(grid, st, P);
+}
+
 template <int PR>
 void launch_halo_prec(bool gm, int c, int kh, dim3 grid, hipStream_t st, const ConvParams& P) {
   if (kh == 2) launch_halo2<PR>(c, grid, st, P);
   else if (kh == 9) launch_halo91<PR>(c, grid, st, P);
+  else if (kh == 1) launch_halo19<PR>(grid, st, P);
   else gm ? launch_halo<PR, true>(c, grid, st, P) : launch_halo<PR, false>(c, grid, st, P);
 }
 

@@ -595,10 +595,17 @@ def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
         GEMM_MODES["bf16x6"], GEMM_MODES["bf16"], GEMM_MODES["f16"]))
 
 
+KBLOCK_RS = KBLOCK_ON and os.environ.get("VST_KBLOCK_RS", "1") != "0"  # A/B: the row-split forward blocked
+
+
 def conv_fwd_rowsplit(x, w, b, epi, aux):
     N, Cin, H, W = x.shape
     Cout, _, K, _ = w.shape
     Hq = H + K - 1
+    # the 1 x K GEMM in the channel-blocked K order: the halo kernel's 1 x 9 form (the source rows
+    # staged once per 16-channel block for the nine column taps)
+    if KBLOCK_RS and Cin % 16 == 0:
+        _CUR[0] |= KBLOCK
     P = conv_gemm(x, packed_weight(w, False, split_kh=True), Cout * K, K, Hq, W, GM_REFLECT, 1, K // 2, 1, kh=1,
                   algo_flops=2.0 * N * Cout * H * W * Cin * K * K)
     out = _empty((N, Cout, H, W), x)
