@@ -55,7 +55,7 @@ def global_stylized_loss(fcs, fs, loss_fn=None, weight=1.0):
     mcs, scs = plane_mean_std(fcs)
     with torch.no_grad():
         ms, ss = plane_mean_std(fs)
-    return _apply_loss(loss_fn, mcs, ms, weight) + _apply_loss(loss_fn, scs, ss, weight)
+    return ops.sum_scalars(_apply_loss(loss_fn, mcs, ms, weight), _apply_loss(loss_fn, scs, ss, weight))
 
 
 def local_feature_loss(fcs, adaattn, loss_fn=None, weight=1.0):

@@ -20,15 +20,24 @@ from .._lib import lib, ptr, stream
 SCALER_WS = 1024  # include/vst_hip.h VST_SCALER_WS
 
 
+def _zeros_dev(n, dev):
+    """A zero-filled fp32 buffer: the library's fill kernel on a HIP device (no ATen kernel in a
+    training process), torch.zeros on the host."""
+    t = torch.empty(n, device=dev, dtype=torch.float32)
+    if t.is_cuda:
+        lib.vst_fill(ptr(t), n, 0.0, stream())
+    else:
+        t.zero_()
+    return t
+
+
 class FlatParams:
     def __init__(self, module):
         params = [p for p in module.parameters() if p.requires_grad]
         n = sum(p.numel() for p in params)
         dev = params[0].device
         self.p = torch.empty(n, device=dev, dtype=torch.float32)
-        self.g = torch.zeros(n, device=dev, dtype=torch.float32)
-        self.m = torch.zeros(n, device=dev, dtype=torch.float32)
-        self.v = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.g, self.m, self.v = (_zeros_dev(n, dev) for _ in range(3))
         off = 0
         with torch.no_grad():
             for prm in params:
@@ -86,9 +95,9 @@ class LossScaler:
         if not (init_scale > 0 and growth_factor >= 1.0 and 0 < backoff_factor <= 1.0 and growth_interval > 0):
             raise ValueError("loss scaler: init_scale > 0, growth_factor >= 1, 0 < backoff_factor <= 1, "
                              "growth_interval > 0")
-        self.state = torch.zeros(8, device=device, dtype=torch.float32)
-        self.state[0] = float(init_scale)
-        self.state[2] = float(step)
+        init = torch.zeros(8, dtype=torch.float32)
+        init[0], init[2] = float(init_scale), float(step)
+        self.state = init.to(device)  # (host-built, one copy: no fill kernel on the device)
         self.ws = torch.empty(SCALER_WS, device=device, dtype=torch.float32)
         self.growth, self.backoff, self.interval = float(growth_factor), float(backoff_factor), int(growth_interval)
 
