@@ -693,7 +693,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   }
 }
 
-enum { W32 = 0, W64, W96, W128, W192, W64N, W96N };  // *N: 256-column variants (row-tiled kernel only)
+// *N: 256-column variants, W64H: a 64 x 64 block for J <= 64 (the 64-channel Gram matrices, VGG16
+// relu1_2: the 64 x 128 block spent half its MFMAs and B staging on the padded columns); row-tiled
+// kernel only
+enum { W32 = 0, W64, W96, W128, W192, W64N, W96N, W64H };
 static int wsel(int M) {
   if (M <= 32) return W32;
   if (M <= 64) return W64;
@@ -821,6 +824,7 @@ static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
     case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
     case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
+    case W64H: wgrad2_kernel<1, 2, 2, 1, 4, PR, GMD, KD><<<g, 128, 0, st>>>(P); break;
     default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
   }
 }
@@ -883,7 +887,10 @@ static int run_wg(const float* a, const float* src, float* slab, int N, int M, i
     // the slab layout and the workspace size do not change.
     int cw = c;
     if ((c == W64 || c == W96) && Q.J > WBN && Q.Jpad % (2 * WBN) == 0) cw = c == W64 ? W64N : W96N;
-    dim3 g(Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
+    // J <= 64 on a 64-row tile: one 64 x 64 block per M tile (the slab keeps its 128-column stride;
+    // its columns >= J are never written nor read)
+    if (c == W64 && Q.J <= 64) cw = W64H;
+    dim3 g(cw == W64H ? 1 : Q.Jpad / (cw == c ? WBN : 2 * WBN), Q.Mpad / wbm(c), N * S);
     if (gmode == 0) launch_wg2<0>(cw, g, mode, st, Q);
     else if (gmode == 2) launch_wg2<2>(cw, g, mode, st, Q);
     else launch_wg2<1>(cw, g, mode, st, Q);
