@@ -128,6 +128,13 @@ int vst_conv_dgrad_s2(const float* dy, const float* wpack, const float* gmask, f
 /* mask (optional, dx-shaped): the fold adds only where mask > 0 (the producer's ReLU backward fused
  * into a masked data gradient: the GEMM epilogue already zeroed dx there) */
 int vst_fold_border(const float* border, const float* mask, float* dx, long NC, int H, int W, int pad, void* stream);
+/* data gradient of a 3x3 stride-1 pad-1 conv with 1..4 output channels (the AdaAttN decoder's last conv,
+ * AA/network.py:99), in exact fp32 on the VALU: dx = [mask > 0] * (the interior of the transposed conv
+ * of dy over the padded grid); reflect != 0 adds the padded grid's ring through `border`
+ * ([N][Cin][H+2][W+2], only its ring is written) and vst_fold_border.  w: [Cout][Cin][3][3];
+ * Cin even, W % 4 == 0, W >= 8; mask NULL or dx-shaped. */
+int vst_conv_dgrad_thin(const float* dy, const float* w, const float* mask, float* dx, float* border, int N, int Cout,
+                        int Cin, int H, int W, int reflect, void* stream);
 /* Thin-channel convolutions (RC/network.py:155 conv1 = ConvLayer(3, 48, 9), :169 deconv3 =
  * ConvTanh(48, 3, 9) backward, VGG conv1_1): a tensor with C*K <= Cu channels is kw-unfolded,
  *   out[n][c*K + kw][y][v] = src[n][c][y][v + sgn*kw + off]  (reflect or zero outside; zero channels
@@ -135,9 +142,10 @@ int vst_fold_border(const float* border, const float* mask, float* dx, long NC, 
  * so the conv becomes a Kx1 conv over Cu channels on the 16-channel k-tile path:
  *   forward:  vst_unfold_kw(x, sgn=+1, off=-pad, Wout=W) then vst_conv_gemm_padx(KH=K, KW=1,
  *             pad_x=0) with A from vst_pack_weight_kwu(transposed=0);
- *   dgrad (thin Cout, stride 1): vst_unfold_kw(dy, sgn=-1, off=0, Wout=W+2p, zero) then
+ *   dgrad (thin Cout, stride 1): vst_unfold_kw(dy, sgn=-1, off=0, Wout=Wu, zero) then
  *             vst_conv_dgrad_padout_kwu with A from vst_pack_weight_kwu(transposed=1), then
- *             vst_fold_border. */
+ *             vst_fold_border; Wu = W+2p rounded up to a multiple of 4 (the unfold's float4 rows: the
+ *             AdaAttN decoder's last conv, 1024 + 2 wide at config 5). */
 /* Direct 3x3 conv of a 3-channel image, stride 1, pad 1 (reflect or zero), out = [relu](conv + b) in
  * exact fp32 on the VALU (VGG conv1_1, RC/network.py:17 / AA/vgg19.py:19; b may be NULL).
  * w: [Cout][3][3][3] (PyTorch layout).  The output-write-bound layer skips the unfold + K = 48 GEMM. */
@@ -192,7 +200,9 @@ int vst_fold_reflect(const float* dpad, float* dx, long NC, int Hs, int Ws, int 
  * weight gradient under the split-product modes (bf16x6 / bf16 / fp16): one block owns all nine taps
  * of 32 input channels and walks a 16-column strip down the rows, the source rows in an LDS ring (each
  * loaded and split once instead of nine times).  VST_GEMM_PERTAP in `mode` selects the row-tiled
- * kernel instead (same sums, other fp32 summation order). */
+ * kernel instead (same sums, other fp32 summation order).  Cout <= 4 (the AdaAttN decoder's last conv,
+ * 64 -> 3) with 3x3 stride-1 pad-1, Cin % 4 == 0, Ws % 4 == 0: a VALU kernel in exact fp32 whatever the
+ * mode (each source row loaded once, deterministic slab sums; PERTAP selects the GEMM here too). */
 long vst_wgrad_workspace(int N, int M, int J, int HWo);
 long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
                               int stride, int pad, int up, int mode);

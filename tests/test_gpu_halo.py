@@ -380,21 +380,23 @@ def test_halo91_kwu_forward_bitwise(mode, shape):
 
 
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("shape", [(2, 48, 24, 64, 3), (1, 32, 13, 32, 3)])
+@pytest.mark.parametrize("shape", [(2, 48, 24, 64, 3, 9), (1, 32, 13, 32, 3, 9), (1, 48, 11, 62, 3, 9),
+                                   (2, 64, 12, 32, 3, 3), (1, 64, 9, 30, 3, 3)])
 def test_halo91_kwu_padout_dgrad_bitwise(mode, shape):
-    """ConvTanh's data gradient (48 -> 3 channels, 9x9 reflect pad 4, RC/network.py:78-85): the output
-    gradient kw-unfolded over the padded width, a 9 x 1 transposed GEMM over the padded grid (interior
-    into dx, border into the side buffer, EPI_PADOUT), then vst_fold_border -- halo vs per-tap bitwise,
-    and float64."""
-    N, Cin, H, W, Cout = shape
-    K, pad = 9, 4
+    """ConvTanh's data gradient (48 -> 3 channels, 9x9 reflect pad 4, RC/network.py:78-85) and the
+    AdaAttN decoder's last conv's (64 -> 3, 3x3 reflect pad 1, AA/network.py:99): the output gradient
+    kw-unfolded over the padded width (rows rounded up to 4 wide: 62 + 8 -> 72, 32 + 2 -> 36), a K x 1
+    transposed GEMM over the padded grid (interior into dx, border into the side buffer, EPI_PADOUT),
+    then vst_fold_border -- halo vs per-tap bitwise, and float64."""
+    N, Cin, H, W, Cout, K = shape
+    pad = K // 2
     dy = _rand(N, Cout, H, W, seed=73)
     w = _rand(Cout, Cin, K, K, seed=74, scale=0.02)
     st = torch.cuda.current_stream().cuda_stream
     res = []
     for mm in (mode | KBLOCK, mode | KBLOCK | PERTAP):
         wp, Cu = _pack_kwu(w, mm, True)
-        dyu = _unfold(dy, K, 0, -1, W + 2 * pad, False, Cu)
+        dyu = _unfold(dy, K, 0, -1, (W + 2 * pad + 3) // 4 * 4, False, Cu)
         dx = torch.full((N, Cin, H, W), float("nan"), device=DEV)
         border = torch.zeros(N, Cin, H + 2 * pad, W + 2 * pad, device=DEV)
         assert lib.vst_conv_dgrad_padout_kwu(dyu.data_ptr(), wp.data_ptr(), None, dx.data_ptr(), border.data_ptr(), N,

@@ -119,3 +119,71 @@ def test_halo_wgrad_undersized_workspace_runs_rowtiled():
         with pytest.raises(VstError):
             lib.vst_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), rt_nf - 1, N, Cin, H, W,
                                Cout, H, W, 3, 3, 0, 1, 1, 1, 0, mode, st)
+
+
+# (N, Cin, H, W, Cout): the AdaAttN decoder's last conv (64 -> 3), one-quad-per-lane widths with several
+# row lanes per block (W 12, 32), two column blocks (W 1040), 1 / 2 / 4 output channels, ragged rows
+THIN_SHAPES = [(2, 64, 16, 32, 3), (1, 8, 9, 12, 3), (1, 16, 7, 1040, 3), (1, 4, 5, 8, 1), (2, 12, 37, 16, 4),
+               (3, 64, 10, 64, 2), (1, 64, 130, 256, 3)]
+
+
+@pytest.mark.parametrize("shape", THIN_SHAPES)
+@pytest.mark.parametrize("gmode", [0, 1])
+@pytest.mark.parametrize("mode", [BF16X6, F16])
+def test_thin_wgrad_vs_fp64(shape, gmode, mode):
+    """Cout <= 4 (AA/network.py:99, the decoder's last conv): vst_conv_wgrad runs the fp32 VALU kernel
+    whatever the mode's MFMA arithmetic -- within fp32 summation error of float64, and against the
+    row-tiled GEMM (VST_GEMM_PERTAP) to that GEMM's own product rounding."""
+    N, Cin, H, W, Cout = shape
+    x = _rand(N, Cin, H, W, seed=11, scale=2.0)
+    dy = _rand(N, Cout, H, W, seed=12, scale=0.5)
+    thin = _wgrad(dy, x, Cout, gmode, mode)
+    rowt = _wgrad(dy, x, Cout, gmode, mode | PERTAP)
+    torch.cuda.synchronize()
+    ref = _ref(dy, x, gmode)
+    scale = float(ref.abs().max())
+    err = float((thin.double() - ref).abs().max()) / scale
+    assert err < 2e-6, err
+    assert float((rowt.double() - ref).abs().max()) / scale < TOL[mode]
+
+
+def test_thin_wgrad_accumulate_deterministic_and_workspace():
+    N, Cin, H, W, Cout = 2, 64, 24, 64, 3
+    x = _rand(N, Cin, H, W, seed=13)
+    dy = _rand(N, Cout, H, W, seed=14)
+    base = _rand(Cout, Cin, 3, 3, seed=15)
+    a = _wgrad(dy, x, Cout, 0, F16, out=base.clone())
+    b = _wgrad(dy, x, Cout, 0, F16)
+    c = _wgrad(dy, x, Cout, 0, BF16X6)
+    torch.cuda.synchronize()
+    assert torch.equal(b, c)  # fp32 VALU: the mode does not enter
+    assert torch.equal(a, b + base)  # the reduce adds the slab sum onto dw in one rounding
+    q = lib.vst_conv_wgrad_workspace
+    assert q(N, Cin, H, W, Cout, H, W, 3, 3, 0, 1, 1, 1, F16) != q(N, Cin, H, W, Cout, H, W, 3, 3, 0, 1, 1, 1, F16 | PERTAP)
+
+
+@pytest.mark.parametrize("shape", THIN_SHAPES)
+@pytest.mark.parametrize("reflect", [True, False])
+@pytest.mark.parametrize("masked", [True, False])
+def test_thin_dgrad_vs_fp64(shape, reflect, masked):
+    """Cout <= 4 data gradient (the AdaAttN decoder's last conv under its fused ReLU mask,
+    AA/network.py:99): vst_conv_dgrad_thin -- interior on the VALU, the reflect ring folded by
+    vst_fold_border -- against float64 autograd of the padded conv, masked by x > 0."""
+    from vst._lib import lib as L
+
+    N, Cin, H, W, Cout = shape
+    x = _rand(N, Cin, H, W, seed=21)
+    w = _rand(Cout, Cin, 3, 3, seed=22, scale=0.1)
+    dy = _rand(N, Cout, H, W, seed=23)
+    dx = torch.full_like(x, float("nan"))
+    border = torch.full((N, Cin, H + 2, W + 2), float("nan"), device=DEV) if reflect else None
+    st = torch.cuda.current_stream().cuda_stream
+    assert L.vst_conv_dgrad_thin(dy.data_ptr(), w.data_ptr(), x.data_ptr() if masked else None, dx.data_ptr(),
+                                 border.data_ptr() if reflect else None, N, Cout, Cin, H, W, int(reflect), st) == 0
+    torch.cuda.synchronize()
+    xd = torch.zeros(N, Cin, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
+    xp = torch.nn.functional.pad(xd, (1, 1, 1, 1), mode="reflect" if reflect else "constant")
+    torch.nn.functional.conv2d(xp, w.double()).backward(dy.double())
+    ref = xd.grad * (x > 0).double() if masked else xd.grad
+    err = float((dx.double() - ref).abs().max()) / float(ref.abs().max())
+    assert err < 2e-6, err

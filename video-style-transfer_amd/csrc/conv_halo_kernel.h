@@ -161,19 +161,29 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
 
+  const int nst_all = P.Cs / 16;
+  const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
+  const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
   float rv[TIT][8];
   float rgv[TIT][GM ? 8 : 1];
-  // stage s = channel block s
+  // stage s = channel block s.  The prefetch of the stage after the last one is issued too, with every
+  // offset out of range (the loads return zeros without touching memory): a prefetch under a branch
+  // made the waitcnt pass merge its two paths conservatively -- the first tap's MFMA then waited for
+  // the whole next patch (s_waitcnt vmcnt(1) behind 24 patch loads), so no gather ever overlapped the
+  // taps
   auto load_into = [&](int st, auto& R, auto& G) {
-    const int cb_off = __builtin_amdgcn_readfirstlane(st * 16 * plane * 4);
+    const bool live = st < nst;
+    const int cb_off = __builtin_amdgcn_readfirstlane((live ? st : 0) * 16 * plane * 4);
 #pragma unroll
-    for (int it = 0; it < TIT; ++it)
+    for (int it = 0; it < TIT; ++it) {
+      const int vo = live ? t_voff[it] : OOR;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        R[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, t_voff[it], cb_off + i * cstep, 0));
+        R[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srd, vo, cb_off + i * cstep, 0));
         if constexpr (GM)
-          G[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, t_voff[it], cb_off + i * cstep, 0));
+          G[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(gsrd, vo, cb_off + i * cstep, 0));
       }
+    }
   };
   auto store_from = [&](int buf, auto& R, auto& G) {
 #pragma unroll
@@ -208,38 +218,59 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  const int nst_all = P.Cs / 16;
-  const int st0 = __builtin_amdgcn_readfirstlane(ks * nst_all / P.ksplit);
-  const int nst = __builtin_amdgcn_readfirstlane((ks + 1) * nst_all / P.ksplit);  // (this slice's end)
+  // Single-product modes (one piece per value): the A fragments of ALL taps of a stage are loaded at the
+  // end of the previous stage, ahead of the next patch's loads.  Vector-memory loads complete in issue
+  // order, so a per-tap A load issued after the patch prefetch made the next tap wait for the whole
+  // patch (the prefetch then overlapped one tap of nine); the split-product modes keep the per-tap
+  // A loads (three pieces x nine taps would not fit the registers) and are MFMA-bound.
+  constexpr bool AST = NPC == 1 && !DB;
+  bf16x8_t arS[AST ? NTAP : 1];
+  auto load_stage_a = [&](int cb) {
+    const int c = cb < nst ? cb : 0;  // (past the slice: a harmless reload, unbranched)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) {
+      const int a_soff = __builtin_amdgcn_readfirstlane((((NTAP * c + t) * P.Mpad + m0) * AW) * 4);
+      arS[t] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff, 0));
+    }
+  };
   // the taps of every channel block of stage st, B fragments from patch buffer buf
   auto taps = [&](int cb, int buf) {
 #pragma unroll
     for (int t = 0; t < NTAP; ++t) {
       const int kh = t / KW, kw = t % KW;
       const int ph = tr ? KH - 1 - kh : kh, pw = tr ? KW - 1 - kw : kw;  // (tr is block-uniform)
-      const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : NTAP * (cb + 1);
-      if (t < NTAP - 1 || cb + 1 < nst) load_a(kt_next, arN);
       // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
       // columns lo + pw
       const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
-      halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
+      if constexpr (AST) {
+        const bf16x8_t a1[1][3] = {{arS[t], arS[t], arS[t]}};
+        halo_tap<TN, PREC, LS>(acc, a1, Bt, lane, HPW);
+      } else {
+        // (past the slice's last k-tile: a harmless reload of k-tile 0, unbranched)
+        const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : (cb + 1 < nst ? NTAP * (cb + 1) : 0);
+        load_a(kt_next, arN);
+        halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+        for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+      }
     }
   };
   load_into(st0, rv, rgv);
-  load_a(NTAP * st0, arC);
+  if constexpr (AST) load_stage_a(st0);
+  else load_a(NTAP * st0, arC);
   store_from(0, rv, rgv);
   if constexpr (PD == 1) {
     __syncthreads();
     for (int st = st0; st < nst; ++st) {
       const int buf = DB ? ((st - st0) & 1) : 0;
-      if (st + 1 < nst) load_into(st + 1, rv, rgv);
+      load_into(st + 1, rv, rgv);
+      // (the loads stay ahead of the taps: no code motion across, and the store below is unconditional
+      // -- under `if (st + 1 < nst)` the IR sink pass moved the loads into that branch, after the taps)
+      __builtin_amdgcn_sched_barrier(0);
       taps(st, buf);
-      if (st + 1 < nst) {
-        if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
-        store_from(DB ? buf ^ 1 : 0, rv, rgv);
-      }
+      if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
+      store_from(DB ? buf ^ 1 : 0, rv, rgv);  // (after the last stage: zeros into a buffer nobody reads)
+      if constexpr (AST) load_stage_a(st + 1);
       __syncthreads();
     }
   } else {
@@ -248,19 +279,24 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
     static_assert(PD == 2 && DB, "depth-2 patch prefetch: double-buffered tiles");
     float rvN[TIT][8];
     float rgvN[TIT][GM ? 8 : 1];
-    if (st0 + 1 < nst) load_into(st0 + 1, rv, rgv);
+    load_into(st0 + 1, rv, rgv);
     __syncthreads();
     auto stage = [&](int st, auto& Rs, auto& Gs, auto& Rl, auto& Gl) {
       const int buf = (st - st0) & 1;
-      if (st + 2 < nst) load_into(st + 2, Rl, Gl);
+      load_into(st + 2, Rl, Gl);
+      __builtin_amdgcn_sched_barrier(0);
       taps(st, buf);
-      if (st + 1 < nst) store_from(buf ^ 1, Rs, Gs);
+      store_from(buf ^ 1, Rs, Gs);
+      if constexpr (AST) load_stage_a(st + 1);
       __syncthreads();
     };
-    for (int st = st0; st < nst; st += 2) {
+    // (pairs in the loop, an odd last stage after it: no branch around a stage inside the loop)
+    int st = st0;
+    for (; st + 1 < nst; st += 2) {
       stage(st, rv, rgv, rvN, rgvN);
-      if (st + 1 < nst) stage(st + 1, rvN, rgvN, rv, rgv);
+      stage(st + 1, rvN, rgvN, rv, rgv);
     }
+    if (st < nst) stage(st, rv, rgv, rvN, rgvN);
   }
 
   int pix[TN];
@@ -321,7 +357,11 @@ inline int halo_cfg(int M, int pack_mpad) {
   return pack_mpad % (32 * halo_wm(c)) == 0 ? c : 0;
 }
 
-constexpr int HALO_SMINW_SP = 4;  // waves per SIMD of the single-product one-buffer tiles (3: config 5 142.31 vs 141.5 ms)
+// waves per SIMD of the single-product one-buffer tiles: 3 -- the stage's nine A fragments (36 VGPRs) and
+// the patch prefetch in flight across the taps do not fit 4 waves' 128 VGPRs without spills (round 5,
+// with the prefetch sunk behind the taps by the compiler and per-tap A loads: 3 measured 142.31 vs
+// 141.5 ms at 4)
+constexpr int HALO_SMINW_SP = 3;
 constexpr int HALO_PD = 2;        // patches in flight for the single-product double-buffered tiles
 template <int C, int PR, bool GM, int KH = 3, int KW = KH>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {

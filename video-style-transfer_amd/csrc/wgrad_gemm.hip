@@ -14,6 +14,7 @@
 
 #include "vst_common.h"
 #include "vst_hip.h"
+#include "thin.h"
 #include "wgrad_halo.h"
 
 namespace {
@@ -1082,6 +1083,8 @@ static bool use_wgrad_halo(int Cout, int Cin, int Hs, int Ws, int Ho, int Wo, in
 long vst_conv_wgrad_workspace(int N, int Cin, int Hs, int Ws, int Cout, int Ho, int Wo, int KH, int KW, int gmode,
                               int stride, int pad, int up, int mode) {
   if (N <= 0 || Cin <= 0 || Cout <= 0 || Ho <= 0 || Wo <= 0 || KH <= 0 || KW <= 0 || !vst_mode_ok(mode)) return 0;
+  if (vst_thin_wgrad_ok(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
+    return vst_thin_wgrad_floats(N, Cout, Cin, Hs, Ws);
   if (use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode))
     return wgrad_halo_slab_floats(N, Cin, wgrad_halo_plan(N, Cout, Cin, Hs, Ws, mode));
   return vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
@@ -1093,6 +1096,11 @@ int vst_conv_wgrad(const float* dy, const float* x, float* dw, float* workspace,
   VST_CHECK_ARG(vst_mode_ok(mode));
   VST_CHECK_ARG(dy && x && dw && workspace && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0);
   VST_CHECK_ARG((gmode == 0 || gmode == 1) && (stride == 1 || stride == 2) && (up == 1 || up == 2));
+  // at most 4 output channels: the VALU kernel (exact fp32, whatever the mode's MFMA arithmetic),
+  // given the workspace vst_conv_wgrad_workspace names for it
+  if (vst_thin_wgrad_ok(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode) &&
+      ws_floats >= vst_thin_wgrad_floats(N, Cout, Cin, Hs, Ws))
+    return vst_thin_wgrad_launch(dy, x, dw, workspace, N, Cin, Hs, Ws, Cout, gmode, accumulate, (hipStream_t)stream);
   const long rowtiled_floats = vst_wgrad_workspace(N, Cout, KH * KW * Cin, Ho * Wo);
   bool halo = use_wgrad_halo(Cout, Cin, Hs, Ws, Ho, Wo, KH, KW, gmode, stride, pad, up, mode);
   // a workspace sized for the row-tiled kernel (the pre-halo rule) but smaller than the halo slabs

@@ -335,6 +335,10 @@ def kwu_ok(C, ks, stride, up, Wout):
     return C % 16 != 0 and ks > 1 and C * ks <= 32 and stride == 1 and up == 1 and Wout % 4 == 0
 
 
+def _round4(n):
+    return (n + 3) // 4 * 4
+
+
 def unfold_kw(x, ks, off, sgn, Wout, reflect):
     """out[n][c*ks + kw][y][v] = x[n][c][y][v + sgn*kw + off] (reflect or zero outside)."""
     N, C, H, W = x.shape
@@ -404,6 +408,8 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
         dx = _empty(x_shape, gz)
         lib.vst_tapsum(ptr(P), ptr(dx), N, Cin, H, W, ks, pad, 0, stream())
         return dx
+    if thin_dgrad_ok(Cout, Cin, ks, stride, pad, up, W) and gmask is None:
+        return conv_dgrad_thin(gz, w, x_shape, pad_mode == "reflect", dmask)
     if pad_mode == "zero" and up == 1:
         return conv_gemm(gz, packed_weight(w, transposed=True), Cin, ks, H, W, GM_TRANSPOSED, stride, pad, 1,
                          gmask=gmask, algo_flops=flops, epi=EPI_MASK if dmask is not None else 0,
@@ -417,7 +423,7 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
         return conv_dgrad_phase2(gz, w, x_shape, ks, pad, gmask, flops)
     if padout:
         dm = dmask.contiguous() if dmask is not None else None
-        if kwu_ok(Cout, ks, stride, up, W + 2 * pad) and w.shape[2] == ks:
+        if kwu_ok(Cout, ks, stride, up, _round4(W + 2 * pad)) and w.shape[2] == ks:
             return conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dm)
         return conv_dgrad_padout(gz, w, x_shape, ks, pad, flops, dm)
     if stride == 1 and gmask is None and ks % 2 == 1 and ks > 1 and pad == ks // 2 and min(H, W) * up > ks + 1:
@@ -427,6 +433,30 @@ def conv_dgrad(gz, w, x_shape, ks, stride, pad, pad_mode, up, gmask=None, dmask=
                      algo_flops=flops)
     dx = _empty(x_shape, gz)
     lib.vst_fold_reflect(ptr(dpad), ptr(dx), N * Cin, H, W, pad, up, 0, stream())
+    return dx
+
+
+THIN_DGRAD = os.environ.get("VST_THIN_DGRAD", "1") != "0"  # A/B: Cout <= 4 3x3 data gradients on the VALU kernel
+
+
+def thin_dgrad_ok(Cout, Cin, ks, stride, pad, up, W):
+    return THIN_DGRAD and Cout <= 4 and ks == 3 and stride == 1 and pad == 1 and up == 1 and Cin % 2 == 0 \
+        and W % 4 == 0 and W >= 8
+
+
+def conv_dgrad_thin(gz, w, x_shape, reflect, dmask=None):
+    """Data gradient of a 3x3 stride-1 pad-1 conv with <= 4 output channels (the AdaAttN decoder's last
+    conv, AA/network.py:99) on vst_conv_dgrad_thin: exact fp32 VALU, the fused ReLU mask applied."""
+    N, Cin, H, W = x_shape
+    Cout = w.shape[0]
+    dx = _empty(x_shape, gz)
+    border = _empty((N, Cin, H + 2, W + 2), gz) if reflect else None
+    dm = dmask.contiguous() if dmask is not None else None
+    tok = kprof.begin(2.0 * N * Cout * H * W * Cin * 9, 4.0 * (gz.numel() + 2 * dx.numel()),
+                      ("thin_dgrad", N, Cout, Cin, H, W), gemm_mode())
+    lib.vst_conv_dgrad_thin(ptr(gz), ptr(w.contiguous()), ptr(dm), ptr(dx), ptr(border), N, Cout, Cin, H, W,
+                            int(reflect), stream())
+    kprof.end(tok, family="thin")  # (a VALU kernel: outside the MFMA families' rooflines)
     return dx
 
 
@@ -459,7 +489,7 @@ def conv_dgrad_padout_kwu(gz, w, x_shape, ks, pad, flops, dmask=None):
     Kx1 gather over 16-multiple channels."""
     N, Cin, H, W = x_shape
     Ho = gz.shape[2]
-    dyu = unfold_kw(gz, ks, 0, -1, W + 2 * pad, reflect=False)
+    dyu = unfold_kw(gz, ks, 0, -1, _round4(W + 2 * pad), reflect=False)
     wp = packed_weight(w, True, kwu=True)
     dx = _empty(x_shape, gz)
     border = _empty((N, Cin, H + 2 * pad, W + 2 * pad), gz)
@@ -540,6 +570,8 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
     mode = gemm_mode()
     if not WGRAD_HALO_RES and (mode & 7) == GEMM_MODES["bf16x6"] and Cout % 192 == 0 and Cout % 128 != 0:
         mode |= PERTAP
+    if not THIN_WGRAD and Cout <= 4:
+        mode |= PERTAP  # (the A/B switch: the row-tiled GEMM instead of the VALU kernel)
     nws = lib.vst_conv_wgrad_workspace(N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad, up, mode)
     ws = _empty((nws,), x)
     acc = out is not None
@@ -548,7 +580,7 @@ def conv_wgrad(gz, x, w_shape, ks, stride, pad, pad_mode, up, out=None):
                       ("wgrad", N, Cin, H, W, Cout, Ho, Wo, ks, stride, pad, up), mode)
     lib.vst_conv_wgrad(ptr(gz), ptr(x), ptr(dw), ptr(ws), nws, N, Cin, H, W, Cout, Ho, Wo, ks, ks, gm, stride, pad,
                        up, int(acc), mode, stream())
-    kprof.end(tok, family="wgrad")
+    kprof.end(tok, family="thin" if pad == 1 and thin_wgrad_ok(Cout, Cin, ks, stride, up, W) else "wgrad")
     return dw
 
 
@@ -573,6 +605,12 @@ def rowsplit_ok(Cout, ks, stride, pad_mode, up):
 
 
 RS_WGRAD = os.environ.get("VST_RSW", "1") != "0"
+THIN_WGRAD = os.environ.get("VST_THIN_WGRAD", "1") != "0"  # A/B: Cout <= 4 3x3 weight gradients on the VALU kernel
+
+
+def thin_wgrad_ok(Cout, Cin, ks, stride, up, W):
+    """vst_conv_wgrad's own choice (csrc/wgrad_gemm.hip thin_wgrad_ok) for pad-1 convs"""
+    return THIN_WGRAD and Cout <= 4 and ks == 3 and stride == 1 and up == 1 and Cin % 4 == 0 and W % 4 == 0 and W >= 8
 
 
 def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
@@ -581,6 +619,8 @@ def rowsplit_wgrad_ok(Cout, Cin, ks, stride, pad_mode, up, W):
     AA/network.py:93-96).  Rows (co, kh) read dY[co][y - kh], columns (kw, ci) read x[ci][y][x + kw]:
     M = 3 Cout and J = 3 Cin instead of M = Cout and J = 9 Cin, so each dY tile feeds 3x the rows and
     is re-read for 3x fewer column tiles (64 x 576 -> 192 x 192 for 64 -> 64)."""
+    if thin_wgrad_ok(Cout, Cin, ks, stride, up, W):
+        return False  # vst_conv_wgrad's fp32 VALU kernel (the AdaAttN decoder's last conv, 64 -> 3)
     if rowsplit_ok(Cout, ks, stride, pad_mode, up):
         return True
     if not (RS_WGRAD and Cout <= 64 and Cin >= 64 and ks == 3 and stride == 1 and pad_mode == "reflect" and up == 1
