@@ -23,6 +23,11 @@
 
 namespace vstk {
 
+// taps of A preloaded ahead of the patch on the double-buffered single-product tiles (conv_halo_kernel):
+// five keep the 4- and 8-wave tiles at 126 / 116 VGPRs (4 waves per SIMD); config 5, fp16 kernel trace:
+// 8-wave 763 -> 726 us, 4-wave 951 -> 921 us against one (profiles/r06_thin_halo_c5_kernel_summary.txt,
+// profiles/r06_apre_c5_kernel_summary.txt)
+constexpr int HALO_APRE_DB = 5;
 constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave covers 4 rows of it
 
 // One tap of a wave's 32 x 128 tile: the B fragments of output row j (LDS pixel rows jstride apart)
@@ -218,17 +223,20 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  // Single-product modes (one piece per value): the A fragments of ALL taps of a stage are loaded at the
-  // end of the previous stage, ahead of the next patch's loads.  Vector-memory loads complete in issue
-  // order, so a per-tap A load issued after the patch prefetch made the next tap wait for the whole
-  // patch (the prefetch then overlapped one tap of nine); the split-product modes keep the per-tap
-  // A loads (three pieces x nine taps would not fit the registers) and are MFMA-bound.
-  constexpr bool AST = NPC == 1 && !DB;
-  bf16x8_t arS[AST ? NTAP : 1];
+  // Single-product modes (one piece per value): the A fragments of the first APRE taps of a stage
+  // (all nine on the one-buffer tiles) are loaded at the end of the previous stage, ahead of the next
+  // patch's loads; later taps load theirs one tap ahead.  Vector-memory loads complete in issue order,
+  // so a per-tap A load issued after the patch prefetch makes its tap wait for the whole patch: with
+  // per-tap loads from tap 1 on, the prefetch overlapped one tap of nine.  The double-buffered tiles
+  // keep 4 waves per SIMD (128 VGPRs) with three preloaded taps; the split-product modes keep the per-tap
+  // loads (three pieces a tap) and are MFMA-bound.
+  constexpr bool AST = NPC == 1;
+  constexpr int APRE = !AST ? 1 : (!DB ? NTAP : HALO_APRE_DB);
+  bf16x8_t arS[APRE];
   auto load_stage_a = [&](int cb) {
     const int c = cb < nst ? cb : 0;  // (past the slice: a harmless reload, unbranched)
 #pragma unroll
-    for (int t = 0; t < NTAP; ++t) {
+    for (int t = 0; t < APRE; ++t) {
       const int a_soff = __builtin_amdgcn_readfirstlane((((NTAP * c + t) * P.Mpad + m0) * AW) * 4);
       arS[t] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff, 0));
     }
@@ -243,8 +251,14 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       // columns lo + pw
       const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
       if constexpr (AST) {
-        const bf16x8_t a1[1][3] = {{arS[t], arS[t], arS[t]}};
-        halo_tap<TN, PREC, LS>(acc, a1, Bt, lane, HPW);
+        if (t + 1 >= APRE && t + 1 < NTAP) load_a(NTAP * cb + t + 1, arN);
+        if (t < APRE) {
+          const bf16x8_t a1[1][3] = {{arS[t], arS[t], arS[t]}};
+          halo_tap<TN, PREC, LS>(acc, a1, Bt, lane, HPW);
+        } else {
+          halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
+        }
+        if (t + 1 >= APRE && t + 1 < NTAP) arC[0][0] = arN[0][0];
       } else {
         // (past the slice's last k-tile: a harmless reload of k-tile 0, unbranched)
         const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : (cb + 1 < nst ? NTAP * (cb + 1) : 0);
@@ -362,7 +376,11 @@ inline int halo_cfg(int M, int pack_mpad) {
 // with the prefetch sunk behind the taps by the compiler and per-tap A loads: 3 measured 142.31 vs
 // 141.5 ms at 4)
 constexpr int HALO_SMINW_SP = 3;
-constexpr int HALO_PD = 2;        // patches in flight for the single-product double-buffered tiles
+// patches in flight for the single-product double-buffered tiles: one.  The second register set (round 4)
+// bought its gain through the compiler's placement of the first one's loads; with the loads pinned ahead
+// of the taps and the taps' A loads ahead of them, a second patch in flight would still be waited for by
+// the first per-tap A load after it (vector loads complete in order)
+constexpr int HALO_PD = 1;
 template <int C, int PR, bool GM, int KH = 3, int KW = KH>
 void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   constexpr int WM = halo_wm_c(C), WN = halo_wn_c(C);
@@ -372,11 +390,8 @@ void launch_halo_c(dim3 grid, hipStream_t st, const ConvParams& P) {
   // layer; fp16 at 4 waves 118 us vs 150 us at 3 on the residual layer); 3 for 4-wave double-
   // buffered tiles, 2 for the 6- and 8-wave double-buffered ones
   constexpr int MINW = !halo_db_c(C) ? (PR == 3 || PR == 1 ? 3 : HALO_SMINW_SP) : (WM * WN <= 4 ? 3 : 2);
-  // depth-2 patch prefetch for the 8-wave single-product tiles (config 5: the fp16 tiles wait on the
-  // next patch's gather; fp16 shapes, one box: AdaAttN decoder 256-row 69 -> 53 us, VGG conv4 150 ->
-  // 144, conv5 123 -> 89; config 5 145.07 -> 141.5 ms, profiles/r04_halo_pd.txt).  Not on the 4-wave
-  // 128-row tile (its second register set costs a wave per SIMD: VGG conv2 232 -> 262 us), not for
-  // bf16x6 (MFMA-bound, registers spoken for)
+  // depth-2 patch prefetch (round 4: config 5 145.07 -> 141.5 ms, profiles/r04_halo_pd.txt) is off
+  // (HALO_PD above)
   constexpr int PD = (PR != 3 && halo_db_c(C) && WM * WN >= 8) ? HALO_PD : 1;
   conv_halo_kernel<WM, WN, MINW, PR, GM, halo_db_c(C), PD, KH, KW><<<grid, WM * WN * 64, 0, st>>>(P);
 }
