@@ -28,6 +28,10 @@ namespace vstk {
 // 8-wave 763 -> 726 us, 4-wave 951 -> 921 us against one (profiles/r06_thin_halo_c5_kernel_summary.txt,
 // profiles/r06_apre_c5_kernel_summary.txt)
 constexpr int HALO_APRE_DB = 5;
+// and under the split products (bf16x6 / bf16x3: 12 / 8 VGPRs a tap) on the 3x3 one-buffer and 8-wave
+// tiles; the 4-wave double-buffered and the 9x1 / 1x9 tiles keep one (their registers would cost a
+// wave per SIMD)
+constexpr int HALO_APRE_SPLIT = 2;
 constexpr int HTW = 32;  // output tile width (one MFMA column block); each wave covers 4 rows of it
 
 // One tap of a wave's 32 x 128 tile: the B fragments of output row j (LDS pixel rows jstride apart)
@@ -223,22 +227,25 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       ar[0][pc] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
   };
 
-  // Single-product modes (one piece per value): the A fragments of the first APRE taps of a stage
-  // (all nine on the one-buffer tiles) are loaded at the end of the previous stage, ahead of the next
-  // patch's loads; later taps load theirs one tap ahead.  Vector-memory loads complete in issue order,
-  // so a per-tap A load issued after the patch prefetch makes its tap wait for the whole patch: with
-  // per-tap loads from tap 1 on, the prefetch overlapped one tap of nine.  The double-buffered tiles
-  // keep 4 waves per SIMD (128 VGPRs) with three preloaded taps; the split-product modes keep the per-tap
-  // loads (three pieces a tap) and are MFMA-bound.
-  constexpr bool AST = NPC == 1;
-  constexpr int APRE = !AST ? 1 : (!DB ? NTAP : HALO_APRE_DB);
-  bf16x8_t arS[APRE];
+  // The A fragments of the first APRE taps of a stage are loaded at the end of the previous stage,
+  // ahead of the next patch's loads; later taps load theirs one tap ahead.  Vector-memory loads complete
+  // in issue order, so a per-tap A load issued after the patch prefetch makes its tap wait for the whole
+  // patch: with per-tap loads from tap 1 on, the prefetch overlapped one tap of nine.  APRE: all nine
+  // taps on the single-product one-buffer tiles (3 waves per SIMD), five on the single-product
+  // double-buffered ones and two (or one) under the split products (two or three pieces a tap), each
+  // within the register budget of its tile's occupancy.
+  constexpr int APRE = NPC == 1 ? (!DB ? NTAP : HALO_APRE_DB)
+                                : ((KH == 3 && KW == 3 && (!DB || WM * WN >= 8)) ? HALO_APRE_SPLIT : 1);
+  bf16x8_t arS[APRE > 1 ? APRE : 1][3];
   auto load_stage_a = [&](int cb) {
     const int c = cb < nst ? cb : 0;  // (past the slice: a harmless reload, unbranched)
 #pragma unroll
     for (int t = 0; t < APRE; ++t) {
       const int a_soff = __builtin_amdgcn_readfirstlane((((NTAP * c + t) * P.Mpad + m0) * AW) * 4);
-      arS[t] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff, 0));
+#pragma unroll
+      for (int pc = 0; pc < NPC; ++pc)
+        arS[t][pc] =
+            __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(asrd, ad_voff, a_soff + 32 * pc, 0));
     }
   };
   // the taps of every channel block of stage st, B fragments from patch buffer buf
@@ -250,28 +257,32 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       // B fragments of tap t: output row 4 wn + j of the tile reads patch row 4 wn + j + ph,
       // columns lo + pw
       const float(*Bt)[LS] = &Ps[buf][(4 * wn + ph) * HPW + pw];
-      if constexpr (AST) {
-        if (t + 1 >= APRE && t + 1 < NTAP) load_a(NTAP * cb + t + 1, arN);
-        if (t < APRE) {
-          const bf16x8_t a1[1][3] = {{arS[t], arS[t], arS[t]}};
-          halo_tap<TN, PREC, LS>(acc, a1, Bt, lane, HPW);
-        } else {
-          halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
-        }
-        if (t + 1 >= APRE && t + 1 < NTAP) arC[0][0] = arN[0][0];
-      } else {
-        // (past the slice's last k-tile: a harmless reload of k-tile 0, unbranched)
+      if constexpr (APRE == 1) {
+        // per-tap loads throughout: the last tap loads the next stage's first (past the slice's last
+        // k-tile: a harmless reload of k-tile 0, unbranched)
         const int kt_next = t < NTAP - 1 ? NTAP * cb + t + 1 : (cb + 1 < nst ? NTAP * (cb + 1) : 0);
         load_a(kt_next, arN);
         halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
 #pragma unroll
         for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+      } else {
+        if (t + 1 >= APRE && t + 1 < NTAP) load_a(NTAP * cb + t + 1, arN);
+        if (t < APRE) {
+          const bf16x8_t a1[1][3] = {{arS[t][0], arS[t][1], arS[t][2]}};
+          halo_tap<TN, PREC, LS>(acc, a1, Bt, lane, HPW);
+        } else {
+          halo_tap<TN, PREC, LS>(acc, arC, Bt, lane, HPW);
+        }
+        if (t + 1 >= APRE && t + 1 < NTAP) {
+#pragma unroll
+          for (int pc = 0; pc < NPC; ++pc) arC[0][pc] = arN[0][pc];
+        }
       }
     }
   };
   load_into(st0, rv, rgv);
-  if constexpr (AST) load_stage_a(st0);
-  else load_a(NTAP * st0, arC);
+  if constexpr (APRE == 1) load_a(NTAP * st0, arC);
+  else load_stage_a(st0);
   store_from(0, rv, rgv);
   if constexpr (PD == 1) {
     __syncthreads();
@@ -284,7 +295,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       taps(st, buf);
       if constexpr (!DB) __syncthreads();  // every wave is done reading the one buffer
       store_from(DB ? buf ^ 1 : 0, rv, rgv);  // (after the last stage: zeros into a buffer nobody reads)
-      if constexpr (AST) load_stage_a(st + 1);
+      if constexpr (APRE > 1) load_stage_a(st + 1);
       __syncthreads();
     }
   } else {
@@ -301,7 +312,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_halo_kernel(ConvParam
       __builtin_amdgcn_sched_barrier(0);
       taps(st, buf);
       store_from(buf ^ 1, Rs, Gs);
-      if constexpr (AST) load_stage_a(st + 1);
+      if constexpr (APRE > 1) load_stage_a(st + 1);
       __syncthreads();
     };
     // (pairs in the loop, an odd last stage after it: no branch around a stage inside the loop)
