@@ -379,7 +379,7 @@ struct Wg2Params {
 // KD: k-tiles per LDS stage (one barrier per KD tiles); two for the single-product modes, whose
 // k loop does 4-6 MFMAs per wave and tile and is otherwise paced by the per-tile barrier
 // (one stage of loads in flight; the round-3 two-stage variant measured no gain and was removed)
-template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1>
+template <int WM, int TM, int WN, int TN, int MINW, int PREC, int GMODE, int KD = 1, bool S1 = false>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
   const float* src_n = P.src + (long)n * P.Cs * plane;
   const __amdgpu_buffer_rsrc_t asrd = uniform_rsrc(a_n, (uint32_t)(a_img * 4));
   const __amdgpu_buffer_rsrc_t bsrd = uniform_rsrc(src_n, (uint32_t)((long)P.Cs * plane * 4));
-  const int Hv = P.Hs * P.up, Wv = P.Ws * P.up, sh = P.up - 1;
+  const int Hv = S1 ? P.Hs : P.Hs * P.up, Wv = S1 ? P.Ws : P.Ws * P.up, sh = P.up - 1;
 
   // A tasks: (row, half) with 8 consecutive lanes on 8 consecutive rows of one half.  Row-split A:
   // a_voff is the (possibly negative) byte offset of a[co][-kh][8*half]; per tile the row oy - kh
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     const int soff = __builtin_amdgcn_readfirstlane((r_begin + t * BK) * 4);
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
-      if (P.asplit) {  // wave-uniform branch
+      if (!S1 && P.asplit) {  // wave-uniform branch
         const int ya = t_oy - a_kh[i];
         const int vo = (ya >= 0 && ya < P.Ha) ? a_voff[i] + soff : OOR;
         ra[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(asrd, vo, 0, 0));
@@ -490,7 +490,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
-      int yv = t_oy * P.stride + b_kh[i] - P.pad;
+      const int stride = S1 ? 1 : P.stride, up = S1 ? 1 : P.up;
+      int yv = t_oy * stride + b_kh[i] - P.pad;
       bool ok = b_ok[i];
       if (GMODE == 0) {
         yv = abs(yv);
@@ -500,11 +501,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       } else {
         ok = ok && yv >= 0 && yv < Hv;
       }
-      const int rowoff = b_cbase[i] + (yv >> sh) * P.Ws;
-      const int xv0 = (t_ox + 8 * b_half[i]) * P.stride + b_kw[i] - P.pad;
-      const int xv7 = xv0 + 7 * P.stride;
+      const int rowoff = b_cbase[i] + (S1 ? yv : yv >> sh) * P.Ws;
+      const int xv0 = (t_ox + 8 * b_half[i]) * stride + b_kw[i] - P.pad;
+      const int xv7 = xv0 + 7 * stride;
       if (xv0 >= 0 && xv7 < Wv) {  // interior window: one base, immediate offsets
-        if (P.up == 2) {           // nearest x2: 8 virtual columns over 4-5 source columns
+        if (up == 2) {             // nearest x2: 8 virtual columns over 4-5 source columns
           const int vo = ok ? (rowoff + (xv0 >> 1)) * 4 : OOR;
           float s[5];
 #pragma unroll
@@ -512,7 +513,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
           const bool odd = xv0 & 1;
 #pragma unroll
           for (int e = 0; e < 8; ++e) rb[i][e] = odd ? s[(e + 1) >> 1] : s[e >> 1];
-        } else if (P.stride == 2) {
+        } else if (stride == 2) {
           const int vo = ok ? (rowoff + xv0) * 4 : OOR;
 #pragma unroll
           for (int e = 0; e < 8; ++e) rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo + 8 * e, 0, 0));
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
       } else {  // border window: per element
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          int xv = xv0 + e * P.stride;
+          int xv = xv0 + e * stride;
           bool oke = ok;
           if (GMODE == 0) {
             xv = abs(xv);
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void wgrad2_kernel(Wg2Params P)
           } else {
             oke = oke && xv >= 0 && xv < Wv;
           }
-          const int vo = oke ? (rowoff + (xv >> sh)) * 4 : OOR;
+          const int vo = oke ? (rowoff + (S1 ? xv : xv >> sh)) * 4 : OOR;
           rb[i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, vo, 0, 0));
         }
       }
@@ -816,18 +817,26 @@ static int plan_splits(long tiles, int N, int HWo, int c, long Mpad, long Jpad) 
   return best;
 }
 
+template <int PR, int GMD, int KD, bool S1>
+static void launch_wg2_pks(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
+  switch (c) {
+    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+    case W64H: wgrad2_kernel<1, 2, 2, 1, 4, PR, GMD, KD, S1><<<g, 128, 0, st>>>(P); break;
+    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD, S1><<<g, NT, 0, st>>>(P); break;
+  }
+}
+// S1: stride 1, no upsampling, plain A rows (every layer but conv2 / conv3, the row-split and the
+// up2 phase GEMMs) -- the gather without the run-time stride / upsample / row-split paths, whose
+// merged branches cost the k loop waits on its own prefetch (residual layer 0.58 -> 0.50 ms)
 template <int PR, int GMD, int KD>
 static void launch_wg2_pk(int c, dim3 g, hipStream_t st, const Wg2Params& P) {
-  switch (c) {
-    case W32: wgrad2_kernel<1, 1, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W64: wgrad2_kernel<1, 2, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W96: wgrad2_kernel<1, 3, 4, 1, 4, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W128: wgrad2_kernel<2, 2, 2, 2, 3, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W64N: wgrad2_kernel<1, 2, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W96N: wgrad2_kernel<1, 3, 4, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-    case W64H: wgrad2_kernel<1, 2, 2, 1, 4, PR, GMD, KD><<<g, 128, 0, st>>>(P); break;
-    default: wgrad2_kernel<2, 3, 2, 2, 2, PR, GMD, KD><<<g, NT, 0, st>>>(P); break;
-  }
+  if (P.stride == 1 && P.up == 1 && !P.asplit) launch_wg2_pks<PR, GMD, KD, true>(c, g, st, P);
+  else launch_wg2_pks<PR, GMD, KD, false>(c, g, st, P);
 }
 
 // k-tiles per stage for the single-product modes (compile-time: one tested kernel per mode)
