@@ -417,10 +417,12 @@ static int conv_gemm_launch(const float* src, const float* wpack, const float* b
   P.M = M;
   int cfg = widen_cfg(select_cfg(M), (long)Ho * Wo);
   {
-    // 256-row tiles for 256-multiple M on the 2-term bf16 paths (VGG conv3_x / conv4_x)
+    // 256-row tiles for 256-multiple M on the single-product paths (then A-direct below).  Not under
+    // bf16x3: its 256 x 128 LDS-A tile spills 63 VGPRs (eight accumulator fragments and two pieces per
+    // operand); the 128-row tile ran config 5 at 128.4 / 128.1 ms against 128.5 / 129.6 (A/B/A/B on one
+    // box, the AdaAttN attention projections)
     const int am = vst_mode_arith(mode);
-    if (cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16X3 || am == VST_GEMM_BF16 || am == VST_GEMM_F16))
-      cfg = T256;
+    if (cfg == T128 && M % 256 == 0 && (am == VST_GEMM_BF16 || am == VST_GEMM_F16)) cfg = T256;
     // bf16x6 A-direct blocks: 64-, 128- and 256-row tiles always, the 192-row tile for data
     // gradients only (its forward keeps the LDS-A tile: DESIGN.md §4.2 item 3)
     const bool dg = gmode == GM_TRANSPOSED;
