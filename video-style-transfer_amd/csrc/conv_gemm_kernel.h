@@ -93,6 +93,37 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 
   const int HWo = P.Ho * P.Wo;
   float* out_n = P.out + (long)n * P.M * HWo;
   const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
+  // plain outputs [+ bias] [-> ReLU] of a full 32-row tile (the halo kernel's forward convs: one weight
+  // fragment per wave): the bias of each of the lane's 16 rows loaded once, not per pixel fragment, and
+  // no per-element epi / row-range branches -- the general path below is ~16k instructions of branchy
+  // code, which on the shallow layers (64 channels: four channel blocks) outweighed the k loop.  Same
+  // operations in the same order: bitwise the general path's result
+  if constexpr (TM == 1) {
+    if ((P.epi & ~(EPI_BIAS | EPI_RELU)) == 0 && mrow0 + 32 <= P.M) {
+      const bool relu = (P.epi & EPI_RELU) != 0, has_b = (P.epi & EPI_BIAS) != 0;
+      float bv[16];
+      int mo[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        bv[r] = has_b ? P.bias[m] : 0.f;
+        mo[r] = m * HWo;  // (< 2^31: one image's output)
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (pix[j] < 0) continue;
+        float* o = out_n + pix[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[0][j][r];
+          if (has_b) v += bv[r];
+          if (relu) v = fmaxf(v, 0.f);
+          o[mo[r]] = v;
+        }
+      }
+      return;
+    }
+  }
   if (P.epi & (EPI_PHASE2 | EPI_PADOUT)) {
     // PHASE2: the 4 consecutive rows of a C-register group are the 4 phases of one channel
     const bool ph2 = P.epi & EPI_PHASE2;
