@@ -93,19 +93,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 
   const int HWo = P.Ho * P.Wo;
   float* out_n = P.out + (long)n * P.M * HWo;
   const float* mask_n = P.mask ? P.mask + (long)n * P.M * HWo : nullptr;
-  // plain outputs [+ bias] [-> ReLU] of a full 32-row tile (the halo kernel's forward convs: one weight
-  // fragment per wave): the bias of each of the lane's 16 rows loaded once, not per pixel fragment, and
-  // no per-element epi / row-range branches -- the general path below is ~16k instructions of branchy
-  // code, which on the shallow layers (64 channels: four channel blocks) outweighed the k loop.  Same
-  // operations in the same order: bitwise the general path's result
-  if constexpr (TM == 1) {
-    if ((P.epi & ~(EPI_BIAS | EPI_RELU)) == 0 && mrow0 + 32 <= P.M) {
-      const bool relu = (P.epi & EPI_RELU) != 0, has_b = (P.epi & EPI_BIAS) != 0;
+  // plain outputs [+ bias] [-> ReLU] of a full row tile (every forward conv but ConvTanh's, the
+  // attention / Gram GEMMs): per weight fragment, the bias of each of the lane's 16 rows loaded once,
+  // not per pixel fragment, and no per-element epi / row-range branches -- the general path below is
+  // ~16k instructions of branchy code, which on the shallow layers (64 channels: four channel blocks)
+  // outweighed the k loop.  Same operations in the same order per element: bitwise the general path's
+  if ((P.epi & ~(EPI_BIAS | EPI_RELU)) == 0 && mrow0 + TM * 32 <= P.M) {
+    const bool relu = (P.epi & EPI_RELU) != 0, has_b = (P.epi & EPI_BIAS) != 0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
       float bv[16];
       int mo[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = mrow0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
         bv[r] = has_b ? P.bias[m] : 0.f;
         mo[r] = m * HWo;  // (< 2^31: one image's output)
       }
@@ -115,14 +116,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& P, const f32x16 
         float* o = out_n + pix[j];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float v = acc[0][j][r];
+          float v = acc[i][j][r];
           if (has_b) v += bv[r];
           if (relu) v = fmaxf(v, 0.f);
           o[mo[r]] = v;
         }
       }
-      return;
     }
+    return;
   }
   if (P.epi & (EPI_PHASE2 | EPI_PADOUT)) {
     // PHASE2: the 4 consecutive rows of a C-register group are the 4 phases of one channel
