@@ -180,30 +180,34 @@ __global__ void pack_phase2_kernel(const float* __restrict__ w, float* __restric
 // channels c*K + kw >= C*K are zero.  A conv over `out` with a Kx1 kernel (pad_x = 0) then runs on
 // the 16-channel k-tile path instead of a per-element tap decode over 3 channels.
 __global__ void unfold_kw_kernel(const float* __restrict__ src, float* __restrict__ out, int N, int C, int H, int Ws,
-                                 int Wout, int K, int Cu, int sgn, int off, int reflect) {
-  // one thread per 4 consecutive outputs of a row (float4 store; Wout % 4 == 0), grid.y = row
-  // (n, cu, y) -- no 64-bit index divisions
+                                 int Wout, int K, int Cu, int Cg, int sgn, int off, int reflect) {
+  // one thread per 4 consecutive outputs (float4 store; Wout % 4 == 0) of all K unfolded rows of one
+  // source row: grid.y = (n, channel group cg, y), the group's rows cu = cg*K + kw (kw < K, cu < Cu;
+  // groups cg >= C write the zero channels).  The K rows re-read one source row segment from L1.
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (4 * q >= Wout) return;
   const int row = blockIdx.y + gridDim.y * blockIdx.z;
-  if (row >= N * Cu * H) return;
-  const int y = row % H, t = row / H, cu = t % Cu, n = t / Cu;
-  const int c = cu / K, kw = cu - c * K;
-  float v4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < C) {
-    const float* sr = src + (((long)n * C + c) * H + y) * Ws;
+  if (row >= N * Cg * H) return;
+  const int y = row % H, t = row / H, cg = t % Cg, n = t / Cg;
+  const float* sr = src + (((long)n * C + (cg < C ? cg : 0)) * H + y) * Ws;
+  float* orow = out + (((long)n * Cu + cg * K) * H + y) * Wout + 4 * q;
+  const long ostride = (long)H * Wout;
+  for (int kw = 0; kw < K && cg * K + kw < Cu; ++kw) {
+    float v4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (cg < C) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int xs = 4 * q + e + sgn * kw + off;
-      if (reflect) {
-        xs = abs(xs);
-        xs = xs >= Ws ? 2 * Ws - 2 - xs : xs;
+      for (int e = 0; e < 4; ++e) {
+        int xs = 4 * q + e + sgn * kw + off;
+        if (reflect) {
+          xs = abs(xs);
+          xs = xs >= Ws ? 2 * Ws - 2 - xs : xs;
+        }
+        // (reflect: single reflections only; anything further reads 0, never out of bounds)
+        v4[e] = (xs >= 0 && xs < Ws) ? sr[xs] : 0.f;
       }
-      // (reflect: single reflections only; anything further reads 0, never out of bounds)
-      v4[e] = (xs >= 0 && xs < Ws) ? sr[xs] : 0.f;
     }
+    *reinterpret_cast<f32x4*>(orow + kw * ostride) = f32x4{v4[0], v4[1], v4[2], v4[3]};
   }
-  *reinterpret_cast<f32x4*>(out + (long)row * Wout + 4 * q) = f32x4{v4[0], v4[1], v4[2], v4[3]};
 }
 
 // dx[n][c][y][x] (+)= sum_{kh,kw} P[n][(c*K + kh)*K + kw][y + pad - kh][x + pad - kw]  (zero outside):
@@ -769,11 +773,14 @@ int vst_unfold_kw(const float* src, float* out, int N, int C, int H, int Ws, int
                   int reflect, void* stream) {
   VST_CHECK_ARG(src && out && N > 0 && C > 0 && H > 0 && Ws > 0 && Wout > 0 && K > 0 && Cu >= C * K);
   VST_CHECK_ARG((sgn == 1 || sgn == -1) && !(reflect && Ws < 2) && Wout % 4 == 0);
-  const long rows = (long)N * Cu * H;
-  VST_CHECK_ARG(rows < (1L << 31));
+  const int Cg = (Cu + K - 1) / K;
+  VST_CHECK_ARG((long)N * Cu * H < (1L << 31));
+  const long rows = (long)N * Cg * H;
   const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
-  dim3 g(ceil_div(Wout / 4, 128), gy, (unsigned)((rows + gy - 1) / gy));
-  unfold_kw_kernel<<<g, 128, 0, (hipStream_t)stream>>>(src, out, N, C, H, Ws, Wout, K, Cu, sgn, off, reflect);
+  // block = the row's float4 columns rounded up to whole wavefronts (at most 256)
+  const int bx = (Wout / 4 + 63) / 64 * 64 < 256 ? (Wout / 4 + 63) / 64 * 64 : 256;
+  dim3 g(ceil_div(Wout / 4, bx), gy, (unsigned)((rows + gy - 1) / gy));
+  unfold_kw_kernel<<<g, bx, 0, (hipStream_t)stream>>>(src, out, N, C, H, Ws, Wout, K, Cu, Cg, sgn, off, reflect);
   return vst_launch_status();
 }
 
