@@ -351,6 +351,41 @@ def _unfold(x, K, off, sgn, Wout, reflect, Cu):
     return out
 
 
+def _unfold_ref(x, K, off, sgn, Wout, reflect, Cu):
+    """out[n][c*K + kw][y][v] = x[n][c][y][v + sgn*kw + off]: single reflection or zero outside; channels
+    >= C*K zero (the vst_unfold_kw contract, include/vst_hip.h)."""
+    N, C, H, W = x.shape
+    out = torch.zeros((N, Cu, H, Wout), device=x.device)
+    v = torch.arange(Wout, device=x.device)
+    for c in range(C):
+        for kw in range(K):
+            xs = v + sgn * kw + off
+            if reflect:
+                xs = xs.abs()
+                xs = torch.where(xs >= W, 2 * W - 2 - xs, xs)
+            ok = (xs >= 0) & (xs < W)
+            out[:, c * K + kw, :, ok] = x[:, c, :, xs[ok]]
+    return out
+
+
+@pytest.mark.parametrize("case", [
+    (2, 3, 7, 64, 64, 9, 32, -4, 1, True),     # ReCoNet conv1's forward unfold (27 -> 32: a zero group)
+    (2, 3, 5, 30, 40, 9, 32, 0, -1, False),    # ConvTanh's padded-grid data gradient (rows rounded to 4)
+    (1, 5, 3, 13, 16, 3, 16, -1, 1, True),     # K = 3, 15 -> 16
+    (1, 2, 4, 9, 12, 9, 32, -4, 1, True),      # Cu spans two zero groups (18 -> 32)
+    (3, 3, 2, 700, 704, 9, 27, -4, 1, False),  # exact fit, a row wider than one block
+])
+def test_unfold_kw_exact(case):
+    """vst_unfold_kw (one thread writes the K unfolded rows of a source row segment) against a torch
+    gather: a copy, so bitwise; NaN-filled output proves every element, zero channels included, is
+    written."""
+    N, C, H, W, Wout, K, Cu, off, sgn, reflect = case
+    x = _rand(N, C, H, W, seed=73)
+    got = _unfold(x, K, off, sgn, Wout, reflect, Cu)
+    torch.cuda.synchronize()
+    assert torch.equal(got, _unfold_ref(x, K, off, sgn, Wout, reflect, Cu))
+
+
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("shape", [(2, 3, 40, 64, 48), (1, 3, 17, 96, 32), (1, 3, 33, 32, 64)])
 def test_halo91_kwu_forward_bitwise(mode, shape):
