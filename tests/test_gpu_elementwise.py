@@ -100,6 +100,42 @@ def test_resize_bilinear(src, dst):
     assert rel_err(C(out), ref + add) < 1e-6
 
 
+def _offset_view(t, k):
+    """a copy of t whose data starts k floats into a fresh buffer (misaligned for k = 1)."""
+    buf = torch.zeros(t.numel() + 4, device=t.device)
+    v = buf[k:k + t.numel()].view(t.shape)
+    v.copy_(t)
+    return v
+
+
+@pytest.mark.parametrize("shape", [(2, 5, 7, 10), (1, 3, 1, 2), (2, 16, 9, 130), (1, 4, 33, 64)])
+def test_resize_up2_bitwise(shape):
+    """The exact x2 upsample kernel (aligned operands, Ho = 2H, Wo = 2W: eight outputs per thread from
+    registers) against the per-element kernel (the same call on a misaligned input): bitwise, with
+    chscale / binarize / addend / a channel-slice output; and F.interpolate within 1e-6."""
+    from vst import ops
+
+    g = torch.Generator().manual_seed(11)
+    N, Cc, H, W = shape
+    x = torch.randn(shape, generator=g)
+    dst = (2 * H, 2 * W)
+    ref = F.interpolate(x, size=dst, mode="bilinear", align_corners=False)
+    xa, xm = _offset_view(G(x), 0), _offset_view(G(x), 1)
+    a = ops.resize_bilinear(xa, dst)
+    assert rel_err(C(a), ref) < 1e-6
+    assert torch.equal(a, ops.resize_bilinear(xm, dst))
+    sc = G(torch.rand(Cc, generator=g) - 0.3)
+    add = G(torch.randn((N, Cc) + dst, generator=g))
+    for kw in ({"chscale": sc}, {"binarize": True}, {"addend": add}, {"chscale": sc, "addend": add}):
+        assert torch.equal(ops.resize_bilinear(xa, dst, **kw), ops.resize_bilinear(xm, dst, **kw)), kw
+    bufa = torch.full((N, Cc + 4) + dst, float("nan"), device=DEV)
+    bufm = bufa.clone()
+    ops.resize_bilinear(xa, dst, chscale=sc, out=bufa[:, 4:])
+    ops.resize_bilinear(xm, dst, chscale=sc, out=bufm[:, 4:])
+    assert torch.equal(bufa[:, 4:], bufm[:, 4:])
+    assert torch.isnan(bufa[:, :4]).all()
+
+
 @pytest.mark.parametrize("n", [4096 * 3, 4097])
 def test_relu_bwd(n):
     from vst import ops

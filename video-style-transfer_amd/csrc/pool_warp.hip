@@ -541,6 +541,13 @@ __device__ __forceinline__ void resize_axis(int d, int n_in, float scale, int& i
   l1 = src - (float)i0;
 }
 
+// the bilinear blend of the four taps (a b / c d), its fused multiply-adds spelled out so that every
+// resize kernel rounds alike whatever the compiler would contract
+__device__ __forceinline__ float bilerp(float a, float b, float c, float d, float lx, float ly) {
+  const float top = fmaf(lx, b, (1.f - lx) * a), bot = fmaf(lx, d, (1.f - lx) * c);
+  return fmaf(ly, bot, (1.f - ly) * top);
+}
+
 // out[n][c] = resize(x[nc]) * chscale[c] (+ addend[n][c]); binarize: out = out > 0
 // out/addend images are out_bs floats apart (channel-concat targets, AA/utilities.py:98-109)
 __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ out, long NC, int C, int H, int W, int Ho,
@@ -557,8 +564,7 @@ __global__ void resize_kernel(const float* __restrict__ x, float* __restrict__ o
   resize_axis(oy, H, sy, y0, y1, ly);
   resize_axis(ox, W, sx, x0, x1, lx);
   const float* p = x + nc * H * W;
-  float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
-            ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
+  float v = bilerp(p[(long)y0 * W + x0], p[(long)y0 * W + x1], p[(long)y1 * W + x0], p[(long)y1 * W + x1], lx, ly);
   if (chscale) v *= chscale[nc % C];
   if (binarize) v = v > 0.f ? 1.f : 0.f;
   const long o = (nc / C) * out_bs + (nc % C) * (long)Ho * Wo + (long)oy * Wo + ox;
@@ -581,13 +587,85 @@ __global__ __launch_bounds__(256) void resize_plane_kernel(const float* __restri
   resize_axis(oy, H, sy, y0, y1, ly);
   resize_axis(ox, W, sx, x0, x1, lx);
   const float* p = x + (long)nc * H * W;
-  float v = (1.f - ly) * ((1.f - lx) * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
-            ly * ((1.f - lx) * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
+  float v = bilerp(p[(long)y0 * W + x0], p[(long)y0 * W + x1], p[(long)y1 * W + x0], p[(long)y1 * W + x1], lx, ly);
   if (chscale) v *= chscale[c];
   if (binarize) v = v > 0.f ? 1.f : 0.f;
   const long o = (long)n * out_bs + (long)c * Ho * Wo + (long)oy * Wo + ox;
   if (addend) v += addend[o];
   out[o] = v;
+}
+
+// resize_plane_kernel for an exact x2 upsample (Ho = 2H, Wo = 2W, both scales 0.5; W even, aligned
+// rows): one thread writes output rows 2r, 2r + 1, columns 4q..4q+3 (two float4 stores) from the input
+// values they read (per output row its two source rows, columns 2q-1..2q+2, clamped: 12 loads for 8
+// outputs instead of 32, and no per-element index decode).  Each output takes resize_axis' indices and weights and the same
+// bilerp, so the result is bitwise the per-element kernel's.
+// the 4 taps of row `row` that output columns 4q..4q+3 read: column 2q-1 (clamped), 2q, 2q+1, 2q+2
+// (clamped); (t[0], t[1]) / (t[1], t[2]) / (t[1], t[2]) / (t[2], t[3]) are resize_axis' (x0, x1)
+// for the four columns, except at q = 0 where column 0 reads (x0, x1) = (0, 1) = (t[0], t[2])
+__device__ __forceinline__ void up2_row(const float* row, int q, int W, float t[4]) {
+  const float2 m = *reinterpret_cast<const float2*>(row + 2 * q);
+  t[0] = row[q > 0 ? 2 * q - 1 : 0];
+  t[1] = m.x;
+  t[2] = m.y;
+  t[3] = row[2 * q + 2 < W ? 2 * q + 2 : W - 1];
+}
+__device__ __forceinline__ void resize_up2_plane(const float* __restrict__ x, float* __restrict__ out, int nc, int C,
+                                                 int H, int W, int r, int q, const float* chscale, int binarize,
+                                                 long out_bs, const float* __restrict__ addend) {
+  const int n = nc / C, c = nc - n * C;
+  const float* p = x + (long)nc * H * W;
+  float lx[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    int x0, x1;
+    resize_axis(4 * q + b, W, 0.5f, x0, x1, lx[b]);
+  }
+  const float cs = chscale ? chscale[c] : 1.f;
+  const int Wo = 2 * W;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int oy = 2 * r + a;
+    int y0, y1;
+    float ly;
+    resize_axis(oy, H, 0.5f, y0, y1, ly);
+    float t0[4], t1[4];
+    up2_row(p + (long)y0 * W, q, W, t0);
+    up2_row(p + (long)y1 * W, q, W, t1);
+    // second tap of output column 4q: column 2q, or column 1 at q = 0
+    const float t0b = q > 0 ? t0[1] : t0[2], t1b = q > 0 ? t1[1] : t1[2];
+    float o4[4];
+    o4[0] = bilerp(t0[0], t0b, t1[0], t1b, lx[0], ly);
+    o4[1] = bilerp(t0[1], t0[2], t1[1], t1[2], lx[1], ly);
+    o4[2] = bilerp(t0[1], t0[2], t1[1], t1[2], lx[2], ly);
+    o4[3] = bilerp(t0[2], t0[3], t1[2], t1[3], lx[3], ly);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (chscale) o4[b] *= cs;
+      if (binarize) o4[b] = o4[b] > 0.f ? 1.f : 0.f;
+    }
+    const long o = (long)n * out_bs + (long)c * (2 * H) * Wo + (long)oy * Wo + 4 * q;
+    if (addend) {
+      const float4 d = *reinterpret_cast<const float4*>(addend + o);
+      o4[0] += d.x, o4[1] += d.y, o4[2] += d.z, o4[3] += d.w;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) __builtin_nontemporal_store(o4[b], out + o + b);
+  }
+}
+
+__global__ __launch_bounds__(256) void resize_up2_kernel(const float* __restrict__ x, float* __restrict__ out, int C,
+                                                         int H, int W, const float* chscale, int binarize,
+                                                         long out_bs, const float* __restrict__ addend) {
+  // the plane's (row r, quad q) pairs in row-major order: a block writes whole output row pairs.
+  // Consecutive blocks land on different XCDs (round robin): when the plane's block count allows, the
+  // blocks of one XCD take one contiguous run of rows so that the rows a block shares with its
+  // neighbours (r - 1, r + 1) hit that XCD's L2
+  const int gx = gridDim.x, bx = (gx & 7) == 0 ? (blockIdx.x & 7) * (gx >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int i = bx * 256 + threadIdx.x, Wq2 = W >> 1;
+  if (i >= H * Wq2) return;
+  const int r = i / Wq2, q = i - r * Wq2;
+  resize_up2_plane(x, out, blockIdx.y, C, H, W, r, q, chscale, binarize, out_bs, addend);
 }
 
 // weight with which input index i enters output index d along one axis (0 if it does not)
@@ -813,6 +891,12 @@ int vst_resize_bilinear_scaled(const float* x, float* out, long NC, int C, int H
   VST_CHECK_ARG(scale_y > 0.f && scale_x > 0.f);
   long total = NC * Ho * Wo;
   if (out_bs <= 0) out_bs = (long)C * Ho * Wo;
+  if (NC <= 65535 && Ho == 2 * H && Wo == 2 * W && scale_y == 0.5f && scale_x == 0.5f && W % 2 == 0 &&
+      (long)H * W < (1L << 31) && out_bs % 4 == 0 && ((uintptr_t)x & 7) == 0 && (((uintptr_t)out | (uintptr_t)addend) & 15) == 0) {
+    const dim3 g((unsigned)ceil_div((long)H * (W / 2), 256), (unsigned)NC);
+    resize_up2_kernel<<<g, 256, 0, (hipStream_t)stream>>>(x, out, C, H, W, chscale, binarize, out_bs, addend);
+    return vst_launch_status();
+  }
   if (NC <= 65535 && Ho <= 4 * 65535) {
     const dim3 g((unsigned)ceil_div(Wo, 64), (unsigned)ceil_div(Ho, 4), (unsigned)NC);
     resize_plane_kernel<<<g, dim3(64, 4), 0, (hipStream_t)stream>>>(x, out, C, H, W, Ho, Wo, scale_y, scale_x, chscale,
