@@ -85,3 +85,20 @@ for C, H, W, Ho, Wo in cases[:4]:
     us = e0.elapsed_time(e1) * 1000 / 20
     nbytes = 4.0 * B * C * (Ho * Wo + H * W)
     print(f"torch C={C:4d} {H}x{W} -> {Ho}x{Wo}: {us:8.1f} us  {nbytes / us / 1e6:6.2f} TB/s", flush=True)
+
+# the x2 upsample's adjoint (with the fused ReLU mask, as the decoder calls it)
+for C, H, W, Ho, Wo in cases[:4]:
+    x = torch.randn(B, C, H, W, device=dev)
+    gout = torch.randn(B, C, Ho, Wo, device=dev)
+    for _ in range(3):
+        ops.upsample2x_bwd(gout, x, relu_mask=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        ops.upsample2x_bwd(gout, x, relu_mask=True)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / 20
+    nbytes = 4.0 * B * C * (Ho * Wo + 2 * H * W)
+    print(f"up2 bwd C={C:4d} {H}x{W} <- {Ho}x{Wo}: {us:8.1f} us  {nbytes / us / 1e6:6.2f} TB/s", flush=True)
