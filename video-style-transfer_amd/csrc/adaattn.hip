@@ -808,7 +808,14 @@ __global__ void channel_dot_kernel(const float* __restrict__ x, const float* __r
     const float* xp = x + (long)n * C * P + p;
     const float* yp = y ? y + (long)n * C * P + p : nullptr;
     const float* vp = v ? v + (long)n * C : nullptr;
-    for (int c = grp; c < C; c += 4) s += (double)xp[(long)c * P] * (vp ? vp[c] : yp[(long)c * P]);
+    // (the same summation order either way; unrolled so that eight channels' loads are in flight)
+    if (vp) {
+#pragma unroll 8
+      for (int c = grp; c < C; c += 4) s += (double)xp[(long)c * P] * vp[c];
+    } else {
+#pragma unroll 8
+      for (int c = grp; c < C; c += 4) s += (double)xp[(long)c * P] * yp[(long)c * P];
+    }
   }
   part[grp][lane] = s;
   __syncthreads();
