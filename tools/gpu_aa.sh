@@ -14,4 +14,4 @@ VST_WGRAD_SIDE=0 VST_CONTENT_SIDE=0 timeout -k 10 300 rocprofv3 --kernel-trace -
   python3 bench.py --model adaattn --batch 8 --height 512 --width 1024 --steps 5 --warmup 2 --prof-steps 0 --no-cpu-baseline --no-vgg19 > gpurun_out/${T}_prof5.log 2>&1 || exit 11
 python tools/prof_summary.py gpurun_out/${T}_prof5 7 > gpurun_out/${T}_c5_kernel_summary.txt 2>&1
 rm -rf gpurun_out/${T}_prof5
-grep -E "total|resize|up2|channel_dot" gpurun_out/${T}_c5_kernel_summary.txt
+grep -E "total|resize|up2|channel_dot|channel_norm|plane_|simloss" gpurun_out/${T}_c5_kernel_summary.txt

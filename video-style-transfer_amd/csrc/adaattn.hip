@@ -106,6 +106,7 @@ __global__ void channel_norm_kernel(const float* __restrict__ x, float* __restri
   if (p < P) {
     const float* xp = x + (long)n * C * P + p;
     int c = grp;
+#pragma unroll 4
     for (; c + 4 < C; c += 8) {
       const float a = xp[(long)c * P], b = xp[(long)(c + 4) * P];
       s0 += a * a;
@@ -347,9 +348,11 @@ __global__ void plane_meanstd_kernel(const float* __restrict__ x, float* __restr
   const long plane = blockIdx.x;
   const float* xp = x + plane * HW;
   double s = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < HW; i += RT) s += xp[i];
   const double mu = block_sum_d(s, sh) / HW;
   double q = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < HW; i += RT) {
     double d = xp[i] - mu;
     q += d * d;
@@ -370,6 +373,7 @@ __global__ void plane_meanstd_bwd_kernel(const float* __restrict__ x, const floa
   const float b = (gstd && sd > 0.f) ? gstd[plane] / ((HW - 1) * sd) : 0.f;
   const float* xp = x + plane * HW;
   float* gp = gx + plane * HW;
+#pragma unroll 8
   for (int i = threadIdx.x; i < HW; i += RT) gp[i] = a + b * (xp[i] - mu);
 }
 
@@ -490,6 +494,7 @@ __global__ void plane_norm_grad_kernel(float* __restrict__ x, const float* __res
                                        const float* __restrict__ nrm, const float* __restrict__ y, int HW) {
   const long plane = blockIdx.x;
   const float k = nrm[plane] > 0.f ? s[plane] / nrm[plane] : 0.f;
+#pragma unroll 8
   for (int i = threadIdx.x; i < HW; i += RT) x[plane * HW + i] += k * y[plane * HW + i];
 }
 
@@ -776,6 +781,7 @@ __global__ __launch_bounds__(RT) void plane_dot_vec_kernel(const float4* __restr
   const float4* wp = w ? w + (long)(plane / C) * P4 : nullptr;
   double acc = 0.0;
   int i = threadIdx.x;
+#pragma unroll 4
   for (; i + RT < P4; i += 2 * RT) {
     float4 a = xp[i], b = xp[i + RT];
     if (wp) {
@@ -873,6 +879,7 @@ __global__ void attn_dkn_kernel(const float* __restrict__ K, const float* __rest
     const float* kp = K + (long)n * d * Ns + j;
     const float* yp = Y + (long)n * d * Ns + j;
     const float* qp = qt + (long)n * d;
+#pragma unroll 8
     for (int c = grp; c < d; c += 4) s += (double)kp[(long)c * Ns] * ((double)yp[(long)c * Ns] - qp[c]);
   }
   part[grp][lane] = s;

@@ -474,6 +474,7 @@ __global__ __launch_bounds__(NTN) void plane_sum_vec_kernel(const float4* __rest
   const float4* xp = x + (long)blockIdx.x * HW4;
   double s = 0.0;
   int i = threadIdx.x;
+#pragma unroll 4
   for (; i + NTN < HW4; i += 2 * NTN) {
     const float4 a = xp[i], b = xp[i + NTN];
     s += (((double)a.x + a.y) + ((double)a.z + a.w)) + (((double)b.x + b.y) + ((double)b.z + b.w));
