@@ -14,6 +14,6 @@ VST_WGRAD_SIDE=0 VST_CONTENT_SIDE=0 timeout -k 10 300 rocprofv3 --kernel-trace -
   python3 bench.py --steps 10 --warmup 2 --prof-steps 0 --no-cpu-baseline --no-vgg19 > gpurun_out/${T}_prof3.log 2>&1 || exit 10
 python tools/prof_summary.py gpurun_out/${T}_prof3 12 -shapes > gpurun_out/${T}_c3_kernel_summary.txt 2>&1
 rm -rf gpurun_out/${T}_prof3
-head -12 gpurun_out/${T}_c3_kernel_summary.txt
+head -3 gpurun_out/${T}_c3_kernel_summary.txt; grep -E "in_fwd|in_bwd" gpurun_out/${T}_c3_kernel_summary.txt
 timeout -k 10 600 python bench.py --model adaattn --batch 8 --height 512 --width 1024 --steps 20 --prof-steps 0 --no-cpu-baseline --no-vgg19 > gpurun_out/${T}_aa5.json 2> gpurun_out/${T}_aa5.err || exit 9
 python tools/show_bench.py gpurun_out/${T}_aa5.json | head -1
