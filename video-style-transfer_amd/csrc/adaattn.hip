@@ -400,6 +400,7 @@ __global__ void simloss_colsum_kernel(const float* __restrict__ Gc, const float*
   const long o = (long)n * C * C;
   const float vc = vnc[n * C + j], vs = vns[n * C + j];
   double a = 0.0, b = 0.0;
+#pragma unroll 8
   for (int i = 0; i < C; ++i) {
     a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vc + 1e-6f);
     b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vs + 1e-6f);
