@@ -390,23 +390,33 @@ __global__ void plane_norm_kernel(const float* __restrict__ x, float* __restrict
 
 // image_similarity_loss core (AA/lossfn.py:25-53), both cosine distances:
 //   D = 1 - G / (un_i vn_j + 1e-6);  Dn = D / colsum_j(D);  loss_n = sum |Dn_c - Dn_cs| / hw
-// pass 1: column sums (grid ceil(C/RT) x N, coalesced over j)
-__global__ void simloss_colsum_kernel(const float* __restrict__ Gc, const float* __restrict__ unc,
-                                      const float* __restrict__ vnc, const float* __restrict__ Gs,
-                                      const float* __restrict__ uns, const float* __restrict__ vns,
-                                      float* __restrict__ colc, float* __restrict__ cols, int C) {
-  const int n = blockIdx.y, j = blockIdx.x * RT + threadIdx.x;
-  if (j >= C) return;
-  const long o = (long)n * C * C;
-  const float vc = vnc[n * C + j], vs = vns[n * C + j];
+// pass 1: column sums.  Block = 64 consecutive columns x 4 row quarters (rows i = grp, grp+4, ...),
+// coalesced 256-B row reads, the quarters combined in a fixed order through LDS (grid ceil(C/64) x N:
+// a column per thread over all C rows left most of the chip idle at C = 4096)
+__global__ __launch_bounds__(256) void simloss_colsum_kernel(const float* __restrict__ Gc, const float* __restrict__ unc,
+                                                             const float* __restrict__ vnc, const float* __restrict__ Gs,
+                                                             const float* __restrict__ uns, const float* __restrict__ vns,
+                                                             float* __restrict__ colc, float* __restrict__ cols, int C) {
+  __shared__ double pa[4][64], pb[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int n = blockIdx.y, j = blockIdx.x * 64 + lane;
   double a = 0.0, b = 0.0;
+  if (j < C) {
+    const long o = (long)n * C * C;
+    const float vc = vnc[n * C + j], vs = vns[n * C + j];
 #pragma unroll 8
-  for (int i = 0; i < C; ++i) {
-    a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vc + 1e-6f);
-    b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vs + 1e-6f);
+    for (int i = grp; i < C; i += 4) {
+      a += 1.0f - Gc[o + (long)i * C + j] / (unc[n * C + i] * vc + 1e-6f);
+      b += 1.0f - Gs[o + (long)i * C + j] / (uns[n * C + i] * vs + 1e-6f);
+    }
   }
-  colc[n * C + j] = (float)a;
-  cols[n * C + j] = (float)b;
+  pa[grp][lane] = a;
+  pb[grp][lane] = b;
+  __syncthreads();
+  if (grp == 0 && j < C) {
+    colc[n * C + j] = (float)(((pa[0][lane] + pa[1][lane]) + pa[2][lane]) + pa[3][lane]);
+    cols[n * C + j] = (float)(((pb[0][lane] + pb[1][lane]) + pb[2][lane]) + pb[3][lane]);
+  }
 }
 
 // pass 2: one block per row (i, n): rowpart[n][i] = sum_j |Dn_c - Dn_cs| / hw
@@ -636,7 +646,7 @@ int vst_simloss(const float* Gc, const float* unc, const float* vnc, const float
                 const float* vns, float* colc, float* cols, float* partial, int N, int C, int HW, void* stream) {
   VST_CHECK_ARG(Gc && unc && vnc && Gs && uns && vns && colc && cols && partial && N > 0 && C > 0 && HW > 0);
   hipStream_t st = (hipStream_t)stream;
-  simloss_colsum_kernel<<<dim3(ceil_div(C, RT), N), RT, 0, st>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, C);
+  simloss_colsum_kernel<<<dim3(ceil_div(C, 64), N), 256, 0, st>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, C);
   simloss_rows_kernel<<<dim3(C, N), RT, 0, st>>>(Gc, unc, vnc, Gs, uns, vns, colc, cols, partial, C, 1.0f / HW);
   return vst_launch_status();
 }
